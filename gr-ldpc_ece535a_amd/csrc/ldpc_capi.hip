@@ -1,0 +1,488 @@
+// ldpc_capi.hip -- the C ABI of include/ldpc_hip.h (libldpc_hip.so).
+//
+// Host side of the drop-in boundary: H ingestion (the constructor's matrix
+// + reorderHMatrix, lib/ldpc_decoder_cb_impl.cc:60-106), the device edge
+// tables, staging buffers and kernel dispatch.  Every decode runs on the GPU;
+// when no device is usable ldpc_create fails with LDPC_EDEVICE.
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/ldpc_hip.h"
+#include "ldpc_kernels.hpp"
+
+using ldpc::ColRec;
+using ldpc::EdgeRec;
+using ldpc::kNone;
+
+struct ldpc_ctx {
+  int M = 0, N = 0, E = 0, K = 0, KB = 0, dc_max = 0, dv_max = 0;
+  int slots = 0, nw = 0, rs = 0;
+  int device = 0;
+  std::vector<uint8_t> H;  // the decoder's (reordered) H
+  hipStream_t stream = nullptr;
+  EdgeRec *d_edges = nullptr;
+  ColRec *d_cols = nullptr;
+  uint64_t *d_rowmask = nullptr;
+  void *d_stage = nullptr;
+  size_t stage_bytes = 0;
+  std::string err;
+};
+
+namespace {
+
+thread_local std::string g_create_error;
+
+// The reference decoder's H, lib/ldpc_decoder_cb_impl.cc:63-96 (32 x 64),
+// one 64-bit word per row, bit c = column c.
+const uint64_t kDefaultH[32] = {
+    0x0000504000000140ull, 0x0000024080100020ull, 0x0020000141004000ull,
+    0x000a008000000220ull, 0x0000080400848000ull, 0x0008000401000090ull,
+    0x4100400204000000ull, 0x0010301000000001ull, 0x00024c0000000008ull,
+    0x9500006000000000ull, 0x0101200080000400ull, 0x1040000000002004ull,
+    0x3080080002000002ull, 0x0200800008010010ull, 0x0410018008040000ull,
+    0x0000001200005020ull, 0x0080000040802200ull, 0x0020008010480000ull,
+    0x0400001000018088ull, 0x2002020000200004ull, 0x0000000300080300ull,
+    0xc200000000240080ull, 0x02000000e4000000ull, 0x0800000000301002ull,
+    0x2000040008402040ull, 0x8800010400080000ull, 0x0070000000800000ull,
+    0x4040010800000840ull, 0x000c02000000c800ull, 0x0000002811000008ull,
+    0x0884000010000401ull, 0x0000900902020000ull,
+};
+
+int set_err(ldpc_ctx *ctx, int code, const std::string &msg) {
+  if (ctx)
+    ctx->err = msg;
+  else
+    g_create_error = msg;
+  return code;
+}
+
+int hip_err(ldpc_ctx *ctx, hipError_t e, const char *what) {
+  return set_err(ctx, LDPC_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// reorderHMatrix, lib/ldpc_decoder_cb_impl.cc:255-307 ('First' strategy):
+// for each row i pick the first column j >= i with F(i,j) != 0 (column 0 if
+// none), swap columns i and j of F and H, and clear column i below row i
+// with GF(2) row additions.  lower/upper (M x (N-M), optional) receive the
+// factors the encoder solves with (lib/ldpc_encoder_bc_impl.cc:259-260).
+void reorder_columns(uint8_t *H, int M, int N, int32_t *chosen,
+                     std::vector<uint8_t> *lower, std::vector<uint8_t> *upper) {
+  std::vector<uint8_t> F(H, H + (size_t)M * N);
+  const int K = N - M;
+  if (lower) lower->assign((size_t)M * std::max(K, 0), 0);
+  if (upper) upper->assign((size_t)M * std::max(K, 0), 0);
+  for (int i = 0; i < M; ++i) {
+    int pick = 0;
+    for (int j = i; j < N; ++j)
+      if (F[(size_t)i * N + j]) {
+        pick = j;
+        break;
+      }
+    if (chosen) chosen[i] = pick;
+    if (pick != i)
+      for (int r = 0; r < M; ++r) {
+        std::swap(F[(size_t)r * N + i], F[(size_t)r * N + pick]);
+        std::swap(H[(size_t)r * N + i], H[(size_t)r * N + pick]);
+      }
+    if (i < K) {
+      if (lower)
+        for (int r = i; r < M; ++r) (*lower)[(size_t)r * K + i] = F[(size_t)r * N + i];
+      if (upper)
+        for (int r = 0; r <= i; ++r) (*upper)[(size_t)r * K + i] = F[(size_t)r * N + i];
+    }
+    for (int k = i + 1; k < M; ++k)
+      if (F[(size_t)k * N + i])
+        for (int c = 0; c < N; ++c) F[(size_t)k * N + c] ^= F[(size_t)i * N + c];
+  }
+}
+
+bool valid_h(const uint8_t *H, int M, int N) {
+  if (!H || M <= 0 || N <= 0 || M >= N) return false;
+  for (size_t t = 0; t < (size_t)M * N; ++t)
+    if (H[t] > 1) return false;
+  return true;
+}
+
+// Edge / column / row tables of the decoder's H (see ldpc_kernels.hpp).
+int build_tables(ldpc_ctx *ctx, std::vector<EdgeRec> &edges, std::vector<ColRec> &cols,
+                 std::vector<uint64_t> &rowmask) {
+  const int M = ctx->M, N = ctx->N;
+  const uint8_t *H = ctx->H.data();
+  std::vector<std::vector<int>> row_edges(M), col_edges(N);
+  std::vector<int> erow, ecol;
+  for (int j = 0; j < M; ++j)
+    for (int i = 0; i < N; ++i)
+      if (H[(size_t)j * N + i]) {
+        const int e = (int)erow.size();
+        erow.push_back(j);
+        ecol.push_back(i);
+        row_edges[j].push_back(e);
+        col_edges[i].push_back(e);  // rows ascend because j ascends
+      }
+  ctx->E = (int)erow.size();
+  ctx->dc_max = 0;
+  ctx->dv_max = 0;
+  for (auto &r : row_edges) ctx->dc_max = std::max(ctx->dc_max, (int)r.size());
+  for (auto &c : col_edges) ctx->dv_max = std::max(ctx->dv_max, (int)c.size());
+  if (ctx->E == 0) return set_err(ctx, LDPC_EINVAL, "H has no ones");
+  if (N > ldpc::kNMax || M > ldpc::kMMax || ctx->E > 64 * ldpc::kSlotsMax ||
+      ctx->dc_max > ldpc::kDcMax || ctx->dv_max > ldpc::kDvMax) {
+    char buf[256];
+    snprintf(buf, sizeof buf,
+             "code shape outside the small-code kernel (M=%d N=%d E=%d dc_max=%d dv_max=%d; "
+             "limits M,N<=%d E<=%d dc<=%d dv<=%d)",
+             M, N, ctx->E, ctx->dc_max, ctx->dv_max, ldpc::kNMax, 64 * ldpc::kSlotsMax,
+             ldpc::kDcMax, ldpc::kDvMax);
+    return set_err(ctx, LDPC_EUNSUPPORTED, buf);
+  }
+  ctx->slots = (ctx->E + 63) / 64;
+  ctx->nw = N <= 64 ? 1 : 4;
+  ctx->rs = (M + 63) / 64;
+  ctx->K = N - M;
+  ctx->KB = (ctx->K + 7) / 8;
+
+  edges.assign((size_t)64 * ctx->slots, EdgeRec{});
+  for (auto &r : edges) {
+    r.col = kNone;
+    r.row = kNone;
+    std::fill(std::begin(r.rn), std::end(r.rn), kNone);
+    std::fill(std::begin(r.cn), std::end(r.cn), kNone);
+  }
+  for (int e = 0; e < ctx->E; ++e) {
+    EdgeRec &r = edges[e];
+    r.col = (uint16_t)ecol[e];
+    r.row = (uint16_t)erow[e];
+    int k = 0;
+    for (int n : row_edges[erow[e]])
+      if (n != e) r.rn[k++] = (uint16_t)n;  // ascending column
+    k = 0;
+    for (int n : col_edges[ecol[e]])
+      if (n != e) r.cn[k++] = (uint16_t)n;  // ascending row
+  }
+  cols.assign((size_t)64 * ctx->nw, ColRec{});
+  for (auto &c : cols) {
+    std::fill(std::begin(c.e), std::end(c.e), kNone);
+    std::fill(std::begin(c.r), std::end(c.r), kNone);
+  }
+  for (int i = 0; i < N; ++i)
+    for (size_t k = 0; k < col_edges[i].size(); ++k) {
+      cols[i].e[k] = (uint16_t)col_edges[i][k];
+      cols[i].r[k] = (uint16_t)erow[col_edges[i][k]];
+    }
+  rowmask.assign((size_t)M * ctx->nw, 0);
+  for (int j = 0; j < M; ++j)
+    for (int i = 0; i < N; ++i)
+      if (H[(size_t)j * N + i]) rowmask[(size_t)j * ctx->nw + i / 64] |= 1ull << (i % 64);
+  return LDPC_OK;
+}
+
+int ensure_stage(ldpc_ctx *ctx, size_t bytes) {
+  if (bytes <= ctx->stage_bytes) return LDPC_OK;
+  if (ctx->d_stage) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->d_stage);
+    ctx->d_stage = nullptr;
+    ctx->stage_bytes = 0;
+  }
+  size_t want = std::max(bytes, (size_t)1 << 20);
+  hipError_t e = hipMalloc(&ctx->d_stage, want);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(staging)");
+  ctx->stage_bytes = want;
+  return LDPC_OK;
+}
+
+int check_decode_args(ldpc_ctx *ctx, int &method, int max_iters, int et_period, int precision,
+                      int B, int elem_stride, int64_t cw_stride) {
+  if (!ctx) return LDPC_EINVAL;
+  if (method < 0 || method > 3) method = 0;  // general_work :162-164
+  if (B < 0) return set_err(ctx, LDPC_EINVAL, "B < 0");
+  if ((method == 0 || method == 1) && max_iters < 1)
+    return set_err(ctx, LDPC_EINVAL, "max_iters must be >= 1 for min-sum / sum-product");
+  if (method == 2 && max_iters < 0) return set_err(ctx, LDPC_EINVAL, "max_iters < 0");
+  if (et_period < 1) return set_err(ctx, LDPC_EINVAL, "et_period must be >= 1");
+  if (precision != LDPC_PREC_F64 && precision != LDPC_PREC_F32)
+    return set_err(ctx, LDPC_EINVAL, "precision must be LDPC_PREC_F64 or LDPC_PREC_F32");
+  if (elem_stride < 1 || cw_stride < 0) return set_err(ctx, LDPC_EINVAL, "bad strides");
+  return LDPC_OK;
+}
+
+ldpc::CodeView code_view(const ldpc_ctx *ctx) {
+  ldpc::CodeView v;
+  v.edges = ctx->d_edges;
+  v.cols = ctx->d_cols;
+  v.rowmask = ctx->d_rowmask;
+  v.M = ctx->M;
+  v.N = ctx->N;
+  v.E = ctx->E;
+  v.KB = ctx->KB;
+  v.rs = ctx->rs;
+  return v;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ldpc_default_h(uint8_t *H_out) {
+  if (!H_out) return LDPC_EINVAL;
+  for (int j = 0; j < 32; ++j)
+    for (int i = 0; i < 64; ++i) H_out[j * 64 + i] = (uint8_t)((kDefaultH[j] >> i) & 1);
+  return LDPC_OK;
+}
+
+int ldpc_reorder_h(uint8_t *H, int M, int N, int32_t *chosen_opt) {
+  if (!valid_h(H, M, N)) return LDPC_EINVAL;
+  reorder_columns(H, M, N, chosen_opt, nullptr, nullptr);
+  return LDPC_OK;
+}
+
+int ldpc_check_frame(const uint8_t *H, int M, int N, const uint8_t *bits, int threshold) {
+  if (!valid_h(H, M, N) || !bits) return LDPC_EINVAL;
+  int unsatisfied = 0;
+  for (int k = 0; k < M; ++k) {
+    int parity = 0;
+    for (int j = 0; j < N; ++j) parity ^= (H[(size_t)k * N + j] & (bits[j] & 1));
+    if (parity) ++unsatisfied;
+    if (unsatisfied > threshold) break;
+  }
+  return unsatisfied;
+}
+
+// makeParityCheck (lib/ldpc_encoder_bc_impl.cc:275-294) over GF(2): the
+// reference's two real-valued dgesv solves on the unit-triangular 0/1
+// factors are exact integer substitutions, which reduce mod 2 to the
+// substitutions below.  The factors come from re-running the reorder on the
+// (already reordered) H, which then moves no column.
+int ldpc_encode(const uint8_t *Hr, int M, int N, const uint8_t *data_bits, int B,
+                uint8_t *codewords_out) {
+  if (!valid_h(Hr, M, N) || N != 2 * M || B < 0 || (B > 0 && (!data_bits || !codewords_out)))
+    return LDPC_EINVAL;
+  std::vector<uint8_t> H(Hr, Hr + (size_t)M * N), L, U;
+  std::vector<int32_t> chosen(M);
+  reorder_columns(H.data(), M, N, chosen.data(), &L, &U);
+  for (int i = 0; i < M; ++i)
+    if (chosen[i] != i) return LDPC_EINVAL;  // not the reordered form
+  const int K = N - M;
+  for (int i = 0; i < M; ++i)
+    if (!L[(size_t)i * K + i] || !U[(size_t)i * K + i]) return LDPC_ESINGULAR;
+  std::vector<uint8_t> z(M), x(M);
+  for (int b = 0; b < B; ++b) {
+    const uint8_t *d = data_bits + (size_t)b * K;
+    uint8_t *cw = codewords_out + (size_t)b * N;
+    for (int i = 0; i < M; ++i) {
+      int acc = 0;
+      for (int j = 0; j < K; ++j) acc ^= Hr[(size_t)i * N + M + j] & (d[j] & 1);
+      z[i] = (uint8_t)acc;
+    }
+    for (int i = 0; i < M; ++i) {  // L x = z
+      int acc = z[i];
+      for (int j = 0; j < i; ++j) acc ^= L[(size_t)i * K + j] & x[j];
+      x[i] = (uint8_t)acc;
+    }
+    for (int i = M - 1; i >= 0; --i) {  // U c = x
+      int acc = x[i];
+      for (int j = i + 1; j < M; ++j) acc ^= U[(size_t)i * K + j] & cw[j];
+      cw[i] = (uint8_t)acc;
+    }
+    for (int j = 0; j < K; ++j) cw[M + j] = d[j] & 1;
+  }
+  return LDPC_OK;
+}
+
+ldpc_ctx *ldpc_create(const uint8_t *H, int M, int N, int flags, int device) {
+  g_create_error.clear();
+  if (!valid_h(H, M, N)) {
+    set_err(nullptr, LDPC_EINVAL, "H must be M x N (M < N) with 0/1 entries");
+    return nullptr;
+  }
+  ldpc_ctx *ctx = new ldpc_ctx();
+  ctx->M = M;
+  ctx->N = N;
+  ctx->device = device;
+  ctx->H.assign(H, H + (size_t)M * N);
+  if (!(flags & LDPC_FLAG_NO_REORDER)) reorder_columns(ctx->H.data(), M, N, nullptr, nullptr, nullptr);
+  std::vector<EdgeRec> edges;
+  std::vector<ColRec> cols;
+  std::vector<uint64_t> rowmask;
+  int rc = build_tables(ctx, edges, cols, rowmask);
+  if (rc != LDPC_OK) {
+    g_create_error = ctx->err;
+    delete ctx;
+    return nullptr;
+  }
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
+    g_create_error = std::string("no usable HIP device (") +
+                     (e != hipSuccess ? hipGetErrorString(e) : "device index out of range") +
+                     "); the decode path has no CPU fallback";
+    delete ctx;
+    return nullptr;
+  }
+  const char *what = nullptr;
+  if ((e = hipSetDevice(device)) != hipSuccess) what = "hipSetDevice";
+  if (!what && (e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
+    what = "hipStreamCreate";
+  if (!what && (e = hipMalloc(&ctx->d_edges, edges.size() * sizeof(EdgeRec))) != hipSuccess)
+    what = "hipMalloc(edges)";
+  if (!what && (e = hipMalloc(&ctx->d_cols, cols.size() * sizeof(ColRec))) != hipSuccess)
+    what = "hipMalloc(cols)";
+  if (!what && (e = hipMalloc(&ctx->d_rowmask, rowmask.size() * 8)) != hipSuccess)
+    what = "hipMalloc(rowmask)";
+  if (!what && (e = hipMemcpy(ctx->d_edges, edges.data(), edges.size() * sizeof(EdgeRec),
+                              hipMemcpyHostToDevice)) != hipSuccess)
+    what = "hipMemcpy(edges)";
+  if (!what && (e = hipMemcpy(ctx->d_cols, cols.data(), cols.size() * sizeof(ColRec),
+                              hipMemcpyHostToDevice)) != hipSuccess)
+    what = "hipMemcpy(cols)";
+  if (!what && (e = hipMemcpy(ctx->d_rowmask, rowmask.data(), rowmask.size() * 8,
+                              hipMemcpyHostToDevice)) != hipSuccess)
+    what = "hipMemcpy(rowmask)";
+  if (what) {
+    g_create_error = std::string(what) + ": " + hipGetErrorString(e);
+    ldpc_destroy(ctx);
+    return nullptr;
+  }
+  return ctx;
+}
+
+void ldpc_destroy(ldpc_ctx *ctx) {
+  if (!ctx) return;
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->d_edges) (void)hipFree(ctx->d_edges);
+  if (ctx->d_cols) (void)hipFree(ctx->d_cols);
+  if (ctx->d_rowmask) (void)hipFree(ctx->d_rowmask);
+  if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char *ldpc_last_error(const ldpc_ctx *ctx) {
+  return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}
+
+int ldpc_ctx_info(const ldpc_ctx *ctx, int *M, int *N, int *E, int *K, int *KB, int *dc_max,
+                  int *dv_max) {
+  if (!ctx) return LDPC_EINVAL;
+  if (M) *M = ctx->M;
+  if (N) *N = ctx->N;
+  if (E) *E = ctx->E;
+  if (K) *K = ctx->K;
+  if (KB) *KB = ctx->KB;
+  if (dc_max) *dc_max = ctx->dc_max;
+  if (dv_max) *dv_max = ctx->dv_max;
+  return LDPC_OK;
+}
+
+int ldpc_ctx_h(const ldpc_ctx *ctx, uint8_t *H_out) {
+  if (!ctx || !H_out) return LDPC_EINVAL;
+  memcpy(H_out, ctx->H.data(), ctx->H.size());
+  return LDPC_OK;
+}
+
+int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+                       const float *d_in, int64_t cw_stride, int elem_stride, float polarity,
+                       int B, uint8_t *d_out_packed, uint8_t *d_out_bits_opt,
+                       int32_t *d_iters_used_opt, int32_t *d_syn_weight_opt,
+                       float *d_llr_out_opt, void *hip_stream) {
+  int rc = check_decode_args(ctx, method, max_iters, et_period, precision, B, elem_stride,
+                             cw_stride);
+  if (rc != LDPC_OK) return rc;
+  if (B == 0) return LDPC_OK;
+  if (!d_in || !d_out_packed) return set_err(ctx, LDPC_EINVAL, "null device buffer");
+  ldpc::DecodeArgs a;
+  a.in = d_in;
+  a.cw_stride = cw_stride;
+  a.elem_stride = elem_stride;
+  a.polarity = polarity;
+  a.B = B;
+  a.max_iters = max_iters;
+  a.et_period = et_period;
+  a.packed = d_out_packed;
+  a.bits = d_out_bits_opt;
+  a.iters = d_iters_used_opt;
+  a.synd = d_syn_weight_opt;
+  a.llr = d_llr_out_opt;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  void *st = hip_stream ? hip_stream : (void *)ctx->stream;
+  rc = ldpc::launch_decode(code_view(ctx), a, method, precision, ctx->slots, ctx->nw, st);
+  if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no kernel for this code shape");
+  if (rc != 0) return hip_err(ctx, hipGetLastError(), "kernel launch");
+  return LDPC_OK;
+}
+
+int ldpc_decode_strided(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+                        const float *in, int64_t n_in_floats, int64_t cw_stride, int elem_stride,
+                        float polarity, int B, uint8_t *out_packed, uint8_t *out_bits_opt,
+                        int32_t *iters_used_opt, int32_t *syn_weight_opt, float *llr_out_opt) {
+  int rc = check_decode_args(ctx, method, max_iters, et_period, precision, B, elem_stride,
+                             cw_stride);
+  if (rc != LDPC_OK) return rc;
+  if (B == 0) return LDPC_OK;
+  if (!in || !out_packed) return set_err(ctx, LDPC_EINVAL, "null buffer");
+  const int64_t span = (int64_t)(B - 1) * cw_stride + (int64_t)(ctx->N - 1) * elem_stride + 1;
+  if (span > n_in_floats) return set_err(ctx, LDPC_EINVAL, "input shorter than the frames read");
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t b_in = al((size_t)span * 4), b_pk = al((size_t)B * ctx->KB),
+               b_bits = out_bits_opt ? al((size_t)B * ctx->N) : 0,
+               b_it = iters_used_opt ? al((size_t)B * 4) : 0,
+               b_sy = syn_weight_opt ? al((size_t)B * 4) : 0,
+               b_llr = llr_out_opt ? al((size_t)B * ctx->N * 4) : 0;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  rc = ensure_stage(ctx, b_in + b_pk + b_bits + b_it + b_sy + b_llr);
+  if (rc != LDPC_OK) return rc;
+  char *base = (char *)ctx->d_stage;
+  float *d_in = (float *)base;
+  uint8_t *d_pk = (uint8_t *)(base + b_in);
+  uint8_t *d_bits = out_bits_opt ? (uint8_t *)(base + b_in + b_pk) : nullptr;
+  int32_t *d_it = iters_used_opt ? (int32_t *)(base + b_in + b_pk + b_bits) : nullptr;
+  int32_t *d_sy = syn_weight_opt ? (int32_t *)(base + b_in + b_pk + b_bits + b_it) : nullptr;
+  float *d_llr = llr_out_opt ? (float *)(base + b_in + b_pk + b_bits + b_it + b_sy) : nullptr;
+  if ((e = hipMemcpyAsync(d_in, in, (size_t)span * 4, hipMemcpyHostToDevice, ctx->stream)) !=
+      hipSuccess)
+    return hip_err(ctx, e, "hipMemcpyAsync(in)");
+  rc = ldpc_decode_device(ctx, method, max_iters, et_period, precision, d_in, cw_stride,
+                          elem_stride, polarity, B, d_pk, d_bits, d_it, d_sy, d_llr, ctx->stream);
+  if (rc != LDPC_OK) return rc;
+  struct {
+    void *dst;
+    const void *src;
+    size_t n;
+  } back[] = {{out_packed, d_pk, (size_t)B * ctx->KB},
+              {out_bits_opt, d_bits, (size_t)B * ctx->N},
+              {iters_used_opt, d_it, (size_t)B * 4},
+              {syn_weight_opt, d_sy, (size_t)B * 4},
+              {llr_out_opt, d_llr, (size_t)B * ctx->N * 4}};
+  for (auto &c : back)
+    if (c.dst && (e = hipMemcpyAsync(c.dst, c.src, c.n, hipMemcpyDeviceToHost, ctx->stream)) !=
+                     hipSuccess)
+      return hip_err(ctx, e, "hipMemcpyAsync(out)");
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipStreamSynchronize");
+  return LDPC_OK;
+}
+
+int ldpc_decode(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+                const float *llr_re, int B, uint8_t *out_packed, uint8_t *out_bits_opt,
+                int32_t *iters_used_opt, int32_t *syn_weight_opt) {
+  if (!ctx) return LDPC_EINVAL;
+  return ldpc_decode_strided(ctx, method, max_iters, et_period, precision, llr_re,
+                             (int64_t)B * ctx->N, ctx->N, 1, 1.0f, B, out_packed, out_bits_opt,
+                             iters_used_opt, syn_weight_opt, nullptr);
+}
+
+int ldpc_synchronize(ldpc_ctx *ctx) {
+  if (!ctx) return LDPC_EINVAL;
+  hipError_t e = hipStreamSynchronize(ctx->stream);
+  return e == hipSuccess ? LDPC_OK : hip_err(ctx, e, "hipStreamSynchronize");
+}
+
+}  // extern "C"

@@ -1,0 +1,69 @@
+// ldpc_kernels.hpp -- shared host/device types of the MI355X decode path.
+//
+// The decoder's view of H is held as per-edge / per-column records in HBM,
+// built once per context (ldpc_capi.hip) from the reordered dense H of
+// lib/ldpc_decoder_cb_impl.cc:98-106.  Edges are numbered in CSR order
+// (row-major, ascending column), which is the order the reference's dense
+// scans visit them.
+#pragma once
+
+#include <stdint.h>
+
+namespace ldpc {
+
+constexpr int kWavesPerBlock = 4;  // one frame (codeword) per 64-lane wave
+constexpr int kThreads = 64 * kWavesPerBlock;
+constexpr int kDcMax = 8;          // check-degree limit of the small-code kernel
+constexpr int kDvMax = 4;          // variable-degree limit
+constexpr int kSlotsMax = 8;       // edge slots per lane: E <= 512
+constexpr int kNMax = 256;         // 4 x 64-bit hard-decision words
+constexpr int kMMax = 256;         // 4 row slots per lane
+constexpr uint16_t kNone = 0xFFFF;
+
+// One edge (j, i) of H.  rn: the other edges of row j in ascending column
+// order -- the order of the product T *= tanh(M(j,k)/2) at :507-511 and of
+// the minimum scan at :363-369.  cn: the other edges of column i in
+// ascending row order -- the order of the sum at :544-548.
+struct EdgeRec {
+  uint16_t col;
+  uint16_t row;
+  uint16_t rn[kDcMax - 1];
+  uint16_t cn[kDvMax - 1];
+};  // 24 bytes
+
+// One column i: its edges and their rows in ascending row order (the sums
+// at :521-525 and :381-385, and the bit-flip vote at :457-461).
+struct ColRec {
+  uint16_t e[kDvMax];
+  uint16_t r[kDvMax];
+};  // 16 bytes
+
+struct CodeView {
+  const EdgeRec *edges;      // 64 * S records; records >= E have col == kNone
+  const ColRec *cols;        // 64 * NW records; records >= N are all kNone
+  const uint64_t *rowmask;   // M x NW words: bit c of row j <=> H(j, c) == 1
+  int M, N, E, KB, rs;       // rs = ceil(M / 64)
+};
+
+struct DecodeArgs {
+  const float *in;           // frame b, sample i: in[b*cw_stride + i*elem_stride]
+  int64_t cw_stride;
+  int elem_stride;
+  float polarity;
+  int B;
+  int max_iters;
+  int et_period;
+  uint8_t *packed;           // B x KB
+  uint8_t *bits;             // B x N   (optional)
+  int32_t *iters;            // B       (optional)
+  int32_t *synd;             // B       (optional)
+  float *llr;                // B x N   (optional)
+};
+
+// Launch one decode (host side, implemented in ldpc_kernels.hip).
+// method: 0 min-sum, 1 sum-product, 2 bit-flip, 3 hard; prec 0 f64, 1 f32;
+// slots = ceil(E/64); nw = 1 or 4 (hard-decision words).
+int launch_decode(const CodeView &code, const DecodeArgs &args, int method,
+                  int prec, int slots, int nw, void *stream);
+
+}  // namespace ldpc

@@ -1,0 +1,191 @@
+"""ctypes binding of the C ABI in include/ldpc_hip.h (lib/libldpc_hip.so).
+
+The shared library is built in-tree (gr-ldpc_ece535a_amd/lib/); importing this
+module never falls back to anything else: if the library is missing, loading
+fails with an error that says how to build it, and if no GPU is usable,
+Decoder() raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(PKG_ROOT, "lib")
+HIP_LIB = os.path.join(LIB_DIR, "libldpc_hip.so")
+
+METHOD_LOGDOMAIN, METHOD_SUMPRODUCT, METHOD_BITFLIP, METHOD_HARD = 0, 1, 2, 3
+PREC_F64, PREC_F32 = 0, 1
+FLAG_NO_REORDER = 1
+ERRORS = {0: "LDPC_OK", -1: "LDPC_EINVAL", -2: "LDPC_EUNSUPPORTED", -3: "LDPC_EDEVICE",
+          -4: "LDPC_ESINGULAR", -5: "LDPC_ENOMEM"}
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); the full set the header declares
+SIGNATURES = {
+    "ldpc_default_h": (_i, [_u8p]),
+    "ldpc_reorder_h": (_i, [_u8p, _i, _i, _i32p]),
+    "ldpc_check_frame": (_i, [_u8p, _i, _i, _u8p, _i]),
+    "ldpc_encode": (_i, [_u8p, _i, _i, _u8p, _i, _u8p]),
+    "ldpc_create": (_vp, [_u8p, _i, _i, _i, _i]),
+    "ldpc_destroy": (None, [_vp]),
+    "ldpc_last_error": (ctypes.c_char_p, [_vp]),
+    "ldpc_ctx_info": (_i, [_vp, _i32p, _i32p, _i32p, _i32p, _i32p, _i32p, _i32p]),
+    "ldpc_ctx_h": (_i, [_vp, _u8p]),
+    "ldpc_decode": (_i, [_vp, _i, _i, _i, _i, _f32p, _i, _u8p, _u8p, _i32p, _i32p]),
+    "ldpc_decode_strided": (_i, [_vp, _i, _i, _i, _i, _f32p, _i64, _i64, _i, ctypes.c_float, _i,
+                                 _u8p, _u8p, _i32p, _i32p, _f32p]),
+    "ldpc_decode_device": (_i, [_vp, _i, _i, _i, _i, _vp, _i64, _i, ctypes.c_float, _i,
+                                _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ldpc_synchronize": (_i, [_vp]),
+}
+
+_lib = None
+
+
+class LdpcError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load lib/libldpc_hip.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(HIP_LIB):
+            raise LdpcError("%s is missing: build it with `make -C %s` (or "
+                            "__graft_entry__.build()); there is no fallback" % (HIP_LIB, PKG_ROOT))
+        L = ctypes.CDLL(HIP_LIB)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(t)
+
+
+def _check(rc, ctx=None):
+    if rc < 0:
+        msg = lib().ldpc_last_error(ctx)
+        raise LdpcError("%s: %s" % (ERRORS.get(rc, rc), (msg or b"").decode()))
+    return rc
+
+
+def default_h():
+    """The reference decoder's 32x64 H (lib/ldpc_decoder_cb_impl.cc:63-96)."""
+    H = np.zeros((32, 64), np.uint8)
+    _check(lib().ldpc_default_h(_p(H, _u8p)))
+    return H
+
+
+def reorder_h(H):
+    """reorderHMatrix (lib/ldpc_decoder_cb_impl.cc:255-307) -> (Hr, chosen)."""
+    H = np.ascontiguousarray(H, np.uint8).copy()
+    M, N = H.shape
+    chosen = np.zeros(M, np.int32)
+    _check(lib().ldpc_reorder_h(_p(H, _u8p), M, N, _p(chosen, _i32p)))
+    return H, chosen
+
+
+def check_frame(H, bits, threshold):
+    """checkFrame (lib/ldpc_decoder_cb_impl.cc:236-253)."""
+    H = np.ascontiguousarray(H, np.uint8)
+    bits = np.ascontiguousarray(bits, np.uint8)
+    M, N = H.shape
+    return _check(lib().ldpc_check_frame(_p(H, _u8p), M, N, _p(bits, _u8p), int(threshold)))
+
+
+def encode(Hr, data_bits):
+    """makeParityCheck (lib/ldpc_encoder_bc_impl.cc:275-294): (B, N-M) data
+    bits -> (B, N) codewords [parity; data]."""
+    Hr = np.ascontiguousarray(Hr, np.uint8)
+    M, N = Hr.shape
+    d = np.ascontiguousarray(np.atleast_2d(data_bits), np.uint8)
+    out = np.zeros((d.shape[0], N), np.uint8)
+    _check(lib().ldpc_encode(_p(Hr, _u8p), M, N, _p(d, _u8p), d.shape[0], _p(out, _u8p)))
+    return out
+
+
+class Decoder:
+    """One decode context (device tables + stream) for one H."""
+
+    def __init__(self, H=None, reorder=True, device=0):
+        if H is None:
+            H = default_h()
+        H = np.ascontiguousarray(H, np.uint8)
+        M, N = H.shape
+        flags = 0 if reorder else FLAG_NO_REORDER
+        self._ctx = lib().ldpc_create(_p(H, _u8p), M, N, flags, int(device))
+        if not self._ctx:
+            raise LdpcError("ldpc_create failed: %s" % lib().ldpc_last_error(None).decode())
+        v = [ctypes.c_int32(0) for _ in range(7)]
+        _check(lib().ldpc_ctx_info(self._ctx, *[ctypes.byref(x) for x in v]), self._ctx)
+        self.M, self.N, self.E, self.K, self.KB, self.dc_max, self.dv_max = [x.value for x in v]
+        self.H = np.zeros((M, N), np.uint8)
+        _check(lib().ldpc_ctx_h(self._ctx, _p(self.H, _u8p)), self._ctx)
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            lib().ldpc_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def decode(self, llr, method=METHOD_SUMPRODUCT, max_iters=50, et_period=1,
+               precision=PREC_F64, polarity=1.0, cw_stride=None, elem_stride=1, B=None,
+               want_bits=True, want_llr=False):
+        """Decode host float32 frames (synchronous).  Returns a dict with
+        packed (B,KB), bits (B,N), iters (B,), synd (B,) [, llr (B,N)]."""
+        x = np.ascontiguousarray(llr, np.float32).reshape(-1)
+        if cw_stride is None:
+            cw_stride = self.N * elem_stride
+        if B is None:
+            B = x.size // cw_stride if cw_stride else 0
+        packed = np.zeros((B, self.KB), np.uint8)
+        bits = np.zeros((B, self.N), np.uint8) if want_bits else None
+        iters = np.zeros(B, np.int32)
+        synd = np.zeros(B, np.int32)
+        post = np.zeros((B, self.N), np.float32) if want_llr else None
+        _check(lib().ldpc_decode_strided(self._ctx, int(method), int(max_iters), int(et_period),
+                                         int(precision), _p(x, _f32p), x.size, int(cw_stride),
+                                         int(elem_stride), float(polarity), int(B),
+                                         _p(packed, _u8p), _p(bits, _u8p), _p(iters, _i32p),
+                                         _p(synd, _i32p), _p(post, _f32p)), self._ctx)
+        out = dict(packed=packed, iters=iters, synd=synd)
+        if want_bits:
+            out["bits"] = bits
+        if want_llr:
+            out["llr"] = post
+        return out
+
+    def decode_device(self, d_in, B, d_packed, method=METHOD_SUMPRODUCT, max_iters=50,
+                      et_period=1, precision=PREC_F64, polarity=1.0, cw_stride=None,
+                      elem_stride=1, d_bits=None, d_iters=None, d_synd=None, d_llr=None,
+                      stream=None):
+        """Enqueue a decode of device-resident buffers (raw pointers / ints)."""
+        if cw_stride is None:
+            cw_stride = self.N * elem_stride
+        _check(lib().ldpc_decode_device(self._ctx, int(method), int(max_iters), int(et_period),
+                                        int(precision), d_in, int(cw_stride), int(elem_stride),
+                                        float(polarity), int(B), d_packed, d_bits, d_iters,
+                                        d_synd, d_llr, stream), self._ctx)
+
+    def synchronize(self):
+        _check(lib().ldpc_synchronize(self._ctx), self._ctx)

@@ -1,0 +1,156 @@
+/*
+ * ldpc_hip.h -- C ABI of the MI355X-native LDPC decode path
+ * (libldpc_hip.so, built from gr-ldpc_ece535a_amd/csrc/).
+ *
+ * Drop-in boundary for the decode hot path of ericdegroot/gr-ldpc_ece535a.
+ * The reference has no FFI for this path: its block calls private member
+ * functions.  Each entry point below names the reference interface it
+ * replaces (paths relative to the reference repository root):
+ *
+ *   ldpc_create / ldpc_destroy
+ *       ldpc_decoder_cb_impl::ldpc_decoder_cb_impl(method)
+ *       lib/ldpc_decoder_cb_impl.cc:35-117 (H setup + reorderHMatrix :104-106)
+ *   ldpc_decode, ldpc_decode_strided, ldpc_decode_device
+ *       decodeLogDomainSimple :309-412, decodeSumProductSoft :478-557,
+ *       decodeBitFlipping :414-476, decodeHard :559-572 and the early-exit
+ *       checkFrame(vhat, 0) they call, dispatched as general_work :155-164;
+ *       the syndrome weight output replaces checkFrame(vhat, M/8) :166, and
+ *       the packed output replaces the byte packing :207-219.
+ *   ldpc_reorder_h          reorderHMatrix :255-307
+ *   ldpc_check_frame        checkFrame :236-253
+ *   ldpc_encode             makeParityCheck, lib/ldpc_encoder_bc_impl.cc:275-294
+ *   ldpc_default_h          the hard-coded 32x64 H, lib/ldpc_decoder_cb_impl.cc:60-96
+ *
+ * Conventions: plain pointers and sizes only; errors are negative return
+ * codes (LDPC_E*), never exceptions; ldpc_last_error() gives the text.  One
+ * context per block instance; a context is not re-entrant.  Host helpers
+ * (ldpc_reorder_h, ldpc_check_frame, ldpc_encode, ldpc_default_h) need no GPU.
+ * Everything that decodes runs on the GPU; there is no CPU fallback.
+ */
+#ifndef LDPC_HIP_H
+#define LDPC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* decode methods: the reference's GRC enum, grc/ldpc_ece535a_ldpc_decoder_cb.xml:11-29.
+ * Any other value behaves as LDPC_METHOD_LOGDOMAIN (general_work :162-164). */
+#define LDPC_METHOD_LOGDOMAIN 0  /* min-sum, decodeLogDomainSimple */
+#define LDPC_METHOD_SUMPRODUCT 1 /* decodeSumProductSoft */
+#define LDPC_METHOD_BITFLIP 2    /* decodeBitFlipping */
+#define LDPC_METHOD_HARD 3       /* decodeHard */
+
+/* arithmetic for methods 0/1.  F64 reproduces the reference's double
+ * arithmetic operation for operation (parity mode, default); F32 is the fast
+ * mode (hard decisions are compared against the oracle, not guaranteed). */
+#define LDPC_PREC_F64 0
+#define LDPC_PREC_F32 1
+
+/* ldpc_create flags */
+#define LDPC_FLAG_NO_REORDER 1 /* use H as given (skip reorderHMatrix) */
+
+/* error codes */
+#define LDPC_OK 0
+#define LDPC_EINVAL -1      /* bad argument */
+#define LDPC_EUNSUPPORTED -2 /* code shape outside the built kernels */
+#define LDPC_EDEVICE -3     /* HIP runtime error (no GPU, launch failure...) */
+#define LDPC_ESINGULAR -4   /* encoder: singular triangular factor */
+#define LDPC_ENOMEM -5
+
+typedef struct ldpc_ctx ldpc_ctx;
+
+/* ---- host helpers (no GPU) ---------------------------------------- */
+
+/* Writes the reference's default 32x64 H (row-major, one byte per entry)
+ * to H_out (2048 bytes).  Returns 0. */
+int ldpc_default_h(uint8_t *H_out);
+
+/* reorderHMatrix: permutes the columns of H (M x N, row-major 0/1 bytes) in
+ * place; chosen_opt (M ints) receives the column chosen at each step. */
+int ldpc_reorder_h(uint8_t *H, int M, int N, int32_t *chosen_opt);
+
+/* checkFrame(u, threshold): number of unsatisfied checks, counting stops
+ * once it exceeds threshold (so the result is min(weight, threshold+1)). */
+int ldpc_check_frame(const uint8_t *H, int M, int N, const uint8_t *bits,
+                     int threshold);
+
+/* makeParityCheck for B frames: H must be the REORDERED H (M x N, N >= 2M);
+ * data_bits is B x (N-M) 0/1 bytes; codewords_out is B x N = [parity; data]
+ * (the encoder's output order, lib/ldpc_encoder_bc_impl.cc:153-165). */
+int ldpc_encode(const uint8_t *H_reordered, int M, int N,
+                const uint8_t *data_bits, int B, uint8_t *codewords_out);
+
+/* ---- device context ----------------------------------------------- */
+
+/* Builds the decoder's view of H (reorderHMatrix unless
+ * LDPC_FLAG_NO_REORDER), uploads its edge tables to `device`.  Returns NULL
+ * on failure; ldpc_last_error(NULL) then says why. */
+ldpc_ctx *ldpc_create(const uint8_t *H, int M, int N, int flags, int device);
+void ldpc_destroy(ldpc_ctx *ctx);
+const char *ldpc_last_error(const ldpc_ctx *ctx);
+
+/* M, N, E (edges), K = N - M info bits, KB = ceil(K/8) packed bytes, and the
+ * max check / variable degrees.  Any pointer may be NULL. */
+int ldpc_ctx_info(const ldpc_ctx *ctx, int *M, int *N, int *E, int *K, int *KB,
+                  int *dc_max, int *dv_max);
+/* Copies the context's (reordered) H, M x N bytes. */
+int ldpc_ctx_h(const ldpc_ctx *ctx, uint8_t *H_out);
+
+/* ---- decode ------------------------------------------------------- */
+/* Common parameters:
+ *   method      LDPC_METHOD_*
+ *   max_iters   iteration cap (the block's d_iterations; >= 1 for methods 0-2)
+ *   et_period   early-termination check period; 1 = every iteration, the
+ *               reference's rule (SP checks after each decision :535-537;
+ *               min-sum / bit-flip only when it+1 < max_iters :406, :470)
+ *   precision   LDPC_PREC_*
+ * Per frame b the samples are in[b*cw_stride + i*elem_stride], i < N
+ * (elem_stride 2 reads the real parts of interleaved gr_complex), and the
+ * decoder sees tx = in * polarity (general_work :149-153; polarity -1 is the
+ * "-tx" retry :180-187).
+ * Outputs per frame (each optional except packed):
+ *   out_packed  KB bytes: bits M.. of the hard decision, MSB first (:207-219)
+ *   out_bits    N bytes 0/1, the full hard decision vhat
+ *   iters_used  iterations executed
+ *   syn_weight  unsatisfied checks of the returned vhat (uncapped)
+ *   llr_out     N floats, the final posterior (SP: L_i of :519-532; min-sum:
+ *               L(Q_i) :395; hard/bit-flip: tx)
+ */
+
+/* Host buffers, contiguous real-valued frames (B x N floats); synchronous. */
+int ldpc_decode(ldpc_ctx *ctx, int method, int max_iters, int et_period,
+                int precision, const float *llr_re, int B, uint8_t *out_packed,
+                uint8_t *out_bits_opt, int32_t *iters_used_opt,
+                int32_t *syn_weight_opt);
+
+/* Host buffers with the strided frame descriptor above; n_in_floats bounds
+ * the input read.  Synchronous. */
+int ldpc_decode_strided(ldpc_ctx *ctx, int method, int max_iters,
+                        int et_period, int precision, const float *in,
+                        int64_t n_in_floats, int64_t cw_stride,
+                        int elem_stride, float polarity, int B,
+                        uint8_t *out_packed, uint8_t *out_bits_opt,
+                        int32_t *iters_used_opt, int32_t *syn_weight_opt,
+                        float *llr_out_opt);
+
+/* Device-resident buffers (already in HBM); enqueues on `hip_stream`
+ * (hipStream_t, NULL = the context's own stream) and returns without
+ * synchronising. */
+int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
+                       int et_period, int precision, const float *d_in,
+                       int64_t cw_stride, int elem_stride, float polarity,
+                       int B, uint8_t *d_out_packed, uint8_t *d_out_bits_opt,
+                       int32_t *d_iters_used_opt, int32_t *d_syn_weight_opt,
+                       float *d_llr_out_opt, void *hip_stream);
+
+/* Blocks until the context's stream is idle. */
+int ldpc_synchronize(ldpc_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LDPC_HIP_H */
