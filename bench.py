@@ -1,0 +1,275 @@
+#!/usr/bin/env python3
+"""Benchmark of the decode hot path (BASELINE.json configs[1] / [2]).
+
+One "step" = one pass of the decoder over one batch of synthetic frames
+already resident in HBM: B = 4096 frames of the reference's default 32x64 H
+(reordered as the block does), sum-product (method 1), 50-iteration cap with
+the reference's per-frame early exit, Eb/N0 = 2 dB with the reference noise
+convention (sigma = sqrt(10^(-EbN0/10)), apps/ldpc_lapack.cpp:635-642).
+
+  python bench.py [--gpus N --steps K --warmup W]
+
+N > 1 runs under torch.distributed.run, one rank per GPU: each rank decodes
+its own batch (weak scaling, independent frames, no collective in the data
+path); after the timed loop RCCL all-gathers the packed outputs and
+all-reduces the counters (the "final throughput gather").  Rank 0 prints ONE
+JSON line.  `value` = info bits of all frames all ranks decoded / the max
+over ranks of the timed wall time.
+
+roofline.achieved uses SURVEY.md 8(d)'s algorithmic byte model per launch:
+  sum_b [4N (fp32 Re in) + KB + 8 (packed, iters, syndrome out)
+         + iters_b * (32E + 10N)]  (f64 parity mode; 16E + 6N for f32)
+divided by the kernel's mean duration measured with HIP events on the
+stream it is launched on.  roofline.traffic is the rocprofv3 PMC measurement
+(profiles/) per launch, when a matching entry exists.
+cpu_baseline: the C oracle (oracle/, a dense double restatement of the
+reference decoder) decoding the same frames on the host's cores.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "gr-ldpc_ece535a_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--method", type=int, default=1)
+    ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--et-period", type=int, default=1)
+    ap.add_argument("--ebn0", type=float, default=2.0)
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--waves-per-cu", type=int, default=0)
+    ap.add_argument("--sweep-wpc", default="", help="comma list; prints a table to stderr")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def synth(Hr, B, ebn0, seed):
+    """Seeded frames: data ~ Bernoulli(1/2) (PCG64), GF(2) encode through the
+    product's ldpc_encode, BPSK 1->+1, AWGN with the reference sigma."""
+    import ldpc_ece535a as L
+    M, N = Hr.shape
+    rng = np.random.Generator(np.random.PCG64(seed))
+    data = rng.integers(0, 2, size=(B, N - M), dtype=np.uint8)
+    cw = L.encode(Hr, data)
+    sigma = np.sqrt(10.0 ** (-ebn0 / 10.0))
+    y = (2.0 * cw.astype(np.float64) - 1.0 + sigma * rng.standard_normal((B, N)))
+    return y.astype(np.float32), data
+
+
+def bytes_per_iter(E, N, prec):
+    return 32 * E + 10 * N if prec == 0 else 16 * E + 6 * N
+
+
+def time_decoder(dec, torch, d_in, B, method, iters, et, prec, steps, warmup, dist=None):
+    """Returns (wall_s, mean_kernel_ms, per-frame iters, outputs)."""
+    dev = d_in.device
+    d_packed = torch.empty((B, dec.KB), dtype=torch.uint8, device=dev)
+    d_iters = torch.empty(B, dtype=torch.int32, device=dev)
+    d_synd = torch.empty(B, dtype=torch.int32, device=dev)
+    # a dedicated (non-null) stream: the kernel and the timing events share it
+    stream = torch.cuda.Stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def step():
+        dec.decode_device(d_in.data_ptr(), B, d_packed.data_ptr(), method=method, max_iters=iters,
+                          et_period=et, precision=prec, d_iters=d_iters.data_ptr(),
+                          d_synd=d_synd.data_ptr(), stream=sp)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(steps):
+        evs[s][0].record(stream)
+        step()
+        evs[s][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    return wall, kern_ms, d_iters.cpu().numpy(), (d_packed, d_iters, d_synd)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import ldpc_ece535a as L
+
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    prec = 0 if args.precision == "f64" else 1
+
+    dec = L.Decoder(device=local)  # default H, reorderHMatrix applied
+    dec.set_waves_per_cu(args.waves_per_cu)
+    Hr = dec.H
+    B = args.batch
+    llr, data = synth(Hr, B, args.ebn0, args.seed + 7919 * rank)
+    d_in = torch.from_numpy(llr).to(dev)  # resident in HBM before timing
+
+    if args.sweep_wpc:
+        for m, p in ((args.method, prec), (1, 1), (0, 0)):
+            for wpc in [int(x) for x in args.sweep_wpc.split(",")]:
+                dec.set_waves_per_cu(wpc)
+                w0, k0, it0, _ = time_decoder(dec, torch, d_in, B, m, args.iters,
+                                              args.et_period, p, args.steps, args.warmup)
+                print("sweep method=%d prec=%d wpc=%2d kernel_ms=%.4f wall_ms/step=%.4f" %
+                      (m, p, wpc, k0, w0 / args.steps * 1e3), file=sys.stderr, flush=True)
+        dec.set_waves_per_cu(args.waves_per_cu)
+
+    wall, kern_ms, iters_b, outs = time_decoder(dec, torch, d_in, B, args.method, args.iters,
+                                                args.et_period, prec, args.steps, args.warmup,
+                                                dist)
+    packed = outs[0].cpu().numpy()
+    synd = outs[2].cpu().numpy()
+
+    # ---- final gather (RCCL): outputs to every rank + counters ------------
+    totals = np.array([B, B * dec.K, int(iters_b.sum()), int((synd > 0).sum())], np.float64)
+    wall_max = wall
+    if dist is not None:
+        g = [torch.empty_like(outs[0]) for _ in range(world)]
+        dist.all_gather(g, outs[0])
+        t = torch.tensor(totals, device=dev)
+        dist.all_reduce(t)
+        totals = t.cpu().numpy()
+        w = torch.tensor([wall], device=dev, dtype=torch.float64)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall_max = float(w.item())
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    frames_all = totals[0] * args.steps
+    info_bits = totals[1] * args.steps
+    value = info_bits / wall_max / 1e6
+    E, N = dec.E, dec.N
+    alg_bytes = float(B * (4 * N + dec.KB + 8) + iters_b.sum() * bytes_per_iter(E, N, prec))
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    workload_key = "sp%d_%s_b%d_i%d_db%g" % (args.method, args.precision, B, args.iters, args.ebn0)
+    try:
+        tj = json.load(open(args.traffic_json))
+        if workload_key in tj:
+            traffic = tj[workload_key]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+
+    line = {
+        "metric": "decoded info Mbit/s @ 50 BP iters, batch=4096; achieved HBM GB/s vs peak",
+        "value": round(value, 3),
+        "unit": "Mbit/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (PCG64 bits, GF(2) encode, BPSK, AWGN sigma=sqrt(10^(-EbN0/10)))",
+        "config": {
+            "workload": "config2: reference default 32x64 H (reordered), B=%d frames/GPU, "
+                        "method %d (%s), %d-iteration cap with per-frame early exit, "
+                        "Eb/N0 %g dB" % (B, args.method,
+                                         {0: "min-sum", 1: "sum-product", 2: "bit-flip",
+                                          3: "hard"}[args.method], args.iters, args.ebn0),
+            "global_batch": int(totals[0]),
+            "frames_per_gpu": B,
+            "parallelism": "dp%d (independent frames)" % world,
+            "mean_iters": round(float(iters_b.mean()), 3),
+            "syndrome_fail_frac": round(float((synd > 0).mean()), 4),
+            "et_period": args.et_period,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel_ms": round(kern_ms, 5),
+            "model": "SURVEY 8(d) algorithmic bytes per launch = %d" % int(alg_bytes),
+        },
+    }
+
+    # ---- variants measured in the same process (not the headline) ----------
+    if not args.no_variants:
+        var = {}
+        for name, (m, p) in {"sum-product f32": (1, 1), "min-sum f64": (0, 0),
+                             "min-sum f32": (0, 1)}.items():
+            w2, k2, it2, o2 = time_decoder(dec, torch, d_in, B, m, args.iters, args.et_period, p,
+                                           max(5, args.steps // 2), 2)
+            st = max(5, args.steps // 2)
+            var[name] = {"Mbit/s": round(B * dec.K * st / w2 / 1e6, 2),
+                         "kernel_ms": round(k2, 5), "mean_iters": round(float(it2.mean()), 3)}
+        line["variants_1gpu"] = var
+
+    # ---- CPU baseline + parity (the oracle as checker) ----------------------
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, REPO)
+        from oracle import oracle as orc
+        try:
+            ncpu = len(os.sched_getaffinity(0))
+        except AttributeError:
+            ncpu = os.cpu_count() or 1
+        threads = args.cpu_threads or max(1, min(16, ncpu))
+        t0 = time.perf_counter()
+        ref = orc.decode_batch(args.method, Hr, llr, args.iters, nthreads=threads)
+        cpu_s = time.perf_counter() - t0
+        nsample = min(B, 128)
+        t1 = time.perf_counter()
+        orc.decode_batch(args.method, Hr, llr[:nsample], args.iters, nthreads=1)
+        cpu1_s = time.perf_counter() - t1
+        mism = int((ref["packed"] != packed).any(axis=1).sum()) if rank == 0 else None
+        line["cpu_baseline"] = {
+            "value": round(B * dec.K / cpu_s / 1e6, 5),
+            "unit": "Mbit/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": "the same %d frames (rank 0's batch), %d threads; 1-core: %.5f Mbit/s on "
+                      "the first %d frames" % (B, threads, nsample * dec.K / cpu1_s / 1e6, nsample),
+        }
+        line["parity"] = {"frames": B, "packed_mismatch_frames": mism,
+                          "iters_mismatch_frames": int((ref["iters"] != iters_b).sum()),
+                          "checker": "oracle/ (C restatement of the reference decoder)"}
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -17,7 +17,8 @@
 #include "ldpc_kernels.hpp"
 
 using ldpc::ColRec;
-using ldpc::EdgeRec;
+using ldpc::EdgeColRec;
+using ldpc::EdgeRowRec;
 using ldpc::kNone;
 
 struct ldpc_ctx {
@@ -26,13 +27,19 @@ struct ldpc_ctx {
   int device = 0;
   std::vector<uint8_t> H;  // the decoder's (reordered) H
   hipStream_t stream = nullptr;
-  EdgeRec *d_edges = nullptr;
+  EdgeRowRec *d_erow = nullptr;
+  EdgeColRec *d_ecol = nullptr;
   ColRec *d_cols = nullptr;
   uint64_t *d_rowmask = nullptr;
   void *d_stage = nullptr;
   size_t stage_bytes = 0;
+  uint32_t *d_tickets = nullptr;  // ring of per-launch frame-queue heads
+  unsigned launch_seq = 0;
+  int waves_per_cu = 0;           // 0: kernel default
   std::string err;
 };
+
+#define LDPC_TICKET_RING 64
 
 namespace {
 
@@ -110,8 +117,8 @@ bool valid_h(const uint8_t *H, int M, int N) {
 }
 
 // Edge / column / row tables of the decoder's H (see ldpc_kernels.hpp).
-int build_tables(ldpc_ctx *ctx, std::vector<EdgeRec> &edges, std::vector<ColRec> &cols,
-                 std::vector<uint64_t> &rowmask) {
+int build_tables(ldpc_ctx *ctx, std::vector<EdgeRowRec> &erecs, std::vector<EdgeColRec> &crecs,
+                 std::vector<ColRec> &cols, std::vector<uint64_t> &rowmask) {
   const int M = ctx->M, N = ctx->N;
   const uint8_t *H = ctx->H.data();
   std::vector<std::vector<int>> row_edges(M), col_edges(N);
@@ -147,23 +154,24 @@ int build_tables(ldpc_ctx *ctx, std::vector<EdgeRec> &edges, std::vector<ColRec>
   ctx->K = N - M;
   ctx->KB = (ctx->K + 7) / 8;
 
-  edges.assign((size_t)64 * ctx->slots, EdgeRec{});
-  for (auto &r : edges) {
-    r.col = kNone;
-    r.row = kNone;
+  erecs.assign((size_t)64 * ctx->slots, EdgeRowRec{});
+  crecs.assign((size_t)64 * ctx->slots, EdgeColRec{});
+  for (auto &r : erecs) {
     std::fill(std::begin(r.rn), std::end(r.rn), kNone);
+    r.col = kNone;
+  }
+  for (auto &r : crecs) {
     std::fill(std::begin(r.cn), std::end(r.cn), kNone);
+    r.col = kNone;
   }
   for (int e = 0; e < ctx->E; ++e) {
-    EdgeRec &r = edges[e];
-    r.col = (uint16_t)ecol[e];
-    r.row = (uint16_t)erow[e];
+    erecs[e].col = crecs[e].col = (uint16_t)ecol[e];
     int k = 0;
     for (int n : row_edges[erow[e]])
-      if (n != e) r.rn[k++] = (uint16_t)n;  // ascending column
+      if (n != e) erecs[e].rn[k++] = (uint16_t)n;  // ascending column
     k = 0;
     for (int n : col_edges[ecol[e]])
-      if (n != e) r.cn[k++] = (uint16_t)n;  // ascending row
+      if (n != e) crecs[e].cn[k++] = (uint16_t)n;  // ascending row
   }
   cols.assign((size_t)64 * ctx->nw, ColRec{});
   for (auto &c : cols) {
@@ -214,7 +222,8 @@ int check_decode_args(ldpc_ctx *ctx, int &method, int max_iters, int et_period, 
 
 ldpc::CodeView code_view(const ldpc_ctx *ctx) {
   ldpc::CodeView v;
-  v.edges = ctx->d_edges;
+  v.erow = ctx->d_erow;
+  v.ecol = ctx->d_ecol;
   v.cols = ctx->d_cols;
   v.rowmask = ctx->d_rowmask;
   v.M = ctx->M;
@@ -307,10 +316,11 @@ ldpc_ctx *ldpc_create(const uint8_t *H, int M, int N, int flags, int device) {
   ctx->device = device;
   ctx->H.assign(H, H + (size_t)M * N);
   if (!(flags & LDPC_FLAG_NO_REORDER)) reorder_columns(ctx->H.data(), M, N, nullptr, nullptr, nullptr);
-  std::vector<EdgeRec> edges;
+  std::vector<EdgeRowRec> erecs;
+  std::vector<EdgeColRec> crecs;
   std::vector<ColRec> cols;
   std::vector<uint64_t> rowmask;
-  int rc = build_tables(ctx, edges, cols, rowmask);
+  int rc = build_tables(ctx, erecs, crecs, cols, rowmask);
   if (rc != LDPC_OK) {
     g_create_error = ctx->err;
     delete ctx;
@@ -329,15 +339,26 @@ ldpc_ctx *ldpc_create(const uint8_t *H, int M, int N, int flags, int device) {
   if ((e = hipSetDevice(device)) != hipSuccess) what = "hipSetDevice";
   if (!what && (e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     what = "hipStreamCreate";
-  if (!what && (e = hipMalloc(&ctx->d_edges, edges.size() * sizeof(EdgeRec))) != hipSuccess)
-    what = "hipMalloc(edges)";
+  if (!what && (e = hipMalloc(&ctx->d_erow, erecs.size() * sizeof(EdgeRowRec))) != hipSuccess)
+    what = "hipMalloc(erow)";
+  if (!what && (e = hipMalloc(&ctx->d_ecol, crecs.size() * sizeof(EdgeColRec))) != hipSuccess)
+    what = "hipMalloc(ecol)";
   if (!what && (e = hipMalloc(&ctx->d_cols, cols.size() * sizeof(ColRec))) != hipSuccess)
     what = "hipMalloc(cols)";
   if (!what && (e = hipMalloc(&ctx->d_rowmask, rowmask.size() * 8)) != hipSuccess)
     what = "hipMalloc(rowmask)";
-  if (!what && (e = hipMemcpy(ctx->d_edges, edges.data(), edges.size() * sizeof(EdgeRec),
+  if (!what && (e = hipMalloc(&ctx->d_tickets, LDPC_TICKET_RING * sizeof(uint32_t))) !=
+                   hipSuccess)
+    what = "hipMalloc(tickets)";
+  if (!what && (e = hipMemset(ctx->d_tickets, 0, LDPC_TICKET_RING * sizeof(uint32_t))) !=
+                   hipSuccess)
+    what = "hipMemset(tickets)";
+  if (!what && (e = hipMemcpy(ctx->d_erow, erecs.data(), erecs.size() * sizeof(EdgeRowRec),
                               hipMemcpyHostToDevice)) != hipSuccess)
-    what = "hipMemcpy(edges)";
+    what = "hipMemcpy(erow)";
+  if (!what && (e = hipMemcpy(ctx->d_ecol, crecs.data(), crecs.size() * sizeof(EdgeColRec),
+                              hipMemcpyHostToDevice)) != hipSuccess)
+    what = "hipMemcpy(ecol)";
   if (!what && (e = hipMemcpy(ctx->d_cols, cols.data(), cols.size() * sizeof(ColRec),
                               hipMemcpyHostToDevice)) != hipSuccess)
     what = "hipMemcpy(cols)";
@@ -355,10 +376,12 @@ ldpc_ctx *ldpc_create(const uint8_t *H, int M, int N, int flags, int device) {
 void ldpc_destroy(ldpc_ctx *ctx) {
   if (!ctx) return;
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->d_edges) (void)hipFree(ctx->d_edges);
+  if (ctx->d_erow) (void)hipFree(ctx->d_erow);
+  if (ctx->d_ecol) (void)hipFree(ctx->d_ecol);
   if (ctx->d_cols) (void)hipFree(ctx->d_cols);
   if (ctx->d_rowmask) (void)hipFree(ctx->d_rowmask);
   if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+  if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -409,12 +432,17 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   a.iters = d_iters_used_opt;
   a.synd = d_syn_weight_opt;
   a.llr = d_llr_out_opt;
+  a.ticket = ctx->d_tickets + (ctx->launch_seq % LDPC_TICKET_RING);
+  a.ticket_next = ctx->d_tickets + ((ctx->launch_seq + 1) % LDPC_TICKET_RING);
+  a.waves = 0;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   void *st = hip_stream ? hip_stream : (void *)ctx->stream;
-  rc = ldpc::launch_decode(code_view(ctx), a, method, precision, ctx->slots, ctx->nw, st);
+  rc = ldpc::launch_decode(code_view(ctx), a, method, precision, ctx->slots, ctx->nw,
+                           ctx->waves_per_cu, st);
   if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no kernel for this code shape");
   if (rc != 0) return hip_err(ctx, hipGetLastError(), "kernel launch");
+  ++ctx->launch_seq;  // only a launched kernel consumes (and re-arms) a ticket slot
   return LDPC_OK;
 }
 
@@ -477,6 +505,13 @@ int ldpc_decode(ldpc_ctx *ctx, int method, int max_iters, int et_period, int pre
   return ldpc_decode_strided(ctx, method, max_iters, et_period, precision, llr_re,
                              (int64_t)B * ctx->N, ctx->N, 1, 1.0f, B, out_packed, out_bits_opt,
                              iters_used_opt, syn_weight_opt, nullptr);
+}
+
+int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu) {
+  if (!ctx || waves_per_cu < 0 || waves_per_cu > 32)
+    return set_err(ctx, LDPC_EINVAL, "waves_per_cu must be in [0, 32]");
+  ctx->waves_per_cu = waves_per_cu;
+  return LDPC_OK;
 }
 
 int ldpc_synchronize(ldpc_ctx *ctx) {

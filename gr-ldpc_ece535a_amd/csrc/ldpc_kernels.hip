@@ -25,7 +25,10 @@
 #include <float.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "ldpc_kernels.hpp"
+#include "ldpc_math.hpp"
 
 namespace ldpc {
 
@@ -42,8 +45,13 @@ template <typename Real>
 struct Math;
 template <>
 struct Math<double> {
+#ifdef LDPC_OCML_F64  // A/B switch: ROCm's ocml tanh/log
   static __device__ __forceinline__ double tanh_(double x) { return ::tanh(x); }
   static __device__ __forceinline__ double log_(double x) { return ::log(x); }
+#else  // fdlibm (ldpc_math.hpp): tanh bit-identical to glibc's, log < 1 ulp
+  static __device__ __forceinline__ double tanh_(double x) { return fm::tanh_f64_bf(x); }
+  static __device__ __forceinline__ double log_(double x) { return fm::log_f64_bf(x); }
+#endif
   static __device__ __forceinline__ double abs_(double x) { return ::fabs(x); }
   static __device__ __forceinline__ double max_() { return DBL_MAX; }
 };
@@ -104,38 +112,34 @@ __device__ __forceinline__ int syndrome_weight(const uint64_t (&hard)[NW],
 
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
+// Block LDS: [rowmask M x NW][row recs 64S][col-neighbour recs 64S]
+// [column recs 64 NW] then one slice per wave [tb 64S][eb 64S][rb 64NW][sb 64NW].
 template <typename Real, int S, int NW>
-__host__ __device__ constexpr size_t wave_lds_bytes() {
-  return (2 * 64 * S + 2 * 64 * NW) * sizeof(Real);
-}
+struct Layout {
+  size_t erow, ecol, cols, waves, per_wave, total;
+  __host__ __device__ explicit Layout(int M) {
+    erow = align16((size_t)M * NW * 8);
+    ecol = erow + (size_t)64 * S * sizeof(EdgeRowRec);
+    cols = ecol + (size_t)64 * S * sizeof(EdgeColRec);
+    waves = align16(cols + (size_t)64 * NW * sizeof(ColRec));
+    per_wave = (2 * 64 * S + 2 * 64 * NW) * sizeof(Real);
+    total = waves + (size_t)kWavesPerBlock * per_wave;
+  }
+};
 
+// Decodes frame b with the wave's resident tables (er/cr) and LDS slice.
 template <typename Real, int METHOD, int S, int NW>
-__global__ void __launch_bounds__(kThreads)
-    decode_small_kernel(CodeView code, DecodeArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+__device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeArgs &a,
+                                             const int64_t b, const int (&col)[S],
+                                             const EdgeRowRec *erow, const EdgeColRec *ecol,
+                                             const ColRec *cols, const uint64_t *rowmask,
+                                             Real *tb, Real *eb, Real *rb, Real *sb,
+                                             const int lane) {
   const int M = code.M, N = code.N;
-
-  // Row masks, shared by the block's waves (the only workgroup barrier).
-  uint64_t *rowmask = reinterpret_cast<uint64_t *>(smem);
-  for (int t = threadIdx.x; t < M * NW; t += kThreads) rowmask[t] = code.rowmask[t];
-  __syncthreads();
-
-  const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-  if (b >= a.B) return;
-
-  Real *tb = reinterpret_cast<Real *>(smem + align16((size_t)M * NW * 8) +
-                                      (size_t)wave * wave_lds_bytes<Real, S, NW>());
-  Real *eb = tb + 64 * S;
-  Real *rb = eb + 64 * S;
-  Real *sb = rb + 64 * NW;
-
   // Channel samples: tx = Re(in) * polarity (:149-153); r = -tx (:486,
   // :318-321).  Lane l reads sample l of each 64-column slot (coalesced).
   const float *src = a.in + b * a.cw_stride;
   Real post[NW];
-  ColRec cr[NW];
 #pragma unroll
   for (int q = 0; q < NW; ++q) {
     const int c = lane + 64 * q;
@@ -143,7 +147,6 @@ __global__ void __launch_bounds__(kThreads)
     if (c < N) x = src[(int64_t)c * a.elem_stride] * a.polarity;
     rb[c] = -(Real)x;
     post[q] = (Real)x;
-    cr[q] = code.cols[c];
   }
 
   uint64_t hard[NW];
@@ -152,15 +155,12 @@ __global__ void __launch_bounds__(kThreads)
   int weight = 0, used = 0;
 
   if constexpr (METHOD == 1 || METHOD == 0) {
-    EdgeRec er[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) er[s] = code.edges[lane + 64 * s];
     wave_lds_sync();  // rb visible to every lane
     Real msg[S];      // SP: M(j,i) (:489-496); min-sum: L(q_ij) (:328-331)
     Real lr[S];       // min-sum: L(r_ji)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      msg[s] = er[s].col != kNone ? rb[er[s].col] : Real(0);
+      msg[s] = col[s] != kNone ? rb[col[s]] : Real(0);
       lr[s] = Real(0);
     }
 
@@ -169,15 +169,16 @@ __global__ void __launch_bounds__(kThreads)
         // ---- check pass, :503-516 -----------------------------------
 #pragma unroll
         for (int s = 0; s < S; ++s)
-          if (er[s].col != kNone) tb[lane + 64 * s] = Math<Real>::tanh_(msg[s] / Real(2));
+          if (col[s] != kNone) tb[lane + 64 * s] = Math<Real>::tanh_(msg[s] / Real(2));
         wave_lds_sync();
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          if (er[s].col != kNone) {
+          if (col[s] != kNone) {
+            const EdgeRowRec er = erow[lane + 64 * s];
             Real T = Real(1);
 #pragma unroll
             for (int k = 0; k < kDcMax - 1; ++k) {
-              const int n = er[s].rn[k];
+              const int n = er.rn[k];
               if (n != kNone) T = T * tb[n];
             }
             eb[lane + 64 * s] = Math<Real>::log_((Real(1) + T) / (Real(1) - T));
@@ -190,11 +191,12 @@ __global__ void __launch_bounds__(kThreads)
           const int c = lane + 64 * q;
           bool bit = false;
           if (c < N) {
+            const ColRec cr = cols[c];
             const Real rc = rb[c];
             Real L = Real(0);
 #pragma unroll
             for (int k = 0; k < kDvMax; ++k) {
-              const int n = cr[q].e[k];
+              const int n = cr.e[k];
               if (n != kNone) L = L + (eb[n] + rc);
             }
             bit = L <= Real(0);
@@ -206,17 +208,18 @@ __global__ void __launch_bounds__(kThreads)
         // ---- min-sum horizontal step, :340-376 ----------------------
 #pragma unroll
         for (int s = 0; s < S; ++s)
-          if (er[s].col != kNone) tb[lane + 64 * s] = msg[s];
+          if (col[s] != kNone) tb[lane + 64 * s] = msg[s];
         wave_lds_sync();
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          if (er[s].col != kNone) {
+          if (col[s] != kNone) {
+            const EdgeRowRec er = erow[lane + 64 * s];
             const int self = sgn(msg[s]);
             int prod = self;
             Real lo = Math<Real>::max_();
 #pragma unroll
             for (int k = 0; k < kDcMax - 1; ++k) {
-              const int n = er[s].rn[k];
+              const int n = er.rn[k];
               if (n != kNone) {
                 const Real v = tb[n];
                 prod *= sgn(v);
@@ -235,10 +238,11 @@ __global__ void __launch_bounds__(kThreads)
           const int c = lane + 64 * q;
           bool bit = false;
           if (c < N) {
+            const ColRec cr = cols[c];
             Real acc = Real(0);
 #pragma unroll
             for (int k = 0; k < kDvMax; ++k) {
-              const int n = cr[q].e[k];
+              const int n = cr.e[k];
               if (n != kNone) acc = acc + eb[n];
             }
             const Real LQ = rb[c] + acc;
@@ -260,12 +264,13 @@ __global__ void __launch_bounds__(kThreads)
         // ---- bit messages, :540-553: M(j,i) = sum_{k != j} (E(k,i) + r(i))
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          if (er[s].col != kNone) {
-            const Real rc = rb[er[s].col];
+          if (col[s] != kNone) {
+            const EdgeColRec ec = ecol[lane + 64 * s];
+            const Real rc = rb[col[s]];
             Real acc = Real(0);
 #pragma unroll
             for (int k = 0; k < kDvMax - 1; ++k) {
-              const int n = er[s].cn[k];
+              const int n = ec.cn[k];
               if (n != kNone) acc = acc + (eb[n] + rc);
             }
             msg[s] = acc;
@@ -276,7 +281,7 @@ __global__ void __launch_bounds__(kThreads)
         // L(q_ij) = Lci(j) + s_j - L(r_ji)  (:387-392)
 #pragma unroll
         for (int s = 0; s < S; ++s)
-          if (er[s].col != kNone) msg[s] = sb[er[s].col] - lr[s];
+          if (col[s] != kNone) msg[s] = sb[col[s]] - lr[s];
       }
     }
   } else {
@@ -315,13 +320,14 @@ __global__ void __launch_bounds__(kThreads)
           const int c = lane + 64 * q;
           bool nb = false;
           if (c < N) {
+            const ColRec cr = cols[c];
             const int cib = (int)((hard[q] >> lane) & 1);
             const int yb = (int)((y[q] >> lane) & 1);
             int votes = 0;
 #pragma unroll
             for (int k = 0; k < kDvMax; ++k) {
-              if (cr[q].e[k] != kNone) {
-                const int r = cr[q].r[k];
+              if (cr.e[k] != kNone) {
+                const int r = cr.r[k];
                 const int par = (int)((word4_at(rowpar, r >> 6) >> (r & 63)) & 1);
                 if ((par ^ cib) != yb) ++votes;
               }
@@ -363,6 +369,56 @@ __global__ void __launch_bounds__(kThreads)
     }
     a.packed[b * code.KB + p] = (uint8_t)o;
   }
+  // the next frame's rb writes must not overtake this frame's LDS reads
+  wave_lds_sync();
+}
+
+// Persistent launch: `a.waves` waves; wave w decodes frame w, then frames
+// a.waves + ticket++ until the batch is exhausted.  Frames stop after 1..cap
+// iterations, so pulling work keeps every SIMD busy to the end instead of
+// leaving it with a fixed share of the batch.
+template <typename Real, int METHOD, int S, int NW>
+__global__ void __launch_bounds__(kThreads)
+    decode_small_kernel(CodeView code, DecodeArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int M = code.M;
+  const Layout<Real, S, NW> L(M);
+
+  // Code tables into LDS, shared by the block's waves (the only workgroup
+  // barrier): row masks, per-edge neighbour records, per-column records.
+  uint64_t *rowmask = reinterpret_cast<uint64_t *>(smem);
+  EdgeRowRec *erow = reinterpret_cast<EdgeRowRec *>(smem + L.erow);
+  EdgeColRec *ecol = reinterpret_cast<EdgeColRec *>(smem + L.ecol);
+  ColRec *cols = reinterpret_cast<ColRec *>(smem + L.cols);
+  for (int t = threadIdx.x; t < M * NW; t += kThreads) rowmask[t] = code.rowmask[t];
+  for (int t = threadIdx.x; t < 64 * S; t += kThreads) {
+    erow[t] = code.erow[t];
+    ecol[t] = code.ecol[t];
+  }
+  for (int t = threadIdx.x; t < 64 * NW; t += kThreads) cols[t] = code.cols[t];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ticket_next = 0u;  // next launch's queue head
+  __syncthreads();
+
+  int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  if (b >= a.waves || b >= a.B) return;
+
+  Real *tb = reinterpret_cast<Real *>(smem + L.waves + (size_t)wave * L.per_wave);
+  Real *eb = tb + 64 * S;
+  Real *rb = eb + 64 * S;
+  Real *sb = rb + 64 * NW;
+  int col[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) col[s] = erow[lane + 64 * s].col;
+
+  while (b < a.B) {
+    decode_frame<Real, METHOD, S, NW>(code, a, b, col, erow, ecol, cols, rowmask, tb, eb, rb, sb,
+                                      lane);
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(a.ticket, 1u);
+    b = (int64_t)a.waves + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -370,9 +426,12 @@ __global__ void __launch_bounds__(kThreads)
 // ---------------------------------------------------------------------------
 template <typename Real, int METHOD, int S, int NW>
 static int launch_one(const CodeView &code, const DecodeArgs &a, hipStream_t st) {
-  const size_t lds = align16((size_t)code.M * NW * 8) +
-                     (size_t)kWavesPerBlock * wave_lds_bytes<Real, S, NW>();
-  const dim3 grid((unsigned)((a.B + kWavesPerBlock - 1) / kWavesPerBlock));
+  const size_t lds = Layout<Real, S, NW>(code.M).total;
+  if (lds > 65536 &&
+      hipFuncSetAttribute((const void *)decode_small_kernel<Real, METHOD, S, NW>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -3;
+  const dim3 grid((unsigned)((a.waves + kWavesPerBlock - 1) / kWavesPerBlock));
   hipLaunchKernelGGL((decode_small_kernel<Real, METHOD, S, NW>), grid, dim3(kThreads),
                      lds, st, code, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
@@ -406,10 +465,18 @@ static int launch_nw(const CodeView &code, const DecodeArgs &a, int method, int 
                    : launch_slots<double, 0, NW>(code, a, slots, st);
 }
 
-int launch_decode(const CodeView &code, const DecodeArgs &a, int method, int prec,
-                  int slots, int nw, void *stream) {
+int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int prec,
+                  int slots, int nw, int waves_per_cu, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (a.B <= 0) return 0;
+  if (args.B <= 0) return 0;
+  DecodeArgs a = args;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (waves_per_cu <= 0) waves_per_cu = 8;
+  const int64_t w = std::min<int64_t>((int64_t)a.B, (int64_t)waves_per_cu * cus);
+  a.waves = (int)((w + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock);
+
   if (nw == 1) return launch_nw<1>(code, a, method, prec, slots, st);
   if (nw == 4) return launch_nw<4>(code, a, method, prec, slots, st);
   return -2;

@@ -20,26 +20,31 @@ constexpr int kNMax = 256;         // 4 x 64-bit hard-decision words
 constexpr int kMMax = 256;         // 4 row slots per lane
 constexpr uint16_t kNone = 0xFFFF;
 
-// One edge (j, i) of H.  rn: the other edges of row j in ascending column
-// order -- the order of the product T *= tanh(M(j,k)/2) at :507-511 and of
-// the minimum scan at :363-369.  cn: the other edges of column i in
-// ascending row order -- the order of the sum at :544-548.
-struct EdgeRec {
-  uint16_t col;
-  uint16_t row;
+// One edge (j, i) of H, split in two 16/8-byte records so each pass reads
+// its half with one LDS load.  rn: the other edges of row j in ascending
+// column order -- the order of the product T *= tanh(M(j,k)/2) at :507-511
+// and of the minimum scan at :363-369.  cn: the other edges of column i in
+// ascending row order -- the order of the sum at :544-548.  Unused entries
+// are kNone; records of padding edges (index >= E) have col == kNone.
+struct alignas(16) EdgeRowRec {
   uint16_t rn[kDcMax - 1];
+  uint16_t col;
+};  // 16 bytes
+struct alignas(8) EdgeColRec {
   uint16_t cn[kDvMax - 1];
-};  // 24 bytes
+  uint16_t col;
+};  // 8 bytes
 
 // One column i: its edges and their rows in ascending row order (the sums
 // at :521-525 and :381-385, and the bit-flip vote at :457-461).
-struct ColRec {
+struct alignas(16) ColRec {
   uint16_t e[kDvMax];
   uint16_t r[kDvMax];
 };  // 16 bytes
 
 struct CodeView {
-  const EdgeRec *edges;      // 64 * S records; records >= E have col == kNone
+  const EdgeRowRec *erow;    // 64 * S records
+  const EdgeColRec *ecol;    // 64 * S records
   const ColRec *cols;        // 64 * NW records; records >= N are all kNone
   const uint64_t *rowmask;   // M x NW words: bit c of row j <=> H(j, c) == 1
   int M, N, E, KB, rs;       // rs = ceil(M / 64)
@@ -58,12 +63,20 @@ struct DecodeArgs {
   int32_t *iters;            // B       (optional)
   int32_t *synd;             // B       (optional)
   float *llr;                // B x N   (optional)
+  // persistent scheduling: `waves` resident waves take frames 0..waves-1,
+  // then pull the next frame index from *ticket.  Tickets are a ring owned by
+  // the context: this launch's slot was zeroed by the previous launch on the
+  // stream (or at context creation), and this launch zeroes ticket_next.
+  uint32_t *ticket;
+  uint32_t *ticket_next;
+  int waves;
 };
 
 // Launch one decode (host side, implemented in ldpc_kernels.hip).
 // method: 0 min-sum, 1 sum-product, 2 bit-flip, 3 hard; prec 0 f64, 1 f32;
 // slots = ceil(E/64); nw = 1 or 4 (hard-decision words).
+// waves_per_cu (0 = default) sets the number of persistent waves.
 int launch_decode(const CodeView &code, const DecodeArgs &args, int method,
-                  int prec, int slots, int nw, void *stream);
+                  int prec, int slots, int nw, int waves_per_cu, void *stream);
 
 }  // namespace ldpc

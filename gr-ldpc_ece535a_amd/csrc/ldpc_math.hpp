@@ -1,0 +1,345 @@
+// ldpc_math.hpp -- double-precision tanh / expm1 / log for the decode kernels.
+//
+// The reference's check-node update calls glibc's tanh and log
+// (lib/ldpc_decoder_cb_impl.cc:509, :513).  ROCm's ocml versions cost 165 and
+// 98 VALU instructions on gfx950; the ones below are the classic fdlibm
+// algorithms (Sun Microsystems, 1993, freely distributable), which is also
+// what glibc's double tanh/expm1 are, written as straight-line double
+// arithmetic without fused multiply-add so host and device round alike:
+//   * tanh_f64 / expm1_f64: fdlibm s_tanh.c / s_expm1.c -- tests/test_math.py
+//     checks them bit for bit against the host libm on the decoder's range;
+//   * log_f64: fdlibm e_log.c (< 1 ulp).  glibc >= 2.28 uses a table-driven
+//     log instead, so results can differ from the oracle's in the last bit.
+// Header-only, __host__ __device__ so the CPU tests run the same code.
+#pragma once
+
+#include <stdint.h>
+#include <string.h>
+
+#ifndef LDPC_HD
+#if defined(__HIPCC__)
+#define LDPC_HD __host__ __device__ __forceinline__
+#else
+#define LDPC_HD inline
+#endif
+#endif
+
+namespace ldpc {
+namespace fm {
+
+LDPC_HD uint32_t hi_word(double x) {
+  uint64_t u;
+  memcpy(&u, &x, 8);
+  return (uint32_t)(u >> 32);
+}
+LDPC_HD uint32_t lo_word(double x) {
+  uint64_t u;
+  memcpy(&u, &x, 8);
+  return (uint32_t)u;
+}
+LDPC_HD double from_words(uint32_t hi, uint32_t lo) {
+  const uint64_t u = ((uint64_t)hi << 32) | lo;
+  double x;
+  memcpy(&x, &u, 8);
+  return x;
+}
+LDPC_HD double with_hi(double x, uint32_t hi) { return from_words(hi, lo_word(x)); }
+
+// fdlibm s_expm1.c (polynomial grouped as in glibc's copy)
+LDPC_HD double expm1_f64(double x) {
+  const double o_threshold = 7.09782712893383973096e+02;
+  const double ln2_hi = 6.93147180369123816490e-01;
+  const double ln2_lo = 1.90821492927058770002e-10;
+  const double invln2 = 1.44269504088896338700e+00;
+  const double Q1 = -3.33333333333331316428e-02;
+  const double Q2 = 1.58730158725481460165e-03;
+  const double Q3 = -7.93650757867487942473e-05;
+  const double Q4 = 4.00821782732936239552e-06;
+  const double Q5 = -2.01099218183624371326e-07;
+  double y, hi, lo, c = 0.0, t, e, hxs, hfx, r1, twopk;
+  int k;
+  uint32_t hx = hi_word(x);
+  const uint32_t xsb = hx & 0x80000000u;
+  hx &= 0x7fffffffu;
+  if (hx >= 0x4043687Au) {  // |x| >= 56 ln2
+    if (hx >= 0x40862E42u) {  // |x| >= 709.78
+      if (hx >= 0x7ff00000u) {
+        if (((hx & 0xfffffu) | lo_word(x)) != 0) return x + x;  // NaN
+        return xsb == 0 ? x : -1.0;                             // exp(+-inf)-1
+      }
+      if (x > o_threshold) return __builtin_inf();
+    }
+    if (xsb != 0) return -1.0;  // x < -56 ln2
+  }
+  if (hx > 0x3fd62e42u) {  // |x| > 0.5 ln2
+    if (hx < 0x3FF0A2B2u) {  // and |x| < 1.5 ln2
+      if (xsb == 0) {
+        hi = x - ln2_hi;
+        lo = ln2_lo;
+        k = 1;
+      } else {
+        hi = x + ln2_hi;
+        lo = -ln2_lo;
+        k = -1;
+      }
+    } else {
+      k = (int)(invln2 * x + ((xsb == 0) ? 0.5 : -0.5));
+      t = k;
+      hi = x - t * ln2_hi;  // t*ln2_hi is exact here
+      lo = t * ln2_lo;
+    }
+    x = hi - lo;
+    c = (hi - x) - lo;
+  } else if (hx < 0x3c900000u) {  // |x| < 2^-54
+    return x;
+  } else {
+    k = 0;
+  }
+  hfx = 0.5 * x;
+  hxs = x * hfx;
+  // Estrin form, as glibc evaluates it (a Horner form differs in the last bit)
+  const double R1 = 1.0 + hxs * Q1, h2 = hxs * hxs;
+  const double R2 = Q2 + hxs * Q3, h4 = h2 * h2;
+  const double R3 = Q4 + hxs * Q5;
+  r1 = R1 + h2 * R2 + h4 * R3;
+  t = 3.0 - r1 * hfx;
+  e = hxs * ((r1 - t) / (6.0 - x * t));
+  if (k == 0) return x - (x * e - hxs);
+  twopk = from_words((uint32_t)(0x3ff + k) << 20, 0);  // 2^k
+  e = (x * (e - c) - c);
+  e -= hxs;
+  if (k == -1) return 0.5 * (x - e) - 0.5;
+  if (k == 1) {
+    if (x < -0.25) return -2.0 * (e - (x + 0.5));
+    return 1.0 + 2.0 * (x - e);
+  }
+  if (k <= -2 || k > 56) {  // exp(x)-1 suffices
+    y = 1.0 - (e - x);
+    if (k == 1024)
+      y = y * 2.0 * 8.98846567431157953865e+307;  // 2^1023
+    else
+      y = y * twopk;
+    return y - 1.0;
+  }
+  if (k < 20) {
+    t = from_words(0x3ff00000u - (0x200000u >> k), 0);  // 1 - 2^-k
+    y = t - (e - x);
+    y = y * twopk;
+  } else {
+    t = from_words((uint32_t)(0x3ff - k) << 20, 0);  // 2^-k
+    y = x - (e + t);
+    y += 1.0;
+    y = y * twopk;
+  }
+  return y;
+}
+
+// fdlibm s_tanh.c
+LDPC_HD double tanh_f64(double x) {
+  const int32_t jx = (int32_t)hi_word(x);
+  const uint32_t ix = (uint32_t)jx & 0x7fffffffu;
+  double t, z;
+  if (ix >= 0x7ff00000u) {  // inf or NaN
+    if (jx >= 0) return 1.0 / x + 1.0;
+    return 1.0 / x - 1.0;
+  }
+  if (ix < 0x40360000u) {  // |x| < 22
+    if (ix < 0x3c800000u) return x * (1.0 + x);  // |x| < 2^-55
+    if (ix >= 0x3ff00000u) {                       // |x| >= 1
+      t = expm1_f64(2.0 * __builtin_fabs(x));
+      z = 1.0 - 2.0 / (t + 2.0);
+    } else {
+      t = expm1_f64(-2.0 * __builtin_fabs(x));
+      z = -t / (t + 2.0);
+    }
+  } else {
+    z = 1.0;  // |x| >= 22
+  }
+  return jx >= 0 ? z : -z;
+}
+
+// fdlibm e_log.c
+LDPC_HD double log_f64(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01;
+  const double ln2_lo = 1.90821492927058770002e-10;
+  const double two54 = 1.80143985094819840000e+16;
+  const double Lg1 = 6.666666666666735130e-01;
+  const double Lg2 = 3.999999999940941908e-01;
+  const double Lg3 = 2.857142874366239149e-01;
+  const double Lg4 = 2.222219843214978396e-01;
+  const double Lg5 = 1.818357216161805012e-01;
+  const double Lg6 = 1.531383769920937332e-01;
+  const double Lg7 = 1.479819860511658591e-01;
+  int32_t hx = (int32_t)hi_word(x);
+  const uint32_t lx = lo_word(x);
+  int32_t k = 0;
+  if (hx < 0x00100000) {  // x < 2^-1022
+    if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -__builtin_inf();  // log(+-0)
+    if (hx < 0) return (x - x) / 0.0;  // log(-#) = NaN
+    k -= 54;
+    x *= two54;  // subnormal: scale up
+    hx = (int32_t)hi_word(x);
+  }
+  if (hx >= 0x7ff00000) return x + x;
+  k += (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i = (hx + 0x95f64) & 0x100000;
+  x = with_hi(x, (uint32_t)(hx | (i ^ 0x3ff00000)));  // normalize x or x/2
+  k += (i >> 20);
+  const double f = x - 1.0;
+  const double dk = (double)k;
+  if ((0x000fffff & (2 + hx)) < 3) {  // -2^-20 <= f < 2^-20
+    if (f == 0.0) return dk * ln2_hi + dk * ln2_lo;
+    const double R = f * f * (0.5 - 0.33333333333333333 * f);
+    return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+  }
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  int32_t ii = hx - 0x6147a;
+  const double w = z * z;
+  const int32_t j = 0x6b851 - hx;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  ii |= j;
+  const double R = t2 + t1;
+  if (ii > 0) {
+    const double hfsq = 0.5 * f * f;
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  }
+  return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+// ---------------------------------------------------------------------------
+// Branch-free restatements for the GPU: every path of the functions above is
+// evaluated and the result selected, so divergent lanes do not serialise.
+// Same operations in the same order, hence the same results (checked bit for
+// bit against the branchy versions by tests/test_math.py).
+// ---------------------------------------------------------------------------
+
+LDPC_HD double sel(bool c, double a, double b) { return c ? a : b; }
+
+// expm1 for -56 ln2 < x < 709.78 (the range tanh_f64_bf feeds it; any other
+// finite input returns an unspecified value that the caller discards).
+LDPC_HD double expm1_f64_bf(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01;
+  const double ln2_lo = 1.90821492927058770002e-10;
+  const double invln2 = 1.44269504088896338700e+00;
+  const double Q1 = -3.33333333333331316428e-02;
+  const double Q2 = 1.58730158725481460165e-03;
+  const double Q3 = -7.93650757867487942473e-05;
+  const double Q4 = 4.00821782732936239552e-06;
+  const double Q5 = -2.01099218183624371326e-07;
+  const uint32_t hw = hi_word(x);
+  const bool neg = (hw & 0x80000000u) != 0;
+  const uint32_t hx = hw & 0x7fffffffu;
+  const double x0 = x;
+  // argument reduction: k = 0 (|x| <= 0.5 ln2), +-1 (< 1.5 ln2), else round
+  const int kgen = (int)(invln2 * x + (neg ? -0.5 : 0.5));
+  int k = hx < 0x3FF0A2B2u ? (neg ? -1 : 1) : kgen;
+  k = hx > 0x3fd62e42u ? k : 0;
+  const double tk = (double)k;
+  const double hi = x - tk * ln2_hi;  // k == 0: hi == x, lo == 0, c == 0
+  const double lo = tk * ln2_lo;
+  x = hi - lo;
+  const double c = (hi - x) - lo;
+  const double hfx = 0.5 * x;
+  const double hxs = x * hfx;
+  const double R1 = 1.0 + hxs * Q1, h2 = hxs * hxs;
+  const double R2 = Q2 + hxs * Q3, h4 = h2 * h2;
+  const double R3 = Q4 + hxs * Q5;
+  const double r1 = R1 + h2 * R2 + h4 * R3;
+  double t = 3.0 - r1 * hfx;
+  double e = hxs * ((r1 - t) / (6.0 - x * t));
+  const double res0 = x - (x * e - hxs);  // k == 0
+  const int kc = k < -1022 ? -1022 : (k > 1023 ? 1023 : k);
+  const double twopk = from_words((uint32_t)(0x3ff + kc) << 20, 0);
+  e = (x * (e - c) - c);
+  e -= hxs;
+  const double resm1 = 0.5 * (x - e) - 0.5;                                   // k == -1
+  const double resp1 = sel(x < -0.25, -2.0 * (e - (x + 0.5)), 1.0 + 2.0 * (x - e));  // k == 1
+  const double resbig = (1.0 - (e - x)) * twopk - 1.0;  // k <= -2 || k > 56
+  const int klo = k < 1 ? 1 : (k > 19 ? 19 : k);
+  const double t20 = from_words(0x3ff00000u - (0x200000u >> klo), 0);  // 1 - 2^-k
+  const double reslt20 = (t20 - (e - x)) * twopk;                      // 2 <= k < 20
+  const int khi = k < 20 ? 20 : (k > 56 ? 56 : k);
+  const double tm = from_words((uint32_t)(0x3ff - khi) << 20, 0);  // 2^-k
+  double yge = x - (e + tm);
+  yge += 1.0;
+  const double resge20 = yge * twopk;  // 20 <= k <= 56
+  double r = sel(k < 20, reslt20, resge20);
+  r = sel(k <= -2 || k > 56, resbig, r);
+  r = sel(k == 1, resp1, r);
+  r = sel(k == -1, resm1, r);
+  r = sel(k == 0, res0, r);
+  return sel(hx < 0x3c900000u, x0, r);  // |x| < 2^-54
+}
+
+LDPC_HD double tanh_f64_bf(double x) {
+  const int32_t jx = (int32_t)hi_word(x);
+  const uint32_t ix = (uint32_t)jx & 0x7fffffffu;
+  const double a = __builtin_fabs(x);
+  const bool big = ix >= 0x3ff00000u;  // |x| >= 1
+  // |x| < 22 keeps the expm1 argument inside expm1_f64_bf's range
+  const double arg = ix < 0x40360000u ? (big ? 2.0 * a : -2.0 * a) : 0.0;
+  const double t = expm1_f64_bf(arg);
+  const double q = (big ? 2.0 : -t) / (t + 2.0);
+  double z = big ? 1.0 - q : q;
+  z = ix < 0x40360000u ? z : 1.0;
+  z = jx >= 0 ? z : -z;
+  z = ix < 0x3c800000u ? x * (1.0 + x) : z;
+  const double special = jx >= 0 ? 1.0 / x + 1.0 : 1.0 / x - 1.0;  // +-inf, NaN
+  return ix >= 0x7ff00000u ? special : z;
+}
+
+LDPC_HD double log_f64_bf(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01;
+  const double ln2_lo = 1.90821492927058770002e-10;
+  const double two54 = 1.80143985094819840000e+16;
+  const double Lg1 = 6.666666666666735130e-01;
+  const double Lg2 = 3.999999999940941908e-01;
+  const double Lg3 = 2.857142874366239149e-01;
+  const double Lg4 = 2.222219843214978396e-01;
+  const double Lg5 = 1.818357216161805012e-01;
+  const double Lg6 = 1.531383769920937332e-01;
+  const double Lg7 = 1.479819860511658591e-01;
+  const double x_in = x;
+  const int32_t hx0 = (int32_t)hi_word(x);
+  const uint32_t lx0 = lo_word(x);
+  const bool zero = ((hx0 & 0x7fffffff) | (int32_t)lx0) == 0;
+  const bool tiny = hx0 < 0x00100000;  // subnormal, zero or negative
+  x = tiny ? x * two54 : x;
+  int32_t k = tiny ? -54 : 0;
+  int32_t hx = (int32_t)hi_word(x);
+  k += (hx >> 20) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i = (hx + 0x95f64) & 0x100000;
+  x = with_hi(x, (uint32_t)(hx | (i ^ 0x3ff00000)));
+  k += (i >> 20);
+  const double f = x - 1.0;
+  const double dk = (double)k;
+  // |f| < 2^-20
+  const double Rs = f * f * (0.5 - 0.33333333333333333 * f);
+  double rsmall = dk * ln2_hi - ((Rs - dk * ln2_lo) - f);
+  rsmall = f == 0.0 ? dk * ln2_hi + dk * ln2_lo : rsmall;
+  // general
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  int32_t ii = hx - 0x6147a;
+  const double w = z * z;
+  const int32_t j = 0x6b851 - hx;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  ii |= j;
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double rpos = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  const double rneg = dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+  double r = ii > 0 ? rpos : rneg;
+  r = (0x000fffff & (2 + hx)) < 3 ? rsmall : r;
+  r = hx0 >= 0x7ff00000 ? x_in + x_in : r;       // +inf, NaN
+  r = hx0 < 0 && !zero ? (x_in - x_in) / 0.0 : r;  // negative: NaN
+  return zero ? -__builtin_inf() : r;
+}
+
+}  // namespace fm
+}  // namespace ldpc

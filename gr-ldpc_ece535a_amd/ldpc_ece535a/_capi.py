@@ -43,6 +43,7 @@ SIGNATURES = {
                                  _u8p, _u8p, _i32p, _i32p, _f32p]),
     "ldpc_decode_device": (_i, [_vp, _i, _i, _i, _i, _vp, _i64, _i, ctypes.c_float, _i,
                                 _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ldpc_set_waves_per_cu": (_i, [_vp, _i]),
     "ldpc_synchronize": (_i, [_vp]),
 }
 
@@ -186,6 +187,9 @@ class Decoder:
                                         int(precision), d_in, int(cw_stride), int(elem_stride),
                                         float(polarity), int(B), d_packed, d_bits, d_iters,
                                         d_synd, d_llr, stream), self._ctx)
+
+    def set_waves_per_cu(self, n):
+        _check(lib().ldpc_set_waves_per_cu(self._ctx, int(n)), self._ctx)
 
     def synchronize(self):
         _check(lib().ldpc_synchronize(self._ctx), self._ctx)

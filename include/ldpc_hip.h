@@ -146,6 +146,10 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
                        int32_t *d_iters_used_opt, int32_t *d_syn_weight_opt,
                        float *d_llr_out_opt, void *hip_stream);
 
+/* Tuning: persistent waves per CU for the decode kernel (0 = default).
+ * Frames are pulled from a per-launch queue by that many resident waves. */
+int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu);
+
 /* Blocks until the context's stream is idle. */
 int ldpc_synchronize(ldpc_ctx *ctx);
 

@@ -1,0 +1,55 @@
+// Host check of gr-ldpc_ece535a_amd/csrc/ldpc_math.hpp against the host libm
+// (glibc: what the oracle and the reference call).  Built by tests/test_math.py.
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../../gr-ldpc_ece535a_amd/csrc/ldpc_math.hpp"
+
+static uint64_t bits(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
+
+static int64_t ulps(double a, double b) {
+  if (a != a && b != b) return 0;
+  if (bits(a) == bits(b)) return 0;
+  int64_t ia = (int64_t)bits(a), ib = (int64_t)bits(b);
+  if (ia < 0) ia = (int64_t)0x8000000000000000ull - ia;
+  if (ib < 0) ib = (int64_t)0x8000000000000000ull - ib;
+  int64_t d = ia - ib;
+  return d < 0 ? -d : d;
+}
+
+extern "C" {
+// fn: 0 tanh, 1 expm1, 2 log.  out[0] = #bit mismatches, out[1] = max ulp.
+void check_fn(int fn, const double *x, int64_t n, int64_t *out) {
+  int64_t mism = 0, maxu = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double a, b;
+    if (fn == 0) { a = ldpc::fm::tanh_f64(x[i]); b = tanh(x[i]); }
+    else if (fn == 1) { a = ldpc::fm::expm1_f64(x[i]); b = expm1(x[i]); }
+    else { a = ldpc::fm::log_f64(x[i]); b = log(x[i]); }
+    int64_t u = ulps(a, b);
+    if (u) ++mism;
+    if (u > maxu) maxu = u;
+  }
+  out[0] = mism; out[1] = maxu;
+}
+void eval_fn(int fn, const double *x, int64_t n, double *y) {
+  for (int64_t i = 0; i < n; ++i)
+    y[i] = fn == 0 ? ldpc::fm::tanh_f64(x[i]) : fn == 1 ? ldpc::fm::expm1_f64(x[i])
+                                                          : ldpc::fm::log_f64(x[i]);
+}
+}
+extern "C" {
+// branch-free vs branchy: fn 0 tanh, 1 expm1 (restricted range), 2 log.
+void check_bf(int fn, const double *x, int64_t n, int64_t *out) {
+  int64_t mism = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double a, b;
+    if (fn == 0) { a = ldpc::fm::tanh_f64_bf(x[i]); b = ldpc::fm::tanh_f64(x[i]); }
+    else if (fn == 1) { a = ldpc::fm::expm1_f64_bf(x[i]); b = ldpc::fm::expm1_f64(x[i]); }
+    else { a = ldpc::fm::log_f64_bf(x[i]); b = ldpc::fm::log_f64(x[i]); }
+    if (ulps(a, b)) ++mism;
+  }
+  out[0] = mism;
+}
+}
