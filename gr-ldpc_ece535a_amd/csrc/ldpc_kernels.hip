@@ -4,21 +4,25 @@
 // ldpc_decoder_cb_impl::general_work (lib/ldpc_decoder_cb_impl.cc:155-164).
 //
 // Mapping ("small code" kernel, N <= 256, E <= 512, dc <= 8, dv <= 4):
-//   * one 64-lane wave decodes one frame; 4 independent waves per 256-thread
-//     workgroup, each with a private LDS slice, no workgroup barrier after the
-//     prologue, so every wave leaves its iteration loop on its own syndrome
-//     (per-frame early termination exactly as the reference);
+//   * one 64-lane wave decodes one frame at a time; 4 independent waves per
+//     256-thread workgroup, each with a private LDS slice; a wave leaves its
+//     iteration loop on its own syndrome (per-frame early termination exactly
+//     as the reference) and pulls the next frame from a launch-wide queue;
 //   * lane l owns edges l, l+64, ... (S slots): its variable->check message
-//     lives in VGPRs across iterations, only the per-iteration exchange goes
+//     lives in VGPRs across iterations; the per-iteration exchange goes
 //     through LDS (tanh values for the check pass, check->variable messages
 //     for the column sums);
+//   * every LDS gather is unconditional: unused neighbour entries point at a
+//     per-wave dummy element holding the operation's identity (1.0 for the
+//     tanh product, DBL_MAX for the min-sum minimum), or their contribution
+//     is dropped with a select -- so a lane's loads issue back to back and the
+//     wave waits once per phase instead of once per neighbour;
 //   * lane l also owns columns l, l+64, ... for the hard decision; the hard
-//     decision vector is a 64-bit wave ballot per 64 columns, and the
-//     syndrome is popcount(rowmask & hard) per row lane + one more ballot;
-//   * the only HBM traffic per frame is the N input samples, the packed
-//     output and the optional per-frame outputs.
+//     decision is a 64-bit wave ballot per 64 columns, the syndrome is
+//     popcount(rowmask & hard) per row lane + one more ballot;
+//   * per frame the only HBM traffic is its N input samples and its outputs.
 // Arithmetic follows the reference operation for operation (same operand
-// order, no contraction: build with -ffp-contract=off), in double
+// order, no contraction: built with -ffp-contract=off), in double
 // (LDPC_PREC_F64) or float (LDPC_PREC_F32).
 #include <hip/hip_runtime.h>
 
@@ -73,69 +77,57 @@ template <int NW>
 __device__ __forceinline__ uint64_t word_at(const uint64_t (&w)[NW], int idx) {
   uint64_t r = w[0];
 #pragma unroll
-  for (int q = 1; q < NW; ++q)
-    if (idx == q) r = w[q];
+  for (int q = 1; q < NW; ++q) r = idx == q ? w[q] : r;
   return r;
 }
 
-__device__ __forceinline__ uint64_t word4_at(const uint64_t (&w)[4], int idx) {
-  uint64_t r = w[0];
-  r = idx == 1 ? w[1] : r;
-  r = idx == 2 ? w[2] : r;
-  r = idx == 3 ? w[3] : r;
-  return r;
+// Hides a register value from loop-invariant code motion: the unpacked
+// neighbour indices are then recomputed (two ALU ops each) inside the
+// iteration loop instead of being hoisted and held live (~30 VGPRs).
+template <int W>
+__device__ __forceinline__ void opaque(uint32_t (&p)[W]) {
+#pragma unroll
+  for (int k = 0; k < W; ++k) asm volatile("" : "+v"(p[k]));
 }
 
-// Unsatisfied checks of the hard decision `hard` (checkFrame :236-253 with
-// an unreachable threshold): row lane j XORs popcount(rowmask_j & hard),
-// one ballot per 64 rows gathers the odd rows.
-template <int NW>
-__device__ __forceinline__ int syndrome_weight(const uint64_t (&hard)[NW],
-                                               const uint64_t *rowmask, int M,
-                                               int rs, int lane) {
-  int weight = 0;
-#pragma unroll
-  for (int q = 0; q < kMMax / 64; ++q) {
-    if (q < rs) {
-      const int j = lane + 64 * q;
-      int odd = 0;
-      if (j < M) {
-#pragma unroll
-        for (int w = 0; w < NW; ++w) odd ^= __popcll(rowmask[j * NW + w] & hard[w]);
-        odd &= 1;
-      }
-      weight += __popcll(__ballot(odd));
-    }
-  }
-  return weight;
+// 16-bit field k of a packed record held in registers
+template <int W>
+__device__ __forceinline__ int field(const uint32_t (&p)[W], int k) {
+  return (int)((p[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
 }
 
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// Block LDS: [rowmask M x NW][row recs 64S][col-neighbour recs 64S]
-// [column recs 64 NW] then one slice per wave [tb 64S][eb 64S][rb 64NW][sb 64NW].
+// Per-wave LDS slice (the workgroup's waves never share LDS):
+//   tb[64S + 2]  check-pass operand per edge (+ dummy at 64S)
+//   eb[64S + 2]  check->variable message per edge (+ dummy at 64S)
+//   rb[64 NW]    -tx per column;  sb[64 NW] min-sum column totals
 template <typename Real, int S, int NW>
 struct Layout {
-  size_t erow, ecol, cols, waves, per_wave, total;
-  __host__ __device__ explicit Layout(int M) {
-    erow = align16((size_t)M * NW * 8);
-    ecol = erow + (size_t)64 * S * sizeof(EdgeRowRec);
-    cols = ecol + (size_t)64 * S * sizeof(EdgeColRec);
-    waves = align16(cols + (size_t)64 * NW * sizeof(ColRec));
-    per_wave = (2 * 64 * S + 2 * 64 * NW) * sizeof(Real);
-    total = waves + (size_t)kWavesPerBlock * per_wave;
+  size_t per_wave, total;
+  __host__ __device__ Layout() {
+    per_wave = align16((2 * (64 * S + 2) + 2 * 64 * NW) * sizeof(Real));
+    total = (size_t)kWavesPerBlock * per_wave;
   }
 };
 
-// Decodes frame b with the wave's resident tables (er/cr) and LDS slice.
+// Per-wave register-resident view of the code (packed 16-bit edge ids).
+template <int S, int NW>
+struct WaveTables {
+  uint32_t rn[S][4];   // rn[0..6] of EdgeRowRec, col in the last half-word
+  uint32_t cn[S][2];   // cn[0..2] of EdgeColRec, col in the last half-word
+  uint32_t ce[NW][2];  // ColRec.e[0..3]
+  uint32_t cr[NW][2];  // ColRec.r[0..3] (bit-flip only)
+  uint64_t rowmask[NW][NW];  // rows lane + 64 q, words k (M < N <= 64 NW)
+};
+
 template <typename Real, int METHOD, int S, int NW>
 __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeArgs &a,
-                                             const int64_t b, const int (&col)[S],
-                                             const EdgeRowRec *erow, const EdgeColRec *ecol,
-                                             const ColRec *cols, const uint64_t *rowmask,
+                                             const int64_t b, WaveTables<S, NW> &wt,
                                              Real *tb, Real *eb, Real *rb, Real *sb,
                                              const int lane) {
   const int M = code.M, N = code.N;
+  constexpr int kDummy = 64 * S;  // index of the per-wave identity element
   // Channel samples: tx = Re(in) * polarity (:149-153); r = -tx (:486,
   // :318-321).  Lane l reads sample l of each 64-column slot (coalesced).
   const float *src = a.in + b * a.cw_stride;
@@ -154,134 +146,153 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
   for (int q = 0; q < NW; ++q) hard[q] = 0;
   int weight = 0, used = 0;
 
+  auto syndrome = [&]() {
+    int w = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      int odd = 0;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) odd ^= __popcll(wt.rowmask[q][k] & hard[k]);
+      w += __popcll(__ballot((odd & 1) != 0 && lane + 64 * q < M));
+    }
+    return w;
+  };
+
   if constexpr (METHOD == 1 || METHOD == 0) {
-    wave_lds_sync();  // rb visible to every lane
+    if (lane == 0) tb[kDummy] = METHOD == 1 ? Real(1) : Math<Real>::max_();
+    int col[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      col[s] = field(wt.rn[s], 7);
+      col[s] = col[s] != kNone ? col[s] : 0;  // padding edges: any column
+    }
+    wave_lds_sync();  // rb and the dummy visible to every lane
     Real msg[S];      // SP: M(j,i) (:489-496); min-sum: L(q_ij) (:328-331)
     Real lr[S];       // min-sum: L(r_ji)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      msg[s] = col[s] != kNone ? rb[col[s]] : Real(0);
+      msg[s] = rb[col[s]];
       lr[s] = Real(0);
     }
 
     for (int h = 0; h < a.max_iters; ++h) {
-      if constexpr (METHOD == 1) {
-        // ---- check pass, :503-516 -----------------------------------
 #pragma unroll
-        for (int s = 0; s < S; ++s)
-          if (col[s] != kNone) tb[lane + 64 * s] = Math<Real>::tanh_(msg[s] / Real(2));
-        wave_lds_sync();
+      for (int s = 0; s < S; ++s) {
+        opaque(wt.rn[s]);
+        opaque(wt.cn[s]);
+      }
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-          if (col[s] != kNone) {
-            const EdgeRowRec er = erow[lane + 64 * s];
-            Real T = Real(1);
+      for (int q = 0; q < NW; ++q) opaque(wt.ce[q]);
+      // ---- check-pass operand of every edge -> LDS ----------------------
 #pragma unroll
-            for (int k = 0; k < kDcMax - 1; ++k) {
-              const int n = er.rn[k];
-              if (n != kNone) T = T * tb[n];
-            }
-            eb[lane + 64 * s] = Math<Real>::log_((Real(1) + T) / (Real(1) - T));
-          }
+      for (int s = 0; s < S; ++s) {
+        if constexpr (METHOD == 1)
+          tb[lane + 64 * s] = Math<Real>::tanh_(msg[s] / Real(2));  // :509
+        else
+          tb[lane + 64 * s] = msg[s];
+      }
+      wave_lds_sync();
+      // gather the row neighbours of every slot (unconditional loads)
+      Real nb[S][kDcMax - 1];
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int k = 0; k < kDcMax - 1; ++k) {
+          const int n = field(wt.rn[s], k);
+          nb[s][k] = tb[n == kNone ? kDummy : n];
         }
-        wave_lds_sync();
-        // ---- decision, :519-532: L = sum_j (E(j,i) + r(i)), 1 iff L <= 0
 #pragma unroll
-        for (int q = 0; q < NW; ++q) {
-          const int c = lane + 64 * q;
-          bool bit = false;
-          if (c < N) {
-            const ColRec cr = cols[c];
-            const Real rc = rb[c];
-            Real L = Real(0);
+      for (int s = 0; s < S; ++s) {
+        if constexpr (METHOD == 1) {
+          // T = prod_{k != i} tanh(M(j,k)/2), ascending k; E = log((1+T)/(1-T))
+          // (:506-513).  Padding neighbours read the 1.0 dummy: exact no-op.
+          Real T = Real(1);
 #pragma unroll
-            for (int k = 0; k < kDvMax; ++k) {
-              const int n = cr.e[k];
-              if (n != kNone) L = L + (eb[n] + rc);
-            }
-            bit = L <= Real(0);
-            post[q] = L;
+          for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[s][k];
+          eb[lane + 64 * s] = Math<Real>::log_((Real(1) + T) / (Real(1) - T));
+        } else {
+          // min-sum horizontal step (:350-376): sign product over the row
+          // times the minimum |L(q)| of the other edges.  Padding neighbours
+          // read DBL_MAX: sign +1, never below the running minimum.
+          const int self = sgn(msg[s]);
+          int prod = self;
+          Real lo = Math<Real>::max_();
+#pragma unroll
+          for (int k = 0; k < kDcMax - 1; ++k) {
+            prod *= sgn(nb[s][k]);
+            const Real beta = Math<Real>::abs_(nb[s][k]);
+            lo = beta < lo ? beta : lo;
           }
-          hard[q] = __ballot(bit);
+          lr[s] = (Real)(prod * self) * lo;
+          eb[lane + 64 * s] = lr[s];
         }
-      } else {
-        // ---- min-sum horizontal step, :340-376 ----------------------
+      }
+      wave_lds_sync();
+      // ---- per-column totals and the hard decision ----------------------
 #pragma unroll
-        for (int s = 0; s < S; ++s)
-          if (col[s] != kNone) tb[lane + 64 * s] = msg[s];
-        wave_lds_sync();
+      for (int q = 0; q < NW; ++q) {
+        const int c = lane + 64 * q;
+        Real ev[kDvMax];
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-          if (col[s] != kNone) {
-            const EdgeRowRec er = erow[lane + 64 * s];
-            const int self = sgn(msg[s]);
-            int prod = self;
-            Real lo = Math<Real>::max_();
-#pragma unroll
-            for (int k = 0; k < kDcMax - 1; ++k) {
-              const int n = er.rn[k];
-              if (n != kNone) {
-                const Real v = tb[n];
-                prod *= sgn(v);
-                const Real beta = Math<Real>::abs_(v);
-                if (beta < lo) lo = beta;
-              }
-            }
-            lr[s] = (Real)(prod * self) * lo;
-            eb[lane + 64 * s] = lr[s];
-          }
+        for (int k = 0; k < kDvMax; ++k) {
+          const int n = field(wt.ce[q], k);
+          ev[k] = eb[n == kNone ? kDummy : n];
         }
-        wave_lds_sync();
-        // ---- vertical step, :379-403: s = sum_i L(r_ji); L(Q) = Lci + s
+        const Real rc = rb[c];
+        Real acc = Real(0);
+        bool bit;
+        if constexpr (METHOD == 1) {
+          // L = sum_j (E(j,i) + r(i)), ascending j; 1 iff L <= 0 (:519-532)
 #pragma unroll
-        for (int q = 0; q < NW; ++q) {
-          const int c = lane + 64 * q;
-          bool bit = false;
-          if (c < N) {
-            const ColRec cr = cols[c];
-            Real acc = Real(0);
+          for (int k = 0; k < kDvMax; ++k)
+            acc = field(wt.ce[q], k) != kNone ? acc + (ev[k] + rc) : acc;
+          bit = acc <= Real(0);
+          post[q] = acc;
+        } else {
+          // s = sum_i L(r_ji) (:380-385); L(Q) = Lci + s; 1 iff L(Q) < 0 (:395-402)
 #pragma unroll
-            for (int k = 0; k < kDvMax; ++k) {
-              const int n = cr.e[k];
-              if (n != kNone) acc = acc + eb[n];
-            }
-            const Real LQ = rb[c] + acc;
-            sb[c] = LQ;
-            bit = LQ < Real(0);
-            post[q] = LQ;
-          }
-          hard[q] = __ballot(bit);
+          for (int k = 0; k < kDvMax; ++k)
+            acc = field(wt.ce[q], k) != kNone ? acc + ev[k] : acc;
+          const Real LQ = rc + acc;
+          sb[c] = LQ;
+          bit = LQ < Real(0);
+          post[q] = LQ;
         }
+        hard[q] = __ballot(bit && c < N);
       }
       // ---- early exit: SP every iteration (:535-537); min-sum only when
       // h+1 < max_iters (:406-408); et_period > 1 thins the checks.
-      weight = syndrome_weight<NW>(hard, rowmask, M, code.rs, lane);
+      weight = syndrome();
       used = h + 1;
       if (h + 1 == a.max_iters) break;
       if ((h + 1) % a.et_period == 0 && weight == 0) break;
 
       if constexpr (METHOD == 1) {
         // ---- bit messages, :540-553: M(j,i) = sum_{k != j} (E(k,i) + r(i))
+        Real cv[S][kDvMax - 1];
+        Real rcs[S];
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          if (col[s] != kNone) {
-            const EdgeColRec ec = ecol[lane + 64 * s];
-            const Real rc = rb[col[s]];
-            Real acc = Real(0);
+          rcs[s] = rb[col[s]];
 #pragma unroll
-            for (int k = 0; k < kDvMax - 1; ++k) {
-              const int n = ec.cn[k];
-              if (n != kNone) acc = acc + (eb[n] + rc);
-            }
-            msg[s] = acc;
+          for (int k = 0; k < kDvMax - 1; ++k) {
+            const int n = field(wt.cn[s], k);
+            cv[s][k] = eb[n == kNone ? kDummy : n];
           }
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          Real acc = Real(0);
+#pragma unroll
+          for (int k = 0; k < kDvMax - 1; ++k)
+            acc = field(wt.cn[s], k) != kNone ? acc + (cv[s][k] + rcs[s]) : acc;
+          msg[s] = acc;
         }
       } else {
         wave_lds_sync();  // sb visible
         // L(q_ij) = Lci(j) + s_j - L(r_ji)  (:387-392)
 #pragma unroll
-        for (int s = 0; s < S; ++s)
-          if (col[s] != kNone) msg[s] = sb[col[s]] - lr[s];
+        for (int s = 0; s < S; ++s) msg[s] = sb[col[s]] - lr[s];
       }
     }
   } else {
@@ -293,52 +304,39 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       y[q] = __ballot(c < N && !(post[q] < Real(0)));
       hard[q] = y[q];
     }
-    weight = syndrome_weight<NW>(hard, rowmask, M, code.rs, lane);
+    weight = syndrome();
     if constexpr (METHOD == 2) {
       // ---- bit flipping, :439-473 ------------------------------------
       const int half = (int)((unsigned)M / 2u);
       for (int h = 0; h < a.max_iters; ++h) {
         // parity of ci over each row; E(i,j) for an edge = parity ^ ci(j)
-        uint64_t rowpar[4];
+        uint64_t rowpar[NW];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          rowpar[q] = 0;
-          if (q < code.rs) {
-            const int j = lane + 64 * q;
-            int odd = 0;
-            if (j < M) {
+        for (int q = 0; q < NW; ++q) {
+          int odd = 0;
 #pragma unroll
-              for (int w = 0; w < NW; ++w) odd ^= __popcll(rowmask[j * NW + w] & hard[w]);
-              odd &= 1;
-            }
-            rowpar[q] = __ballot(odd);
-          }
+          for (int k = 0; k < NW; ++k) odd ^= __popcll(wt.rowmask[q][k] & hard[k]);
+          rowpar[q] = __ballot((odd & 1) != 0);
         }
         uint64_t next[NW];
 #pragma unroll
         for (int q = 0; q < NW; ++q) {
           const int c = lane + 64 * q;
-          bool nb = false;
-          if (c < N) {
-            const ColRec cr = cols[c];
-            const int cib = (int)((hard[q] >> lane) & 1);
-            const int yb = (int)((y[q] >> lane) & 1);
-            int votes = 0;
+          const int cib = (int)((hard[q] >> lane) & 1);
+          const int yb = (int)((y[q] >> lane) & 1);
+          int votes = 0;
 #pragma unroll
-            for (int k = 0; k < kDvMax; ++k) {
-              if (cr.e[k] != kNone) {
-                const int r = cr.r[k];
-                const int par = (int)((word4_at(rowpar, r >> 6) >> (r & 63)) & 1);
-                if ((par ^ cib) != yb) ++votes;
-              }
-            }
-            nb = votes > half ? (yb == 0) : (cib != 0);
+          for (int k = 0; k < kDvMax; ++k) {
+            const int r = field(wt.cr[q], k);
+            const int par = (int)((word_at<NW>(rowpar, (r >> 6) & (NW - 1)) >> (r & 63)) & 1);
+            votes += (r != kNone && (par ^ cib) != yb) ? 1 : 0;
           }
-          next[q] = __ballot(nb);
+          const bool nb = votes > half ? (yb == 0) : (cib != 0);
+          next[q] = __ballot(nb && c < N);
         }
 #pragma unroll
         for (int q = 0; q < NW; ++q) hard[q] = next[q];
-        weight = syndrome_weight<NW>(hard, rowmask, M, code.rs, lane);
+        weight = syndrome();
         used = h + 1;
         if (h + 1 == a.max_iters) break;
         if ((h + 1) % a.et_period == 0 && weight == 0) break;
@@ -384,37 +382,46 @@ __global__ void __launch_bounds__(kThreads)
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int M = code.M;
-  const Layout<Real, S, NW> L(M);
-
-  // Code tables into LDS, shared by the block's waves (the only workgroup
-  // barrier): row masks, per-edge neighbour records, per-column records.
-  uint64_t *rowmask = reinterpret_cast<uint64_t *>(smem);
-  EdgeRowRec *erow = reinterpret_cast<EdgeRowRec *>(smem + L.erow);
-  EdgeColRec *ecol = reinterpret_cast<EdgeColRec *>(smem + L.ecol);
-  ColRec *cols = reinterpret_cast<ColRec *>(smem + L.cols);
-  for (int t = threadIdx.x; t < M * NW; t += kThreads) rowmask[t] = code.rowmask[t];
-  for (int t = threadIdx.x; t < 64 * S; t += kThreads) {
-    erow[t] = code.erow[t];
-    ecol[t] = code.ecol[t];
-  }
-  for (int t = threadIdx.x; t < 64 * NW; t += kThreads) cols[t] = code.cols[t];
+  const Layout<Real, S, NW> L;
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.ticket_next = 0u;  // next launch's queue head
-  __syncthreads();
 
   int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave;
   if (b >= a.waves || b >= a.B) return;
 
-  Real *tb = reinterpret_cast<Real *>(smem + L.waves + (size_t)wave * L.per_wave);
-  Real *eb = tb + 64 * S;
-  Real *rb = eb + 64 * S;
-  Real *sb = rb + 64 * NW;
-  int col[S];
+  // the wave's view of the code, in registers
+  WaveTables<S, NW> wt;
 #pragma unroll
-  for (int s = 0; s < S; ++s) col[s] = erow[lane + 64 * s].col;
+  for (int s = 0; s < S; ++s) {
+    const uint4 r = reinterpret_cast<const uint4 *>(code.erow)[lane + 64 * s];
+    wt.rn[s][0] = r.x;
+    wt.rn[s][1] = r.y;
+    wt.rn[s][2] = r.z;
+    wt.rn[s][3] = r.w;
+    const uint2 c = reinterpret_cast<const uint2 *>(code.ecol)[lane + 64 * s];
+    wt.cn[s][0] = c.x;
+    wt.cn[s][1] = c.y;
+  }
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const uint4 c = reinterpret_cast<const uint4 *>(code.cols)[lane + 64 * q];
+    wt.ce[q][0] = c.x;
+    wt.ce[q][1] = c.y;
+    wt.cr[q][0] = c.z;
+    wt.cr[q][1] = c.w;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int j = lane + 64 * q;
+      wt.rowmask[q][k] = j < M ? code.rowmask[j * NW + k] : 0ull;
+    }
+  }
+
+  Real *tb = reinterpret_cast<Real *>(smem + (size_t)wave * L.per_wave);
+  Real *eb = tb + (64 * S + 2);
+  Real *rb = eb + (64 * S + 2);
+  Real *sb = rb + 64 * NW;
 
   while (b < a.B) {
-    decode_frame<Real, METHOD, S, NW>(code, a, b, col, erow, ecol, cols, rowmask, tb, eb, rb, sb,
-                                      lane);
+    decode_frame<Real, METHOD, S, NW>(code, a, b, wt, tb, eb, rb, sb, lane);
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(a.ticket, 1u);
     b = (int64_t)a.waves + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
@@ -426,20 +433,19 @@ __global__ void __launch_bounds__(kThreads)
 // ---------------------------------------------------------------------------
 template <typename Real, int METHOD, int S, int NW>
 static int launch_one(const CodeView &code, const DecodeArgs &a, hipStream_t st) {
-  const size_t lds = Layout<Real, S, NW>(code.M).total;
+  const size_t lds = Layout<Real, S, NW>().total;
   if (lds > 65536 &&
       hipFuncSetAttribute((const void *)decode_small_kernel<Real, METHOD, S, NW>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -3;
   const dim3 grid((unsigned)((a.waves + kWavesPerBlock - 1) / kWavesPerBlock));
-  hipLaunchKernelGGL((decode_small_kernel<Real, METHOD, S, NW>), grid, dim3(kThreads),
-                     lds, st, code, a);
+  hipLaunchKernelGGL((decode_small_kernel<Real, METHOD, S, NW>), grid, dim3(kThreads), lds, st,
+                     code, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 template <typename Real, int METHOD, int NW>
-static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots,
-                        hipStream_t st) {
+static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots, hipStream_t st) {
   switch (slots) {
     case 1: return launch_one<Real, METHOD, 1, NW>(code, a, st);
     case 2: return launch_one<Real, METHOD, 2, NW>(code, a, st);
@@ -454,8 +460,8 @@ static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots,
 }
 
 template <int NW>
-static int launch_nw(const CodeView &code, const DecodeArgs &a, int method, int prec,
-                     int slots, hipStream_t st) {
+static int launch_nw(const CodeView &code, const DecodeArgs &a, int method, int prec, int slots,
+                     hipStream_t st) {
   if (method == 3) return launch_one<float, 3, 1, NW>(code, a, st);
   if (method == 2) return launch_one<float, 2, 1, NW>(code, a, st);
   if (method == 1)
@@ -465,18 +471,17 @@ static int launch_nw(const CodeView &code, const DecodeArgs &a, int method, int 
                    : launch_slots<double, 0, NW>(code, a, slots, st);
 }
 
-int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int prec,
-                  int slots, int nw, int waves_per_cu, void *stream) {
+int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int prec, int slots,
+                  int nw, int waves_per_cu, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (args.B <= 0) return 0;
   DecodeArgs a = args;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (waves_per_cu <= 0) waves_per_cu = 8;
+  if (waves_per_cu <= 0) waves_per_cu = 12;
   const int64_t w = std::min<int64_t>((int64_t)a.B, (int64_t)waves_per_cu * cus);
   a.waves = (int)((w + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock);
-
   if (nw == 1) return launch_nw<1>(code, a, method, prec, slots, st);
   if (nw == 4) return launch_nw<4>(code, a, method, prec, slots, st);
   return -2;

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Summarise tools/profile.sh output: per-kernel mean duration (kernel
+trace) and mean PMC counters per dispatch.  FETCH_SIZE is doubled per
+MI355X_MICROARCH.md (gfx950 reports half of a wide coalesced read); both
+FETCH_SIZE and WRITE_SIZE are in KiB.
+
+usage: tools/parse_prof.py gpurun_out/prof/<tag> [--kernel substr] [--json out.json --key K]
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import statistics
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--kernel", default="decode_small_kernel")
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--key", default=None)
+    a = ap.parse_args()
+    res = {}
+    kt = rows(os.path.join(a.dir, "kt", "**", "*kernel_trace.csv"))
+    durs = collections.defaultdict(list)
+    for r in kt:
+        durs[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    print("== kernel trace (ns) ==")
+    for k, v in sorted(durs.items(), key=lambda kv: -sum(kv[1])):
+        print("%-90s n=%4d mean=%10.1f median=%10.1f" % (k[:90], len(v), statistics.mean(v),
+                                                          statistics.median(v)))
+        if a.kernel in k:
+            res["kernel"] = k
+            res["mean_ns"] = statistics.mean(v)
+            res["median_ns"] = statistics.median(v)
+            res["dispatches"] = len(v)
+    stats = rows(os.path.join(a.dir, "kt", "**", "*kernel_stats.csv"))
+    for r in stats:
+        if a.kernel in r.get("Name", ""):
+            print("stats:", {k: r[k] for k in r if k in ("Name", "Calls", "AverageNs", "TotalDurationNs",
+                                                           "Percentage")})
+    counters = collections.defaultdict(list)
+    for p in ("pmc1", "pmc2", "pmc3", "pmc4"):
+        for r in rows(os.path.join(a.dir, p, "**", "*counter_collection.csv")):
+            if a.kernel in r["Kernel_Name"]:
+                counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    print("== counters (mean per dispatch of %s) ==" % a.kernel)
+    pmc = {}
+    for k, v in sorted(counters.items()):
+        pmc[k] = statistics.mean(v)
+        print("%-28s %16.1f  (n=%d)" % (k, pmc[k], len(v)))
+    res["pmc"] = pmc
+    if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+        fetch = 2.0 * pmc["FETCH_SIZE"] * 1024.0  # gfx950: FETCH_SIZE reads half
+        write = pmc["WRITE_SIZE"] * 1024.0
+        res["hbm_bytes_per_launch"] = fetch + write
+        print("HBM bytes/launch (2*FETCH_SIZE + WRITE_SIZE, KiB->B): %.0f" % (fetch + write))
+    if a.json and a.key:
+        try:
+            allj = json.load(open(a.json))
+        except (OSError, ValueError):
+            allj = {}
+        allj[a.key] = res
+        json.dump(allj, open(a.json, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
