@@ -1,0 +1,43 @@
+/* -*- c++ -*- */
+/*
+ * LDPC decoder block, MI355X edition.
+ *
+ * Same public interface as gr-ldpc_ece535a's
+ * include/ldpc_ece535a/ldpc_decoder_cb.h:22-36 -- a gr::block taking
+ * gr_complex samples and producing packed data bytes, created with
+ * make(method) -- so existing flowgraphs, GRC descriptors and SWIG bindings
+ * keep working.  The decode itself runs on the GPU through the C ABI of
+ * include/ldpc_hip.h.
+ */
+#ifndef INCLUDED_LDPC_ECE535A_LDPC_DECODER_CB_H
+#define INCLUDED_LDPC_ECE535A_LDPC_DECODER_CB_H
+
+#include <gnuradio/block.h>
+#include <ldpc_ece535a/api.h>
+
+namespace gr {
+namespace ldpc_ece535a {
+
+/*!
+ * \brief LDPC decoder block
+ * \ingroup ldpc_ece535a
+ *
+ * method: 0 LogDomain (min-sum), 1 SumProduct, 2 BitFlip, 3 Hard
+ * (grc/ldpc_ece535a_ldpc_decoder_cb.xml:11-29); other values behave as 0.
+ */
+class LDPC_ECE535A_API ldpc_decoder_cb : virtual public gr::block {
+ public:
+  typedef boost::shared_ptr<ldpc_decoder_cb> sptr;
+
+  /*! The reference's factory: default 32x64 H, 5 iterations. */
+  static sptr make(const int method);
+
+  /*! Additive overload: iteration cap (the reference hard-codes 5) and
+   *  arithmetic precision (0 = f64 parity mode, 1 = f32). */
+  static sptr make(const int method, const int iterations, const int precision = 0);
+};
+
+}  // namespace ldpc_ece535a
+}  // namespace gr
+
+#endif /* INCLUDED_LDPC_ECE535A_LDPC_DECODER_CB_H */

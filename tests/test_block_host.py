@@ -1,0 +1,100 @@
+"""Host logic of the decoder block (batched windows, replayed frame-sync
+state machine, polarity retry, packing) driven on the CPU through the
+block's test seam, with the oracle as the frame decoder.  The expected
+streams come from the restated general_work (oracle/, tests/golden).
+
+The product path never takes this seam: ldpc_decoder_cb(method) always
+decodes on the GPU (tests/test_gpu_block.py runs the same streams there)."""
+import numpy as np
+import pytest
+
+import ldpc_ece535a as L
+from ldpc_ece535a import flowgraph as fg
+from oracle import oracle as orc
+
+
+def oracle_backend(method, Hr, iterations=5):
+    Hr = np.ascontiguousarray(Hr, np.uint8)
+
+    def fn(user, inp, n_floats, cw_stride, elem_stride, polarity, B, packed, synd):
+        x = np.ctypeslib.as_array(inp, shape=(int(n_floats),))
+        r = orc.decode_batch(method, Hr, x, iterations, polarity=polarity, cw_stride=cw_stride,
+                             elem_stride=elem_stride, B=B)
+        np.ctypeslib.as_array(packed, shape=(B * r["packed"].shape[1],))[:] = r["packed"].ravel()
+        np.ctypeslib.as_array(synd, shape=(B,))[:] = r["synd"]
+        return 0
+    return fn
+
+
+@pytest.fixture(scope="module")
+def Hr(golden):
+    return golden("frames_default.npz")["H_reordered"]
+
+
+@pytest.mark.parametrize("name", ["aligned", "offset", "inverted", "burst", "noisy"])
+@pytest.mark.parametrize("method", [0, 1, 2, 3])
+def test_block_streams_match_restated_general_work(golden, Hr, name, method):
+    st = golden("streams.npz")
+    s = st[name + "_in"]
+    blk = L.ldpc_decoder_cb(method, _backend=oracle_backend(method, Hr))
+    tb = fg.top_block()
+    src, dst = fg.vector_source_c(s), fg.vector_sink_b()
+    tb.connect((src, 0), (blk, 0))
+    tb.connect((blk, 0), (dst, 0))
+    tb.run()
+    assert (dst.array() == st["%s_m%d_out" % (name, method)]).all()
+
+
+@pytest.mark.parametrize("chunk,out_space", [(7, 4), (64, 8), (100, 1000), (333, 12)])
+def test_block_chunking_and_output_space(golden, Hr, chunk, out_space):
+    st = golden("streams.npz")
+    s = st["burst_in"]
+    blk = L.ldpc_decoder_cb(1, _backend=oracle_backend(1, Hr))
+    tb = fg.top_block(chunk=chunk, out_space=out_space)
+    src, dst = fg.vector_source_c(s), fg.vector_sink_b()
+    tb.connect(src, blk, dst)
+    tb.run()
+    assert (dst.array() == st["burst_m1_out"]).all()
+
+
+def test_forecast(Hr):
+    blk = L.ldpc_decoder_cb(1, _backend=oracle_backend(1, Hr))
+    assert blk.forecast(4) == 256  # noutput * N (:126-130)
+    assert L.ldpc_encoder_bc().forecast(64) == 4  # ceil(64/16) (:112-116)
+
+
+def test_state_machine_inverted_quirk(Hr):
+    """Out of sync while INVERTED, the '-tx' retry decodes the un-inverted
+    samples yet sets INVERTED again (:150-152 with :180-191)."""
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 2, size=(30, 32), dtype=np.uint8)
+    cw = L.encode(Hr, data)
+    x = (2.0 * cw - 1.0).astype(np.float32)
+    frames = np.concatenate([-x[:10], rng.standard_normal((12, 64)).astype(np.float32), x[10:]])
+    s = frames.reshape(-1).astype(np.complex64)
+    exp = orc.run_stream(1, Hr, s, iterations=5)
+    blk = L.ldpc_decoder_cb(1, _backend=oracle_backend(1, Hr))
+    out, used = blk.general_work(10 ** 6, s)
+    assert (out == exp).all()
+    ob = orc.Block(1, Hr, 5)
+    ob.general_work(10 ** 6, s)
+    assert blk.state == ob.state and blk.errors == ob.errors
+
+
+def test_encoder_block_roundtrip(Hr):
+    rng = np.random.default_rng(9)
+    payload = rng.integers(0, 256, 40, dtype=np.uint8)
+    enc = L.ldpc_encoder_bc()
+    tb = fg.top_block(chunk=3, out_space=200)
+    src, dst = fg.vector_source_b(payload), fg.vector_sink_c()
+    tb.connect(src, enc, dst)
+    tb.run()
+    sym = dst.array()
+    assert len(sym) == 40 // 4 * 64 and (sym.imag == 0).all()
+    bits = (sym.real.reshape(-1, 64) > 0).astype(np.uint8)
+    assert not ((Hr.astype(int) @ bits.T.astype(int)) % 2).any()
+    assert (np.packbits(bits[:, 32:].reshape(-1)) == payload).all()
+    # noiseless frames decode back through the (oracle-backed) block
+    blk = L.ldpc_decoder_cb(1, _backend=oracle_backend(1, Hr))
+    out, _ = blk.general_work(10 ** 6, sym)
+    assert (out == payload).all()

@@ -1,0 +1,73 @@
+"""ldpc_math.hpp (the f64 tanh/expm1/log the kernels use) on the host:
+tanh/expm1 bit-identical to the host libm (glibc, what the reference and the
+oracle call); the branch-free GPU forms identical to the branchy fdlibm
+forms; log within 1 ulp of glibc."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "native", "math_check.cc")
+
+
+@pytest.fixture(scope="module")
+def mc(tmp_path_factory):
+    so = str(tmp_path_factory.mktemp("mc") / "math_check.so")
+    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-fPIC", "-shared", "-o", so, SRC,
+                           "-lm"])
+    return ctypes.CDLL(so)
+
+
+def _run(mc, fname, fn, x):
+    x = np.ascontiguousarray(x, np.float64)
+    out = np.zeros(2, np.int64)
+    getattr(mc, fname)(fn, x.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(x.size),
+                       out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+SPECIALS = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324, 1e-310, 2.0 ** -55,
+                     2.0 ** -54, 22.0, -22.0, 21.999, 1.0, -1.0, 0.34657359, 1.0397, 38.8,
+                     44.0, 1e300, -1e300])
+
+
+def _inputs(seed, n=400_000):
+    rng = np.random.default_rng(seed)
+    return [rng.uniform(-1, 1, n), rng.uniform(-30, 30, n), rng.normal(0, 8, n),
+            rng.uniform(-1, 1, n) * 10.0 ** rng.uniform(-20, 0, n), SPECIALS]
+
+
+def test_tanh_bit_identical_to_libm(mc):
+    for x in _inputs(1):
+        mism, maxulp = _run(mc, "check_fn", 0, x)
+        assert mism == 0, (mism, maxulp)
+
+
+def test_expm1_bit_identical_to_libm(mc):
+    rng = np.random.default_rng(2)
+    for x in (rng.uniform(-2, 0, 400_000), rng.uniform(2, 44, 400_000),
+              rng.uniform(-60, 300, 400_000), SPECIALS):
+        mism, _ = _run(mc, "check_fn", 1, x)
+        assert mism == 0
+
+
+def test_branch_free_forms_identical(mc):
+    rng = np.random.default_rng(3)
+    for x in _inputs(4):
+        assert _run(mc, "check_bf", 0, x)[0] == 0
+    for x in (rng.uniform(-2, 0, 400_000), rng.uniform(2, 44, 400_000)):
+        assert _run(mc, "check_bf", 1, x)[0] == 0
+    for x in (np.exp(rng.uniform(-40, 40, 400_000)), 1 + rng.uniform(-2e-6, 2e-6, 400_000),
+              rng.uniform(0, 3, 400_000), SPECIALS):
+        assert _run(mc, "check_bf", 2, x)[0] == 0
+
+
+def test_log_within_one_ulp(mc):
+    rng = np.random.default_rng(5)
+    for x in (np.exp(rng.uniform(-40, 40, 400_000)), rng.uniform(0, 3, 400_000),
+              1 + rng.uniform(-1e-3, 1e-3, 400_000)):
+        _, maxulp = _run(mc, "check_fn", 2, x)
+        assert maxulp <= 1
