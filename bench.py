@@ -227,15 +227,21 @@ def main():
     }
 
     # ---- variants measured in the same process (not the headline) ----------
+    variant_outs = {}
     if not args.no_variants:
         var = {}
-        for name, (m, p) in {"sum-product f32": (1, 1), "min-sum f64": (0, 0),
-                             "min-sum f32": (0, 1)}.items():
-            w2, k2, it2, o2 = time_decoder(dec, torch, d_in, B, m, args.iters, args.et_period, p,
-                                           max(5, args.steps // 2), 2)
+        for name, (m, p) in {"sum-product f32": (1, 1), "sum-product f64": (1, 0),
+                             "min-sum f64": (0, 0), "min-sum f32": (0, 1)}.items():
+            if (m, p) == (args.method, prec):
+                continue
             st = max(5, args.steps // 2)
+            w2, k2, it2, o2 = time_decoder(dec, torch, d_in, B, m, args.iters, args.et_period, p,
+                                           st, 2)
+            alg2 = float(B * (4 * dec.N + dec.KB + 8) + it2.sum() * bytes_per_iter(dec.E, dec.N, p))
             var[name] = {"Mbit/s": round(B * dec.K * st / w2 / 1e6, 2),
-                         "kernel_ms": round(k2, 5), "mean_iters": round(float(it2.mean()), 3)}
+                         "kernel_ms": round(k2, 5), "mean_iters": round(float(it2.mean()), 3),
+                         "alg_GB/s": round(alg2 / (k2 * 1e-3) / 1e9, 1)}
+            variant_outs[name] = (m, o2[0].cpu().numpy(), it2)
         line["variants_1gpu"] = var
 
     # ---- CPU baseline + parity (the oracle as checker) ----------------------
@@ -266,6 +272,12 @@ def main():
         line["parity"] = {"frames": B, "packed_mismatch_frames": mism,
                           "iters_mismatch_frames": int((ref["iters"] != iters_b).sum()),
                           "checker": "oracle/ (C restatement of the reference decoder)"}
+        refs = {args.method: ref}
+        for name, (m, pk, it2) in variant_outs.items():
+            if m not in refs:
+                refs[m] = orc.decode_batch(m, Hr, llr, args.iters, nthreads=threads)
+            line["variants_1gpu"][name]["packed_mismatch_frames"] = int(
+                (refs[m]["packed"] != pk).any(axis=1).sum())
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
