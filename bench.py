@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--sweep-wpc", default="", help="comma list; prints a table to stderr")
+    ap.add_argument("--sweep-batch", default="",
+                    help="comma list of B: latency/throughput sweep (config 5) to stderr")
+    ap.add_argument("--sweep-modes", default="1:f64,1:f32,0:f64",
+                    help="method:precision list for the sweeps")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -139,6 +143,21 @@ def main():
     B = args.batch
     llr, data = synth(Hr, B, args.ebn0, args.seed + 7919 * rank)
     d_in = torch.from_numpy(llr).to(dev)  # resident in HBM before timing
+
+    if args.sweep_batch:
+        modes = [(int(m.split(":")[0]), 0 if m.split(":")[1] == "f64" else 1)
+                 for m in args.sweep_modes.split(",")]
+        for Bs in [int(x) for x in args.sweep_batch.split(",")]:
+            y, _ = synth(Hr, Bs, args.ebn0, args.seed + 17)
+            d_y = torch.from_numpy(y).to(dev)
+            for m, p in modes:
+                w0, k0, it0, _ = time_decoder(dec, torch, d_y, Bs, m, args.iters, args.et_period,
+                                              p, args.steps, args.warmup)
+                print("sweepB method=%d prec=%d B=%6d ebn0=%g mean_it=%6.2f max_it=%2d "
+                      "kernel_ms=%8.4f Mbit/s=%9.2f us/iter(max-frame)=%7.3f" %
+                      (m, p, Bs, args.ebn0, it0.mean(), it0.max(), k0,
+                       Bs * dec.K / (k0 * 1e-3) / 1e6, k0 * 1e3 / max(1, it0.max())),
+                      file=sys.stderr, flush=True)
 
     if args.sweep_wpc:
         for m, p in ((args.method, prec), (1, 1), (0, 0)):

@@ -45,22 +45,28 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <typename Real>
+// Arithmetic per precision mode (include/ldpc_hip.h LDPC_PREC_*):
+//   0 F64       double, compact tanh/log of ldpc_math.hpp (<= 3 ulp of glibc)
+//   1 F32       float, ROCm libm
+//   2 F64_LIBM  double, fdlibm tanh bit-identical to glibc's, fdlibm log
+template <int PREC>
 struct Math;
 template <>
-struct Math<double> {
-#ifdef LDPC_OCML_F64  // A/B switch: ROCm's ocml tanh/log
-  static __device__ __forceinline__ double tanh_(double x) { return ::tanh(x); }
-  static __device__ __forceinline__ double log_(double x) { return ::log(x); }
-#else  // fdlibm (ldpc_math.hpp): tanh bit-identical to glibc's, log < 1 ulp
-  static __device__ __forceinline__ double tanh_(double x) { return fm::tanh_f64_bf(x); }
-  static __device__ __forceinline__ double log_(double x) { return fm::log_f64_bf(x); }
-#endif
+struct Math<0> {
+  typedef double Real;
+  static __device__ __forceinline__ double tanh_(double x) { return fm::tanh_fast_f64(x); }
+  static __device__ __forceinline__ double log_(double x) { return fm::log_fast_f64(x); }
   static __device__ __forceinline__ double abs_(double x) { return ::fabs(x); }
   static __device__ __forceinline__ double max_() { return DBL_MAX; }
 };
 template <>
-struct Math<float> {
+struct Math<2> : Math<0> {
+  static __device__ __forceinline__ double tanh_(double x) { return fm::tanh_f64_bf(x); }
+  static __device__ __forceinline__ double log_(double x) { return fm::log_f64_bf(x); }
+};
+template <>
+struct Math<1> {
+  typedef float Real;
   static __device__ __forceinline__ float tanh_(float x) { return ::tanhf(x); }
   static __device__ __forceinline__ float log_(float x) { return ::logf(x); }
   static __device__ __forceinline__ float abs_(float x) { return ::fabsf(x); }
@@ -121,7 +127,7 @@ struct WaveTables {
   uint64_t rowmask[NW][NW];  // rows lane + 64 q, words k (M < N <= 64 NW)
 };
 
-template <typename Real, int METHOD, int S, int NW>
+template <int PREC, int METHOD, int S, int NW, typename Real = typename Math<PREC>::Real>
 __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeArgs &a,
                                              const int64_t b, WaveTables<S, NW> &wt,
                                              Real *tb, Real *eb, Real *rb, Real *sb,
@@ -159,7 +165,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
   };
 
   if constexpr (METHOD == 1 || METHOD == 0) {
-    if (lane == 0) tb[kDummy] = METHOD == 1 ? Real(1) : Math<Real>::max_();
+    if (lane == 0) tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
     int col[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -187,7 +193,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         if constexpr (METHOD == 1)
-          tb[lane + 64 * s] = Math<Real>::tanh_(msg[s] / Real(2));  // :509
+          tb[lane + 64 * s] = Math<PREC>::tanh_(msg[s] / Real(2));  // :509
         else
           tb[lane + 64 * s] = msg[s];
       }
@@ -209,18 +215,18 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           Real T = Real(1);
 #pragma unroll
           for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[s][k];
-          eb[lane + 64 * s] = Math<Real>::log_((Real(1) + T) / (Real(1) - T));
+          eb[lane + 64 * s] = Math<PREC>::log_((Real(1) + T) / (Real(1) - T));
         } else {
           // min-sum horizontal step (:350-376): sign product over the row
           // times the minimum |L(q)| of the other edges.  Padding neighbours
           // read DBL_MAX: sign +1, never below the running minimum.
           const int self = sgn(msg[s]);
           int prod = self;
-          Real lo = Math<Real>::max_();
+          Real lo = Math<PREC>::max_();
 #pragma unroll
           for (int k = 0; k < kDcMax - 1; ++k) {
             prod *= sgn(nb[s][k]);
-            const Real beta = Math<Real>::abs_(nb[s][k]);
+            const Real beta = Math<PREC>::abs_(nb[s][k]);
             lo = beta < lo ? beta : lo;
           }
           lr[s] = (Real)(prod * self) * lo;
@@ -375,9 +381,10 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 // a.waves + ticket++ until the batch is exhausted.  Frames stop after 1..cap
 // iterations, so pulling work keeps every SIMD busy to the end instead of
 // leaving it with a fixed share of the batch.
-template <typename Real, int METHOD, int S, int NW>
+template <int PREC, int METHOD, int S, int NW>
 __global__ void __launch_bounds__(kThreads)
     decode_small_kernel(CodeView code, DecodeArgs a) {
+  typedef typename Math<PREC>::Real Real;
   extern __shared__ __align__(16) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -421,7 +428,7 @@ __global__ void __launch_bounds__(kThreads)
   Real *sb = rb + 64 * NW;
 
   while (b < a.B) {
-    decode_frame<Real, METHOD, S, NW>(code, a, b, wt, tb, eb, rb, sb, lane);
+    decode_frame<PREC, METHOD, S, NW>(code, a, b, wt, tb, eb, rb, sb, lane);
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(a.ticket, 1u);
     b = (int64_t)a.waves + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
@@ -431,30 +438,31 @@ __global__ void __launch_bounds__(kThreads)
 // ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
-template <typename Real, int METHOD, int S, int NW>
+template <int PREC, int METHOD, int S, int NW>
 static int launch_one(const CodeView &code, const DecodeArgs &a, hipStream_t st) {
+  typedef typename Math<PREC>::Real Real;
   const size_t lds = Layout<Real, S, NW>().total;
   if (lds > 65536 &&
-      hipFuncSetAttribute((const void *)decode_small_kernel<Real, METHOD, S, NW>,
+      hipFuncSetAttribute((const void *)decode_small_kernel<PREC, METHOD, S, NW>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -3;
   const dim3 grid((unsigned)((a.waves + kWavesPerBlock - 1) / kWavesPerBlock));
-  hipLaunchKernelGGL((decode_small_kernel<Real, METHOD, S, NW>), grid, dim3(kThreads), lds, st,
+  hipLaunchKernelGGL((decode_small_kernel<PREC, METHOD, S, NW>), grid, dim3(kThreads), lds, st,
                      code, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-template <typename Real, int METHOD, int NW>
+template <int PREC, int METHOD, int NW>
 static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots, hipStream_t st) {
   switch (slots) {
-    case 1: return launch_one<Real, METHOD, 1, NW>(code, a, st);
-    case 2: return launch_one<Real, METHOD, 2, NW>(code, a, st);
-    case 3: return launch_one<Real, METHOD, 3, NW>(code, a, st);
-    case 4: return launch_one<Real, METHOD, 4, NW>(code, a, st);
-    case 5: return launch_one<Real, METHOD, 5, NW>(code, a, st);
-    case 6: return launch_one<Real, METHOD, 6, NW>(code, a, st);
-    case 7: return launch_one<Real, METHOD, 7, NW>(code, a, st);
-    case 8: return launch_one<Real, METHOD, 8, NW>(code, a, st);
+    case 1: return launch_one<PREC, METHOD, 1, NW>(code, a, st);
+    case 2: return launch_one<PREC, METHOD, 2, NW>(code, a, st);
+    case 3: return launch_one<PREC, METHOD, 3, NW>(code, a, st);
+    case 4: return launch_one<PREC, METHOD, 4, NW>(code, a, st);
+    case 5: return launch_one<PREC, METHOD, 5, NW>(code, a, st);
+    case 6: return launch_one<PREC, METHOD, 6, NW>(code, a, st);
+    case 7: return launch_one<PREC, METHOD, 7, NW>(code, a, st);
+    case 8: return launch_one<PREC, METHOD, 8, NW>(code, a, st);
     default: return -2;
   }
 }
@@ -462,13 +470,16 @@ static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots, hi
 template <int NW>
 static int launch_nw(const CodeView &code, const DecodeArgs &a, int method, int prec, int slots,
                      hipStream_t st) {
-  if (method == 3) return launch_one<float, 3, 1, NW>(code, a, st);
-  if (method == 2) return launch_one<float, 2, 1, NW>(code, a, st);
-  if (method == 1)
-    return prec == 1 ? launch_slots<float, 1, NW>(code, a, slots, st)
-                     : launch_slots<double, 1, NW>(code, a, slots, st);
-  return prec == 1 ? launch_slots<float, 0, NW>(code, a, slots, st)
-                   : launch_slots<double, 0, NW>(code, a, slots, st);
+  if (method == 3) return launch_one<1, 3, 1, NW>(code, a, st);
+  if (method == 2) return launch_one<1, 2, 1, NW>(code, a, st);
+  if (method == 1) {
+    if (prec == 1) return launch_slots<1, 1, NW>(code, a, slots, st);
+    if (prec == 2) return launch_slots<2, 1, NW>(code, a, slots, st);
+    return launch_slots<0, 1, NW>(code, a, slots, st);
+  }
+  // min-sum has no transcendentals: both f64 modes are the same kernel
+  return prec == 1 ? launch_slots<1, 0, NW>(code, a, slots, st)
+                   : launch_slots<0, 0, NW>(code, a, slots, st);
 }
 
 int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int prec, int slots,

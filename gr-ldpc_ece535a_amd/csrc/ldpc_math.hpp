@@ -341,5 +341,100 @@ LDPC_HD double log_f64_bf(double x) {
   return zero ? -__builtin_inf() : r;
 }
 
+// ---------------------------------------------------------------------------
+// Compact forms for the default f64 mode: same functions, a fraction of the
+// instructions, within a few ulp of glibc (tests/test_math.py bounds them).
+// Domain handling is complete (0, +-inf, NaN), but the fast paths assume what
+// the decoder feeds them: tanh of a finite or infinite double, log of a
+// quotient (1+T)/(1-T) in [0, 2^54] or +inf.
+// ---------------------------------------------------------------------------
+
+#if defined(__HIP_DEVICE_COMPILE__)
+LDPC_HD double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
+LDPC_HD double rint_(double x) { return __builtin_rint(x); }
+LDPC_HD double ldexp_(double x, int e) { return __builtin_ldexp(x, e); }
+LDPC_HD double frexp_(double x, int *e) { return __builtin_frexp(x, e); }
+#else
+LDPC_HD double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
+LDPC_HD double rint_(double x) { return __builtin_rint(x); }
+LDPC_HD double ldexp_(double x, int e) { return __builtin_ldexp(x, e); }
+LDPC_HD double frexp_(double x, int *e) { return __builtin_frexp(x, e); }
+#endif
+
+// expm1(z) for z in [-44, 44]: z = n ln2 + r, |r| <= ln2/2, expm1(r) by its
+// Taylor polynomial to r^13 (truncation < 2^-60 relative), then
+// expm1(z) = 2^n expm1(r) + (2^n - 1) as one fma (2^n - 1 exact for n <= 53).
+LDPC_HD double expm1_mid_f64(double z) {
+  const double log2e = 1.4426950408889634;
+  const double ln2_hi = 6.93147180369123816490e-01;  // low 21 bits zero
+  const double ln2_lo = 1.90821492927058770002e-10;
+  const double n = rint_(z * log2e);
+  double r = fma_(-n, ln2_hi, z);
+  r = fma_(-n, ln2_lo, r);
+  double p = 1.0 / 6227020800.0;          // 1/13!
+  p = fma_(p, r, 1.0 / 479001600.0);      // 1/12!
+  p = fma_(p, r, 1.0 / 39916800.0);
+  p = fma_(p, r, 1.0 / 3628800.0);
+  p = fma_(p, r, 1.0 / 362880.0);
+  p = fma_(p, r, 1.0 / 40320.0);
+  p = fma_(p, r, 1.0 / 5040.0);
+  p = fma_(p, r, 1.0 / 720.0);
+  p = fma_(p, r, 1.0 / 120.0);
+  p = fma_(p, r, 1.0 / 24.0);
+  p = fma_(p, r, 1.0 / 6.0);
+  p = fma_(p, r, 0.5);
+  const double em = fma_(r * r, p, r);  // expm1(r)
+  const double s = ldexp_(1.0, (int)n);  // 2^n, exact
+  return fma_(s, em, s - 1.0);
+}
+
+// tanh with fdlibm's two ranges (s_tanh.c), one expm1 and one division:
+//   |x| <  1: t = expm1(-2|x|), tanh = -t / (t + 2)
+//   |x| >= 1: t = expm1( 2|x|), tanh = 1 - 2 / (t + 2);  |x| >= 22: 1
+LDPC_HD double tanh_fast_f64(double x) {
+  const double a = __builtin_fabs(x);
+  const bool big = a >= 1.0;
+  const double z = big ? 2.0 * (a < 22.0 ? a : 22.0) : -2.0 * a;
+  const double t = expm1_mid_f64(z);
+  const double q = (big ? 2.0 : -t) / (t + 2.0);
+  double r = big ? 1.0 - q : q;
+  r = a >= 22.0 ? 1.0 : r;
+  r = x < 0.0 ? -r : r;
+  return x != x ? x : r;  // NaN
+}
+
+// log(q) for q >= 0: q = 2^k (1 + f), sqrt(1/2) <= 1 + f < sqrt(2);
+// s = f / (2 + f); log(1 + f) = f - (hfsq - s (hfsq + R(s^2))) with fdlibm's
+// minimax R (e_log.c Lg1..Lg7).
+LDPC_HD double log_fast_f64(double q) {
+  const double ln2_hi = 6.93147180369123816490e-01;
+  const double ln2_lo = 1.90821492927058770002e-10;
+  const double Lg1 = 6.666666666666735130e-01;
+  const double Lg2 = 3.999999999940941908e-01;
+  const double Lg3 = 2.857142874366239149e-01;
+  const double Lg4 = 2.222219843214978396e-01;
+  const double Lg5 = 1.818357216161805012e-01;
+  const double Lg6 = 1.531383769920937332e-01;
+  const double Lg7 = 1.479819860511658591e-01;
+  int k;
+  double m = frexp_(q, &k);  // m in [0.5, 1)
+  const bool lo = m < 0.70710678118654752440;
+  m = lo ? m + m : m;
+  k = lo ? k - 1 : k;
+  const double f = m - 1.0;  // exact
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  const double w = z * z;
+  const double t1 = w * fma_(w, fma_(w, Lg6, Lg4), Lg2);
+  const double t2 = z * fma_(w, fma_(w, fma_(w, Lg7, Lg5), Lg3), Lg1);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  double r = dk * ln2_hi - ((hfsq - fma_(s, hfsq + R, dk * ln2_lo)) - f);
+  r = q == 0.0 ? -__builtin_inf() : r;
+  r = q < 0.0 ? __builtin_nan("") : r;
+  return (q == __builtin_inf() || q != q) ? q + q : r;
+}
+
 }  // namespace fm
 }  // namespace ldpc

@@ -43,11 +43,15 @@ extern "C" {
 #define LDPC_METHOD_BITFLIP 2    /* decodeBitFlipping */
 #define LDPC_METHOD_HARD 3       /* decodeHard */
 
-/* arithmetic for methods 0/1.  F64 reproduces the reference's double
- * arithmetic operation for operation (parity mode, default); F32 is the fast
- * mode (hard decisions are compared against the oracle, not guaranteed). */
+/* arithmetic for methods 0/1.  The F64 modes repeat the reference's double
+ * operations in the reference's order (parity modes): F64 (default) with
+ * compact tanh/log within 3 ulp of glibc's, F64_LIBM with fdlibm tanh
+ * bit-identical to glibc's (and fdlibm log); min-sum has no transcendentals
+ * and is exact in both.  F32 is the fast mode: its hard decisions are
+ * measured against the oracle, not guaranteed. */
 #define LDPC_PREC_F64 0
 #define LDPC_PREC_F32 1
+#define LDPC_PREC_F64_LIBM 2
 
 /* ldpc_create flags */
 #define LDPC_FLAG_NO_REORDER 1 /* use H as given (skip reorderHMatrix) */

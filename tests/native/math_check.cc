@@ -53,3 +53,20 @@ void check_bf(int fn, const double *x, int64_t n, int64_t *out) {
   out[0] = mism;
 }
 }
+extern "C" {
+// compact forms vs host libm: fn 0 tanh_fast, 1 expm1_neg, 2 log_fast.
+// out[0] = mismatches, out[1] = max ulp
+void check_fast(int fn, const double *x, int64_t n, int64_t *out) {
+  int64_t mism = 0, maxu = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double a, b;
+    if (fn == 0) { a = ldpc::fm::tanh_fast_f64(x[i]); b = tanh(x[i]); }
+    else if (fn == 1) { a = ldpc::fm::expm1_mid_f64(x[i]); b = expm1(x[i]); }
+    else { a = ldpc::fm::log_fast_f64(x[i]); b = log(x[i]); }
+    int64_t u = ulps(a, b);
+    if (u) ++mism;
+    if (u > maxu) maxu = u;
+  }
+  out[0] = mism; out[1] = maxu;
+}
+}
