@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--sweep-wpc", default="", help="comma list; prints a table to stderr")
     ap.add_argument("--sweep-batch", default="",
                     help="comma list of B: latency/throughput sweep (config 5) to stderr")
+    ap.add_argument("--schedule", type=int, default=0, help="0 auto, 1 wave/frame, 2 workgroup/frame")
+    ap.add_argument("--sweep-schedules", default="0", help="comma list for --sweep-batch")
     ap.add_argument("--sweep-modes", default="1:f64,1:f32,0:f64",
                     help="method:precision list for the sweeps")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -139,6 +141,7 @@ def main():
 
     dec = L.Decoder(device=local)  # default H, reorderHMatrix applied
     dec.set_waves_per_cu(args.waves_per_cu)
+    dec.set_schedule(args.schedule)
     Hr = dec.H
     B = args.batch
     llr, data = synth(Hr, B, args.ebn0, args.seed + 7919 * rank)
@@ -150,14 +153,17 @@ def main():
         for Bs in [int(x) for x in args.sweep_batch.split(",")]:
             y, _ = synth(Hr, Bs, args.ebn0, args.seed + 17)
             d_y = torch.from_numpy(y).to(dev)
-            for m, p in modes:
-                w0, k0, it0, _ = time_decoder(dec, torch, d_y, Bs, m, args.iters, args.et_period,
-                                              p, args.steps, args.warmup)
-                print("sweepB method=%d prec=%d B=%6d ebn0=%g mean_it=%6.2f max_it=%2d "
-                      "kernel_ms=%8.4f Mbit/s=%9.2f us/iter(max-frame)=%7.3f" %
-                      (m, p, Bs, args.ebn0, it0.mean(), it0.max(), k0,
-                       Bs * dec.K / (k0 * 1e-3) / 1e6, k0 * 1e3 / max(1, it0.max())),
-                      file=sys.stderr, flush=True)
+            for sched in [int(x) for x in args.sweep_schedules.split(",")]:
+                dec.set_schedule(sched)
+                for m, p in modes:
+                    w0, k0, it0, _ = time_decoder(dec, torch, d_y, Bs, m, args.iters,
+                                                  args.et_period, p, args.steps, args.warmup)
+                    print("sweepB sched=%d method=%d prec=%d B=%6d ebn0=%g mean_it=%6.2f "
+                          "max_it=%2d kernel_ms=%8.4f Mbit/s=%9.2f us/iter(max-frame)=%7.3f" %
+                          (sched, m, p, Bs, args.ebn0, it0.mean(), it0.max(), k0,
+                           Bs * dec.K / (k0 * 1e-3) / 1e6, k0 * 1e3 / max(1, it0.max())),
+                          file=sys.stderr, flush=True)
+            dec.set_schedule(args.schedule)
 
     if args.sweep_wpc:
         for m, p in ((args.method, prec), (1, 1), (0, 0)):

@@ -36,6 +36,7 @@ struct ldpc_ctx {
   uint32_t *d_tickets = nullptr;  // ring of per-launch frame-queue heads
   unsigned launch_seq = 0;
   int waves_per_cu = 0;           // 0: kernel default
+  int schedule = 0;               // 0 auto, 1 wave per frame, 2 workgroup per frame
   std::string err;
 };
 
@@ -439,7 +440,7 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   void *st = hip_stream ? hip_stream : (void *)ctx->stream;
   rc = ldpc::launch_decode(code_view(ctx), a, method, precision, ctx->slots, ctx->nw,
-                           ctx->waves_per_cu, st);
+                           ctx->waves_per_cu, ctx->schedule, st);
   if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no kernel for this code shape");
   if (rc != 0) return hip_err(ctx, hipGetLastError(), "kernel launch");
   ++ctx->launch_seq;  // only a launched kernel consumes (and re-arms) a ticket slot
@@ -511,6 +512,13 @@ int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu) {
   if (!ctx || waves_per_cu < 0 || waves_per_cu > 32)
     return set_err(ctx, LDPC_EINVAL, "waves_per_cu must be in [0, 32]");
   ctx->waves_per_cu = waves_per_cu;
+  return LDPC_OK;
+}
+
+int ldpc_set_schedule(ldpc_ctx *ctx, int schedule) {
+  if (!ctx || schedule < 0 || schedule > 2)
+    return set_err(ctx, LDPC_EINVAL, "schedule must be 0 (auto), 1 or 2");
+  ctx->schedule = schedule;
   return LDPC_OK;
 }
 

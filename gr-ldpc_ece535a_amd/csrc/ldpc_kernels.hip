@@ -36,13 +36,20 @@
 
 namespace ldpc {
 
-// LDS hand-off between lanes of ONE wave: the wave's LDS operations execute
-// in issue order, so a wavefront-scope fence (compiler ordering + lgkmcnt)
-// is all that is needed; no s_barrier, waves stay independent.
+// LDS hand-off between lanes of ONE wave.  The LDS executes a wave's DS
+// instructions in issue order, so a read issued after a write sees it: only
+// the compiler must be kept from reordering the accesses -- no s_waitcnt,
+// no s_barrier, waves stay independent.  (LDPC_LDS_FENCE restores the
+// wavefront-scope fences for A/B checks.)
 __device__ __forceinline__ void wave_lds_sync() {
+#ifdef LDPC_LDS_FENCE
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+#endif
 }
 
 // Arithmetic per precision mode (include/ldpc_hip.h LDPC_PREC_*):
@@ -234,6 +241,21 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         }
       }
       wave_lds_sync();
+      // the variable pass's gathers go out with the column gathers (one
+      // wait); they are simply unused when the frame stops here
+      Real cv[S][kDvMax - 1];
+      Real rcs[S];
+      if constexpr (METHOD == 1) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          rcs[s] = rb[col[s]];
+#pragma unroll
+          for (int k = 0; k < kDvMax - 1; ++k) {
+            const int n = field(wt.cn[s], k);
+            cv[s][k] = eb[n == kNone ? kDummy : n];
+          }
+        }
+      }
       // ---- per-column totals and the hard decision ----------------------
 #pragma unroll
       for (int q = 0; q < NW; ++q) {
@@ -275,17 +297,6 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 
       if constexpr (METHOD == 1) {
         // ---- bit messages, :540-553: M(j,i) = sum_{k != j} (E(k,i) + r(i))
-        Real cv[S][kDvMax - 1];
-        Real rcs[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-          rcs[s] = rb[col[s]];
-#pragma unroll
-          for (int k = 0; k < kDvMax - 1; ++k) {
-            const int n = field(wt.cn[s], k);
-            cv[s][k] = eb[n == kNone ? kDummy : n];
-          }
-        }
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           Real acc = Real(0);
@@ -436,6 +447,210 @@ __global__ void __launch_bounds__(kThreads)
 }
 
 // ---------------------------------------------------------------------------
+// Multi-wave kernel: one frame per S-wave workgroup, one edge per lane.
+//
+// At small batches the decode time is set by the frames that run to the
+// iteration cap, i.e. by one frame's per-iteration latency.  Spreading a
+// frame over S waves (on different SIMDs of the CU) divides the edge work of
+// an iteration by S; the price is two workgroup barriers per iteration.  The
+// cheap column phase (posterior, hard decision, syndrome) is computed by
+// every wave redundantly from the shared check messages, so every wave
+// reaches the same early-exit decision without a third barrier.
+// ---------------------------------------------------------------------------
+template <typename Real, int S, int NW>
+struct MwLayout {
+  size_t eb, waves, per_wave, fslot, total;
+  __host__ __device__ MwLayout() {
+    eb = align16((64 * S + 2) * sizeof(Real));           // tb at 0
+    waves = eb + align16((64 * S + 2) * sizeof(Real));   // per-wave rb, sb
+    per_wave = align16(2 * 64 * NW * sizeof(Real));
+    fslot = waves + (size_t)S * per_wave;
+    total = fslot + 16;
+  }
+};
+
+template <int PREC, int METHOD, int S, int NW>
+__global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, DecodeArgs a) {
+  typedef typename Math<PREC>::Real Real;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const MwLayout<Real, S, NW> L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = code.M, N = code.N;
+  constexpr int kDummy = 64 * S;
+  Real *tb = reinterpret_cast<Real *>(smem);
+  Real *eb = reinterpret_cast<Real *>(smem + L.eb);
+  Real *rb = reinterpret_cast<Real *>(smem + L.waves + (size_t)wave * L.per_wave);
+  Real *sb = rb + 64 * NW;
+  int *fslot = reinterpret_cast<int *>(smem + L.fslot);
+  if (blockIdx.x == 0 && tid == 0) *a.ticket_next = 0u;  // next launch's queue head
+  if (tid == 0) tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
+
+  // this lane's edge, and (every wave) the columns lane + 64 q
+  uint32_t rn[4], cn[2], ce[NW][2];
+  {
+    const uint4 r = reinterpret_cast<const uint4 *>(code.erow)[tid];
+    rn[0] = r.x; rn[1] = r.y; rn[2] = r.z; rn[3] = r.w;
+    const uint2 c = reinterpret_cast<const uint2 *>(code.ecol)[tid];
+    cn[0] = c.x; cn[1] = c.y;
+  }
+  uint64_t rowmask[NW][NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const uint4 c = reinterpret_cast<const uint4 *>(code.cols)[lane + 64 * q];
+    ce[q][0] = c.x; ce[q][1] = c.y;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int j = lane + 64 * q;
+      rowmask[q][k] = j < M ? code.rowmask[j * NW + k] : 0ull;
+    }
+  }
+  int col = field(rn, 7);
+  col = col != kNone ? col : 0;
+
+  int64_t b = blockIdx.x;
+  while (b < a.B) {
+    // channel samples, one private copy per wave (:149-153, :486)
+    const float *src = a.in + b * a.cw_stride;
+    Real post[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int c = lane + 64 * q;
+      float x = 0.0f;
+      if (c < N) x = src[(int64_t)c * a.elem_stride] * a.polarity;
+      rb[c] = -(Real)x;
+      post[q] = (Real)x;
+    }
+    __syncthreads();  // dummy written; previous frame's tb/eb readers done
+    uint64_t hard[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) hard[q] = 0;
+    int weight = 0, used = 0;
+    Real msg = rb[col], lr = Real(0);
+    for (int h = 0; h < a.max_iters; ++h) {
+      opaque(rn);
+      opaque(cn);
+      if constexpr (METHOD == 1)
+        tb[tid] = Math<PREC>::tanh_(msg / Real(2));  // :509
+      else
+        tb[tid] = msg;
+      __syncthreads();
+      Real nb[kDcMax - 1];
+#pragma unroll
+      for (int k = 0; k < kDcMax - 1; ++k) {
+        const int n = field(rn, k);
+        nb[k] = tb[n == kNone ? kDummy : n];
+      }
+      if constexpr (METHOD == 1) {
+        Real T = Real(1);  // ascending column; dummies are exact 1.0 (:506-511)
+#pragma unroll
+        for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[k];
+        eb[tid] = Math<PREC>::log_((Real(1) + T) / (Real(1) - T));  // :513
+      } else {
+        const int self = sgn(msg);  // :350-376
+        int prod = self;
+        Real lo = Math<PREC>::max_();
+#pragma unroll
+        for (int k = 0; k < kDcMax - 1; ++k) {
+          prod *= sgn(nb[k]);
+          const Real beta = Math<PREC>::abs_(nb[k]);
+          lo = beta < lo ? beta : lo;
+        }
+        lr = (Real)(prod * self) * lo;
+        eb[tid] = lr;
+      }
+      __syncthreads();
+      // column phase, identical in every wave
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        opaque(ce[q]);
+        const int c = lane + 64 * q;
+        Real ev[kDvMax];
+#pragma unroll
+        for (int k = 0; k < kDvMax; ++k) {
+          const int n = field(ce[q], k);
+          ev[k] = eb[n == kNone ? kDummy : n];
+        }
+        const Real rc = rb[c];
+        Real acc = Real(0);
+        bool bit;
+        if constexpr (METHOD == 1) {  // :519-532
+#pragma unroll
+          for (int k = 0; k < kDvMax; ++k)
+            acc = field(ce[q], k) != kNone ? acc + (ev[k] + rc) : acc;
+          bit = acc <= Real(0);
+          post[q] = acc;
+        } else {  // :379-403
+#pragma unroll
+          for (int k = 0; k < kDvMax; ++k)
+            acc = field(ce[q], k) != kNone ? acc + ev[k] : acc;
+          const Real LQ = rc + acc;
+          sb[c] = LQ;
+          bit = LQ < Real(0);
+          post[q] = LQ;
+        }
+        hard[q] = __ballot(bit && c < N);
+      }
+      weight = 0;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        int odd = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) odd ^= __popcll(rowmask[q][k] & hard[k]);
+        weight += __popcll(__ballot((odd & 1) != 0 && lane + 64 * q < M));
+      }
+      used = h + 1;
+      if (h + 1 == a.max_iters) break;
+      if ((h + 1) % a.et_period == 0 && weight == 0) break;
+      if constexpr (METHOD == 1) {  // :540-553
+        const Real rc = rb[col];
+        Real cv[kDvMax - 1];
+#pragma unroll
+        for (int k = 0; k < kDvMax - 1; ++k) {
+          const int n = field(cn, k);
+          cv[k] = eb[n == kNone ? kDummy : n];
+        }
+        Real acc = Real(0);
+#pragma unroll
+        for (int k = 0; k < kDvMax - 1; ++k)
+          acc = field(cn, k) != kNone ? acc + (cv[k] + rc) : acc;
+        msg = acc;
+      } else {
+        wave_lds_sync();  // this wave's sb
+        msg = sb[col] - lr;  // :387-392
+      }
+    }
+    // outputs (wave 0)
+    if (wave == 0) {
+      if (lane == 0) {
+        if (a.iters) a.iters[b] = used;
+        if (a.synd) a.synd[b] = weight;
+      }
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int c = lane + 64 * q;
+        if (c < N) {
+          if (a.bits) a.bits[b * N + c] = (uint8_t)((hard[q] >> lane) & 1);
+          if (a.llr) a.llr[b * N + c] = (float)post[q];
+        }
+      }
+      for (int p = lane; p < code.KB; p += 64) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = M + 8 * p + j;
+          if (c < N) o |= (uint32_t)((word_at<NW>(hard, c >> 6) >> (c & 63)) & 1) << (7 - j);
+        }
+        a.packed[b * code.KB + p] = (uint8_t)o;
+      }
+    }
+    wave_lds_sync();  // this wave's rb reads done before the next frame's writes
+    if (tid == 0) *fslot = (int)atomicAdd(a.ticket, 1u);
+    __syncthreads();
+    b = (int64_t)a.waves + (int64_t)*fslot;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
 template <int PREC, int METHOD, int S, int NW>
@@ -450,6 +665,34 @@ static int launch_one(const CodeView &code, const DecodeArgs &a, hipStream_t st)
   hipLaunchKernelGGL((decode_small_kernel<PREC, METHOD, S, NW>), grid, dim3(kThreads), lds, st,
                      code, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <int PREC, int METHOD, int S, int NW>
+static int launch_mw(const CodeView &code, const DecodeArgs &a, hipStream_t st) {
+  typedef typename Math<PREC>::Real Real;
+  const size_t lds = MwLayout<Real, S, NW>().total;
+  if (lds > 65536 &&
+      hipFuncSetAttribute((const void *)decode_mw_kernel<PREC, METHOD, S, NW>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -3;
+  hipLaunchKernelGGL((decode_mw_kernel<PREC, METHOD, S, NW>), dim3((unsigned)a.waves),
+                     dim3(64 * S), lds, st, code, a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <int PREC, int METHOD, int NW>
+static int launch_mw_slots(const CodeView &code, const DecodeArgs &a, int slots, hipStream_t st) {
+  switch (slots) {
+    case 1: return launch_mw<PREC, METHOD, 1, NW>(code, a, st);
+    case 2: return launch_mw<PREC, METHOD, 2, NW>(code, a, st);
+    case 3: return launch_mw<PREC, METHOD, 3, NW>(code, a, st);
+    case 4: return launch_mw<PREC, METHOD, 4, NW>(code, a, st);
+    case 5: return launch_mw<PREC, METHOD, 5, NW>(code, a, st);
+    case 6: return launch_mw<PREC, METHOD, 6, NW>(code, a, st);
+    case 7: return launch_mw<PREC, METHOD, 7, NW>(code, a, st);
+    case 8: return launch_mw<PREC, METHOD, 8, NW>(code, a, st);
+    default: return -2;
+  }
 }
 
 template <int PREC, int METHOD, int NW>
@@ -469,7 +712,15 @@ static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots, hi
 
 template <int NW>
 static int launch_nw(const CodeView &code, const DecodeArgs &a, int method, int prec, int slots,
-                     hipStream_t st) {
+                     bool mw, hipStream_t st) {
+  if (mw && method == 1) {
+    if (prec == 1) return launch_mw_slots<1, 1, NW>(code, a, slots, st);
+    if (prec == 2) return launch_mw_slots<2, 1, NW>(code, a, slots, st);
+    return launch_mw_slots<0, 1, NW>(code, a, slots, st);
+  }
+  if (mw && method == 0)
+    return prec == 1 ? launch_mw_slots<1, 0, NW>(code, a, slots, st)
+                     : launch_mw_slots<0, 0, NW>(code, a, slots, st);
   if (method == 3) return launch_one<1, 3, 1, NW>(code, a, st);
   if (method == 2) return launch_one<1, 2, 1, NW>(code, a, st);
   if (method == 1) {
@@ -483,7 +734,7 @@ static int launch_nw(const CodeView &code, const DecodeArgs &a, int method, int 
 }
 
 int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int prec, int slots,
-                  int nw, int waves_per_cu, void *stream) {
+                  int nw, int waves_per_cu, int schedule, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (args.B <= 0) return 0;
   DecodeArgs a = args;
@@ -491,10 +742,22 @@ int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int 
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (waves_per_cu <= 0) waves_per_cu = 12;
-  const int64_t w = std::min<int64_t>((int64_t)a.B, (int64_t)waves_per_cu * cus);
-  a.waves = (int)((w + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock);
-  if (nw == 1) return launch_nw<1>(code, a, method, prec, slots, st);
-  if (nw == 4) return launch_nw<4>(code, a, method, prec, slots, st);
+  // schedule: 1 one wave per frame, 2 one workgroup of `slots` waves per
+  // frame, 0 auto.  Measured (bench.py --sweep-batch): the workgroup form
+  // wins for min-sum until the batch fills the persistent grid several times
+  // over; sum-product's long per-edge chains keep the one-wave form ahead.
+  bool mw = schedule == 2;
+  if (schedule == 0)
+    mw = method == 0 && slots > 1 && (int64_t)a.B <= (int64_t)4 * waves_per_cu * cus;
+  if (mw) {
+    const int64_t frames_in_flight = std::max<int64_t>(1, (int64_t)waves_per_cu * cus / slots);
+    a.waves = (int)std::min<int64_t>((int64_t)a.B, frames_in_flight);
+  } else {
+    const int64_t w = std::min<int64_t>((int64_t)a.B, (int64_t)waves_per_cu * cus);
+    a.waves = (int)((w + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock);
+  }
+  if (nw == 1) return launch_nw<1>(code, a, method, prec, slots, mw, st);
+  if (nw == 4) return launch_nw<4>(code, a, method, prec, slots, mw, st);
   return -2;
 }
 

@@ -75,8 +75,9 @@ struct DecodeArgs {
 // Launch one decode (host side, implemented in ldpc_kernels.hip).
 // method: 0 min-sum, 1 sum-product, 2 bit-flip, 3 hard; prec 0 f64, 1 f32;
 // slots = ceil(E/64); nw = 1 or 4 (hard-decision words).
-// waves_per_cu (0 = default) sets the number of persistent waves.
+// waves_per_cu (0 = default) sets the number of persistent waves;
+// schedule: 0 auto, 1 one wave per frame, 2 one multi-wave workgroup per frame.
 int launch_decode(const CodeView &code, const DecodeArgs &args, int method,
-                  int prec, int slots, int nw, int waves_per_cu, void *stream);
+                  int prec, int slots, int nw, int waves_per_cu, int schedule, void *stream);
 
 }  // namespace ldpc

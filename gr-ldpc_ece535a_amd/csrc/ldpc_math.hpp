@@ -361,6 +361,21 @@ LDPC_HD double ldexp_(double x, int e) { return __builtin_ldexp(x, e); }
 LDPC_HD double frexp_(double x, int *e) { return __builtin_frexp(x, e); }
 #endif
 
+// n / d for the divisions inside the compact forms (not the decoder's own
+// (1+T)/(1-T), which stays an IEEE division): reciprocal, one Newton step,
+// one residual correction -- within 1 ulp for the normal, finite operands
+// these functions produce (d in [1, 2^64]).
+LDPC_HD double div_fast(double n, double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double y = __builtin_amdgcn_rcp(d);
+#else
+  double y = 1.0 / d;
+#endif
+  y = fma_(fma_(-d, y, 1.0), y, y);
+  const double q = n * y;
+  return fma_(fma_(-d, q, n), y, q);
+}
+
 // expm1(z) for z in [-44, 44]: z = n ln2 + r, |r| <= ln2/2, expm1(r) by its
 // Taylor polynomial to r^13 (truncation < 2^-60 relative), then
 // expm1(z) = 2^n expm1(r) + (2^n - 1) as one fma (2^n - 1 exact for n <= 53).
@@ -396,7 +411,7 @@ LDPC_HD double tanh_fast_f64(double x) {
   const bool big = a >= 1.0;
   const double z = big ? 2.0 * (a < 22.0 ? a : 22.0) : -2.0 * a;
   const double t = expm1_mid_f64(z);
-  const double q = (big ? 2.0 : -t) / (t + 2.0);
+  const double q = div_fast(big ? 2.0 : -t, t + 2.0);
   double r = big ? 1.0 - q : q;
   r = a >= 22.0 ? 1.0 : r;
   r = x < 0.0 ? -r : r;
@@ -422,7 +437,7 @@ LDPC_HD double log_fast_f64(double q) {
   m = lo ? m + m : m;
   k = lo ? k - 1 : k;
   const double f = m - 1.0;  // exact
-  const double s = f / (2.0 + f);
+  const double s = div_fast(f, 2.0 + f);
   const double z = s * s;
   const double w = z * z;
   const double t1 = w * fma_(w, fma_(w, Lg6, Lg4), Lg2);

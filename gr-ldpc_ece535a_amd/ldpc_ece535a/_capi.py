@@ -44,6 +44,7 @@ SIGNATURES = {
     "ldpc_decode_device": (_i, [_vp, _i, _i, _i, _i, _vp, _i64, _i, ctypes.c_float, _i,
                                 _vp, _vp, _vp, _vp, _vp, _vp]),
     "ldpc_set_waves_per_cu": (_i, [_vp, _i]),
+    "ldpc_set_schedule": (_i, [_vp, _i]),
     "ldpc_synchronize": (_i, [_vp]),
 }
 
@@ -190,6 +191,10 @@ class Decoder:
 
     def set_waves_per_cu(self, n):
         _check(lib().ldpc_set_waves_per_cu(self._ctx, int(n)), self._ctx)
+
+    def set_schedule(self, mode):
+        """0 auto, 1 one wave per frame, 2 one workgroup per frame."""
+        _check(lib().ldpc_set_schedule(self._ctx, int(mode)), self._ctx)
 
     def synchronize(self):
         _check(lib().ldpc_synchronize(self._ctx), self._ctx)

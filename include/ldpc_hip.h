@@ -154,6 +154,12 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
  * Frames are pulled from a per-launch queue by that many resident waves. */
 int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu);
 
+/* Tuning: kernel schedule.  0 (default) chooses by batch size; 1 decodes
+ * one frame per wave (throughput regime); 2 one frame per workgroup of
+ * ceil(E/64) waves, one edge per lane (latency regime, small batches).
+ * Results are identical across schedules. */
+int ldpc_set_schedule(ldpc_ctx *ctx, int schedule);
+
 /* Blocks until the context's stream is idle. */
 int ldpc_synchronize(ldpc_ctx *ctx);
 

@@ -12,14 +12,30 @@ def dec():
     return ldpc_ece535a.Decoder()  # default H, reordered like the block
 
 
+@pytest.fixture(scope="module")
+def dec_by_schedule():
+    import ldpc_ece535a
+    out = {}
+    for sched in (1, 2):
+        d = ldpc_ece535a.Decoder()
+        d.set_schedule(sched)
+        out[sched] = d
+    return out
+
+
+@pytest.mark.parametrize("sched", [1, 2])
+@pytest.mark.parametrize("prec", [0, 2])
 @pytest.mark.parametrize("db", [0, 2, 4])
 @pytest.mark.parametrize("method", [0, 1, 2, 3])
 @pytest.mark.parametrize("iters", [5, 50])
-def test_default_h_fixtures_f64(dec, golden, db, method, iters):
+def test_default_h_fixtures_f64(dec_by_schedule, golden, db, method, iters, prec, sched):
+    """Both f64 modes, both kernel schedules (one wave per frame / one
+    workgroup per frame) against the oracle's fixtures."""
+    dec = dec_by_schedule[sched]
     fd = golden("frames_default.npz")
     assert (dec.H == fd["H_reordered"]).all()
     llr = fd["db%d_llr" % db]
-    out = dec.decode(llr, method=method, max_iters=iters, precision=0, want_llr=True)
+    out = dec.decode(llr, method=method, max_iters=iters, precision=prec, want_llr=True)
     key = "db%d_m%d_i%d" % (db, method, iters)
     np.testing.assert_array_equal(out["bits"], fd[key + "_bits"])
     np.testing.assert_array_equal(out["packed"], fd[key + "_packed"])

@@ -23,11 +23,13 @@ def frames(Hr, B, db, seed):
     return (x + np.sqrt(10 ** (-db / 10)) * rng.standard_normal(x.shape)).astype(np.float32)
 
 
-@pytest.mark.parametrize("method,db", [(1, 0.0), (1, 1.0), (1, 2.0), (1, 3.0), (0, 0.0),
-                                       (0, 2.0), (0, 4.0), (2, 2.0)])
-def test_parity_16k(dec, method, db):
+@pytest.mark.parametrize("method,db,sched", [(1, 0.0, 1), (1, 1.0, 2), (1, 2.0, 1), (1, 2.0, 2),
+                                             (1, 3.0, 1), (0, 0.0, 2), (0, 2.0, 1), (0, 4.0, 2),
+                                             (2, 2.0, 0)])
+def test_parity_16k(dec, method, db, sched):
     from oracle import oracle as orc
     y = frames(dec.H, 16384, db, seed=int(100 + 10 * db + method))
+    dec.set_schedule(sched)
     out = dec.decode(y, method=method, max_iters=50)
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     ref = orc.decode_batch(method, dec.H, y, 50, nthreads=threads)
