@@ -45,8 +45,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096)
-    ap.add_argument("--method", type=int, default=1)
+    ap.add_argument("--code", choices=["default", "dvbs2"], default="default",
+                    help="default: the reference's 32x64 H (config 2); dvbs2: the DVB-S2-size "
+                         "code of config 4 (synthetic rate-1/2 address table)")
+    ap.add_argument("--batch", type=int, default=None, help="default 4096 (1024 for dvbs2)")
+    ap.add_argument("--method", type=int, default=None, help="default 1 (0 for dvbs2)")
+    ap.add_argument("--no-config4", action="store_true", help="skip the config-4 variant")
     ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--et-period", type=int, default=1)
@@ -65,6 +69,55 @@ def parse():
                     help="method:precision list for the sweeps")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
+
+
+def synth_csr(csr, B, ebn0, seed):
+    """Config 4: PCG64 info bits, IRA encode (ldpc_ece535a.codes), BPSK, AWGN."""
+    from ldpc_ece535a import codes
+    M, N = csr[0], csr[1]
+    rng = np.random.Generator(np.random.PCG64(seed))
+    data = rng.integers(0, 2, size=(B, N - M), dtype=np.uint8)
+    cw = codes.ira_encode(csr, data)
+    sigma = np.sqrt(10.0 ** (-ebn0 / 10.0))
+    y = (2.0 * cw.astype(np.float64) - 1.0 + sigma * rng.standard_normal((B, N)))
+    return y.astype(np.float32), data
+
+
+def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
+    """DVB-S2-like N=64800 code, min-sum f64, 1024 frames (config 4) on the
+    large-code path; optional parity of the first frames vs the sparse oracle."""
+    from ldpc_ece535a import codes
+    csr = codes.dvbs2_like(0)
+    dec = L.Decoder(csr=csr, device=dev.index or 0)
+    B = 1024
+    y, data = synth_csr(csr, B, args.ebn0, seed)
+    d_y = torch.from_numpy(y).to(dev)
+    out = {}
+    for name, p in (("f64", 0), ("f32", 1)):
+        w, k, it, o = time_decoder(dec, torch, d_y, B, 0, args.iters, 1, p, steps, warmup)
+        alg = float(B * (4 * dec.N + dec.KB + 8) + it.sum() * bytes_per_iter(dec.E, dec.N, p))
+        pk = o[0].cpu().numpy()
+        out["min-sum " + name] = {
+            "Mbit/s": round(B * dec.K * steps / w / 1e6, 2), "ms_per_decode": round(k, 4),
+            "mean_iters": round(float(it.mean()), 3), "max_iters": int(it.max()),
+            "alg_GB/s": round(alg / (k * 1e-3) / 1e9, 1),
+            "frames_decoded_to_sent_data": int((pk == np.packbits(data, axis=1)).all(axis=1).sum())}
+        if p == 0 and cpu_sample:
+            from oracle import oracle as orc
+            t0 = time.perf_counter()
+            ref = orc.decode_batch_sparse(0, csr[2], csr[3], csr[0], csr[1], y[:cpu_sample],
+                                          args.iters, nthreads=16, want_bits=False)
+            cpu_s = time.perf_counter() - t0
+            out["min-sum f64"]["parity_sample"] = {
+                "frames": cpu_sample,
+                "packed_mismatch_frames": int((ref["packed"] != pk[:cpu_sample]).any(axis=1).sum()),
+                "iters_mismatch_frames": int((ref["iters"] != it[:cpu_sample]).sum()),
+                "checker": "oracle sparse restatement (orc_decode_batch_sparse)",
+                "cpu_Mbit/s_16_threads": round(cpu_sample * dec.K / cpu_s / 1e6, 4)}
+    out["code"] = ("DVB-S2-like N=64800 K=32400 E=226799 (synthetic rate-1/2 address table, "
+                   "ldpc_ece535a.codes.dvbs2_like(0)), B=1024, %d-iteration cap" % args.iters)
+    dec.close()
+    return out
 
 
 def synth(Hr, B, ebn0, seed):
@@ -138,13 +191,28 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     prec = 0 if args.precision == "f64" else 1
+    dvb = args.code == "dvbs2"
+    if args.method is None:
+        args.method = 0 if dvb else 1
+    if args.batch is None:
+        args.batch = 1024 if dvb else 4096
 
-    dec = L.Decoder(device=local)  # default H, reorderHMatrix applied
-    dec.set_waves_per_cu(args.waves_per_cu)
-    dec.set_schedule(args.schedule)
-    Hr = dec.H
+    csr = None
+    if dvb:
+        from ldpc_ece535a import codes
+        csr = codes.dvbs2_like(0)
+        dec = L.Decoder(csr=csr, device=local)
+        Hr = None
+    else:
+        dec = L.Decoder(device=local)  # default H, reorderHMatrix applied
+        dec.set_waves_per_cu(args.waves_per_cu)
+        dec.set_schedule(args.schedule)
+        Hr = dec.H
     B = args.batch
-    llr, data = synth(Hr, B, args.ebn0, args.seed + 7919 * rank)
+    if dvb:
+        llr, data = synth_csr(csr, B, args.ebn0, args.seed + 7919 * rank)
+    else:
+        llr, data = synth(Hr, B, args.ebn0, args.seed + 7919 * rank)
     d_in = torch.from_numpy(llr).to(dev)  # resident in HBM before timing
 
     if args.sweep_batch:
@@ -205,7 +273,8 @@ def main():
     alg_bytes = float(B * (4 * N + dec.KB + 8) + iters_b.sum() * bytes_per_iter(E, N, prec))
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
-    workload_key = "sp%d_%s_b%d_i%d_db%g" % (args.method, args.precision, B, args.iters, args.ebn0)
+    workload_key = "%s%d_%s_b%d_i%d_db%g" % ("dvb" if dvb else "sp", args.method, args.precision, B,
+                                            args.iters, args.ebn0)
     try:
         tj = json.load(open(args.traffic_json))
         if workload_key in tj:
@@ -213,6 +282,16 @@ def main():
     except (OSError, ValueError, KeyError):
         pass
 
+    mname = {0: "min-sum", 1: "sum-product", 2: "bit-flip", 3: "hard"}[args.method]
+    if dvb:
+        workload = ("config4: DVB-S2-like N=64800 K=32400 E=226799 code (synthetic rate-1/2 "
+                    "address table), large-code path (messages in HBM), B=%d frames/GPU, "
+                    "method %d (%s), %d-iteration cap with per-frame early exit, Eb/N0 %g dB"
+                    % (B, args.method, mname, args.iters, args.ebn0))
+    else:
+        workload = ("config2: reference default 32x64 H (reordered), B=%d frames/GPU, "
+                    "method %d (%s), %d-iteration cap with per-frame early exit, "
+                    "Eb/N0 %g dB" % (B, args.method, mname, args.iters, args.ebn0))
     line = {
         "metric": "decoded info Mbit/s @ 50 BP iters, batch=4096; achieved HBM GB/s vs peak",
         "value": round(value, 3),
@@ -227,11 +306,7 @@ def main():
         "dtype": args.precision,
         "data": "synthetic (PCG64 bits, GF(2) encode, BPSK, AWGN sigma=sqrt(10^(-EbN0/10)))",
         "config": {
-            "workload": "config2: reference default 32x64 H (reordered), B=%d frames/GPU, "
-                        "method %d (%s), %d-iteration cap with per-frame early exit, "
-                        "Eb/N0 %g dB" % (B, args.method,
-                                         {0: "min-sum", 1: "sum-product", 2: "bit-flip",
-                                          3: "hard"}[args.method], args.iters, args.ebn0),
+            "workload": workload,
             "global_batch": int(totals[0]),
             "frames_per_gpu": B,
             "parallelism": "dp%d (independent frames)" % world,
@@ -253,7 +328,7 @@ def main():
 
     # ---- variants measured in the same process (not the headline) ----------
     variant_outs = {}
-    if not args.no_variants:
+    if not args.no_variants and not dvb:
         var = {}
         for name, (m, p) in {"sum-product f32": (1, 1), "sum-product f64": (1, 0),
                              "min-sum f64": (0, 0), "min-sum f32": (0, 1)}.items():
@@ -278,6 +353,24 @@ def main():
         except AttributeError:
             ncpu = os.cpu_count() or 1
         threads = args.cpu_threads or max(1, min(16, ncpu))
+        if dvb:  # bounded sample: the sparse restatement on the first 128 frames
+            nb = min(B, 128)
+            t0 = time.perf_counter()
+            ref = orc.decode_batch_sparse(args.method, csr[2], csr[3], csr[0], csr[1], llr[:nb],
+                                          args.iters, nthreads=threads, want_bits=False)
+            cpu_s = time.perf_counter() - t0
+            line["cpu_baseline"] = {
+                "value": round(nb * dec.K / cpu_s / 1e6, 5), "unit": "Mbit/s", "cores": threads,
+                "kind": "port",
+                "sample": "first %d of rank 0's %d frames, sparse oracle, %d threads" % (nb, B, threads)}
+            line["parity"] = {"frames": nb,
+                              "packed_mismatch_frames": int((ref["packed"] != packed[:nb]).any(axis=1).sum()),
+                              "iters_mismatch_frames": int((ref["iters"] != iters_b[:nb]).sum()),
+                              "checker": "oracle sparse restatement (orc_decode_batch_sparse)"}
+            print(json.dumps(line), flush=True)
+            if dist is not None:
+                dist.destroy_process_group()
+            return
         t0 = time.perf_counter()
         ref = orc.decode_batch(args.method, Hr, llr, args.iters, nthreads=threads)
         cpu_s = time.perf_counter() - t0
@@ -303,6 +396,9 @@ def main():
                 refs[m] = orc.decode_batch(m, Hr, llr, args.iters, nthreads=threads)
             line["variants_1gpu"][name]["packed_mismatch_frames"] = int(
                 (refs[m]["packed"] != pk).any(axis=1).sum())
+    if not args.no_variants and not dvb and not args.no_config4:
+        line.setdefault("variants_1gpu", {})["config4"] = config4_variant(
+            L, torch, dev, args, args.seed + 31, cpu_sample=0 if args.no_cpu_baseline else 64)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

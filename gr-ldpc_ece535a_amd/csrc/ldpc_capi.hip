@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/ldpc_hip.h"
+#include "ldpc_graph.hpp"
 #include "ldpc_kernels.hpp"
 
 using ldpc::ColRec;
@@ -37,6 +38,13 @@ struct ldpc_ctx {
   unsigned launch_seq = 0;
   int waves_per_cu = 0;           // 0: kernel default
   int schedule = 0;               // 0 auto, 1 wave per frame, 2 workgroup per frame
+  // large-code path (ldpc_graph.hip): H as CSR + CSC, messages in a workspace
+  bool graph = false;
+  std::vector<int32_t> rp, ci;    // host CSR of the decoder's H
+  int32_t *d_rp = nullptr, *d_ci = nullptr, *d_cp = nullptr, *d_ce = nullptr, *d_cr = nullptr;
+  void *d_work = nullptr;
+  size_t work_bytes = 0;
+  size_t work_limit = (size_t)8 << 30;
   std::string err;
 };
 
@@ -221,6 +229,82 @@ int check_decode_args(ldpc_ctx *ctx, int &method, int max_iters, int et_period, 
   return LDPC_OK;
 }
 
+// CSR of a dense H (edges row-major, ascending column).
+void dense_to_csr(const uint8_t *H, int M, int N, std::vector<int32_t> &rp,
+                  std::vector<int32_t> &ci) {
+  rp.assign((size_t)M + 1, 0);
+  ci.clear();
+  for (int j = 0; j < M; ++j) {
+    for (int i = 0; i < N; ++i)
+      if (H[(size_t)j * N + i]) ci.push_back(i);
+    rp[j + 1] = (int32_t)ci.size();
+  }
+}
+
+bool valid_csr(int M, int N, const int32_t *rp, const int32_t *ci) {
+  if (!rp || M <= 0 || N <= 0 || M >= N || rp[0] != 0) return false;
+  for (int j = 0; j < M; ++j) {
+    if (rp[j + 1] < rp[j]) return false;
+    for (int32_t e = rp[j]; e < rp[j + 1]; ++e) {
+      if (!ci || ci[e] < 0 || ci[e] >= N) return false;
+      if (e > rp[j] && ci[e] <= ci[e - 1]) return false;  // ascending, no duplicates
+    }
+  }
+  return true;
+}
+
+// Degrees and the CSC permutation of the context's CSR; checks the
+// large-code kernels' degree limits.
+int build_graph(ldpc_ctx *ctx, std::vector<int32_t> &cp, std::vector<int32_t> &ce,
+                std::vector<int32_t> &cr) {
+  const int M = ctx->M, N = ctx->N;
+  ctx->E = ctx->rp[M];
+  if (ctx->E == 0) return set_err(ctx, LDPC_EINVAL, "H has no ones");
+  cp.assign((size_t)N + 1, 0);
+  for (int e = 0; e < ctx->E; ++e) cp[ctx->ci[e] + 1]++;
+  ctx->dc_max = 0;
+  ctx->dv_max = 0;
+  for (int i = 0; i < N; ++i) ctx->dv_max = std::max(ctx->dv_max, cp[i + 1]);
+  for (int j = 0; j < M; ++j) ctx->dc_max = std::max(ctx->dc_max, ctx->rp[j + 1] - ctx->rp[j]);
+  for (int i = 0; i < N; ++i) cp[i + 1] += cp[i];
+  ce.assign((size_t)ctx->E, 0);
+  cr.assign((size_t)ctx->E, 0);
+  std::vector<int32_t> fill(cp.begin(), cp.end() - 1);
+  for (int j = 0; j < M; ++j)
+    for (int32_t e = ctx->rp[j]; e < ctx->rp[j + 1]; ++e) {
+      const int32_t k = fill[ctx->ci[e]]++;  // rows ascend because j ascends
+      ce[k] = e;
+      cr[k] = j;
+    }
+  if (ctx->dc_max > ldpc::kGraphDcMax || ctx->dv_max > ldpc::kGraphDvMax) {
+    char buf[160];
+    snprintf(buf, sizeof buf,
+             "code degrees outside the large-code kernels (dc_max=%d dv_max=%d; limits %d, %d)",
+             ctx->dc_max, ctx->dv_max, ldpc::kGraphDcMax, ldpc::kGraphDvMax);
+    return set_err(ctx, LDPC_EUNSUPPORTED, buf);
+  }
+  ctx->K = N - M;
+  ctx->KB = (ctx->K + 7) / 8;
+  ctx->graph = true;
+  return LDPC_OK;
+}
+
+ldpc::GraphView graph_view(const ldpc_ctx *ctx) {
+  ldpc::GraphView g;
+  g.rp = ctx->d_rp;
+  g.ci = ctx->d_ci;
+  g.cp = ctx->d_cp;
+  g.ce = ctx->d_ce;
+  g.cr = ctx->d_cr;
+  g.M = ctx->M;
+  g.N = ctx->N;
+  g.E = ctx->E;
+  g.KB = ctx->KB;
+  g.dc_max = ctx->dc_max;
+  g.dv_max = ctx->dv_max;
+  return g;
+}
+
 ldpc::CodeView code_view(const ldpc_ctx *ctx) {
   ldpc::CodeView v;
   v.erow = ctx->d_erow;
@@ -233,6 +317,45 @@ ldpc::CodeView code_view(const ldpc_ctx *ctx) {
   v.KB = ctx->KB;
   v.rs = ctx->rs;
   return v;
+}
+
+// Large-code path: frames in groups that fit the workspace limit, each group
+// decoded by launch_graph_decode on `st`.
+int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int precision, void *st) {
+  const ldpc::GraphView g = graph_view(ctx);
+  const bool want_post = a.llr != nullptr;
+  const size_t per64 = ldpc::graph_work_bytes(g, 64, precision, method, want_post);
+  int group = (int)std::min<size_t>((size_t)1 << 30, std::max<size_t>(1, ctx->work_limit / per64) * 64);
+  group = std::min(group, (a.B + 63) / 64 * 64);
+  const size_t need = ldpc::graph_work_bytes(g, group, precision, method, want_post);
+  if (need > ctx->work_bytes) {
+    if (ctx->d_work) {
+      (void)hipDeviceSynchronize();  // the old workspace may be in use on any stream
+      (void)hipFree(ctx->d_work);
+      ctx->d_work = nullptr;
+      ctx->work_bytes = 0;
+    }
+    hipError_t e = hipMalloc(&ctx->d_work, need);
+    if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(graph workspace)");
+    ctx->work_bytes = need;
+  }
+  for (int b0 = 0; b0 < a.B; b0 += group) {
+    const int nb = std::min(group, a.B - b0);
+    ldpc::GraphWork w;
+    ldpc::graph_work_carve(w, ctx->d_work, g, (nb + 63) / 64 * 64, precision, method, want_post);
+    ldpc::DecodeArgs s = a;
+    s.in = a.in + (int64_t)b0 * a.cw_stride;
+    s.B = nb;
+    s.packed = a.packed + (int64_t)b0 * ctx->KB;
+    if (a.bits) s.bits = a.bits + (int64_t)b0 * ctx->N;
+    if (a.iters) s.iters = a.iters + b0;
+    if (a.synd) s.synd = a.synd + b0;
+    if (a.llr) s.llr = a.llr + (int64_t)b0 * ctx->N;
+    const int rc = ldpc::launch_graph_decode(g, w, s, method, precision, st);
+    if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "code degrees outside the large-code kernels");
+    if (rc != 0) return hip_err(ctx, hipGetLastError(), "graph kernel launch");
+  }
+  return LDPC_OK;
 }
 
 }  // namespace
@@ -305,23 +428,40 @@ int ldpc_encode(const uint8_t *Hr, int M, int N, const uint8_t *data_bits, int B
   return LDPC_OK;
 }
 
-ldpc_ctx *ldpc_create(const uint8_t *H, int M, int N, int flags, int device) {
-  g_create_error.clear();
-  if (!valid_h(H, M, N)) {
-    set_err(nullptr, LDPC_EINVAL, "H must be M x N (M < N) with 0/1 entries");
-    return nullptr;
+}  // extern "C"
+
+namespace {
+
+template <typename T>
+bool upload(ldpc_ctx *ctx, T **dst, const std::vector<T> &src, const char *what,
+            const char *&failed, hipError_t &e) {
+  if (failed) return false;
+  if ((e = hipMalloc((void **)dst, std::max<size_t>(src.size(), 1) * sizeof(T))) != hipSuccess ||
+      (!src.empty() &&
+       (e = hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice)) !=
+           hipSuccess)) {
+    failed = what;
+    return false;
   }
-  ldpc_ctx *ctx = new ldpc_ctx();
-  ctx->M = M;
-  ctx->N = N;
-  ctx->device = device;
-  ctx->H.assign(H, H + (size_t)M * N);
-  if (!(flags & LDPC_FLAG_NO_REORDER)) reorder_columns(ctx->H.data(), M, N, nullptr, nullptr, nullptr);
+  return true;
+}
+
+// Device setup shared by ldpc_create / ldpc_create_csr: the context's H is
+// in ctx->rp / ctx->ci (and ctx->H for small codes).  Picks the small-code
+// kernel when the code fits it (unless LDPC_FLAG_GRAPH), else the large-code
+// path.  Consumes ctx on failure.
+ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
   std::vector<EdgeRowRec> erecs;
   std::vector<EdgeColRec> crecs;
   std::vector<ColRec> cols;
   std::vector<uint64_t> rowmask;
-  int rc = build_tables(ctx, erecs, crecs, cols, rowmask);
+  std::vector<int32_t> cp, ce, cr;
+  int rc = LDPC_EUNSUPPORTED;
+  if (!(flags & LDPC_FLAG_GRAPH) && !ctx->H.empty()) rc = build_tables(ctx, erecs, crecs, cols, rowmask);
+  if (rc == LDPC_EUNSUPPORTED) {
+    ctx->err.clear();
+    rc = build_graph(ctx, cp, ce, cr);
+  }
   if (rc != LDPC_OK) {
     g_create_error = ctx->err;
     delete ctx;
@@ -336,42 +476,72 @@ ldpc_ctx *ldpc_create(const uint8_t *H, int M, int N, int flags, int device) {
     delete ctx;
     return nullptr;
   }
+  ctx->device = device;
   const char *what = nullptr;
   if ((e = hipSetDevice(device)) != hipSuccess) what = "hipSetDevice";
   if (!what && (e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
     what = "hipStreamCreate";
-  if (!what && (e = hipMalloc(&ctx->d_erow, erecs.size() * sizeof(EdgeRowRec))) != hipSuccess)
-    what = "hipMalloc(erow)";
-  if (!what && (e = hipMalloc(&ctx->d_ecol, crecs.size() * sizeof(EdgeColRec))) != hipSuccess)
-    what = "hipMalloc(ecol)";
-  if (!what && (e = hipMalloc(&ctx->d_cols, cols.size() * sizeof(ColRec))) != hipSuccess)
-    what = "hipMalloc(cols)";
-  if (!what && (e = hipMalloc(&ctx->d_rowmask, rowmask.size() * 8)) != hipSuccess)
-    what = "hipMalloc(rowmask)";
-  if (!what && (e = hipMalloc(&ctx->d_tickets, LDPC_TICKET_RING * sizeof(uint32_t))) !=
-                   hipSuccess)
-    what = "hipMalloc(tickets)";
-  if (!what && (e = hipMemset(ctx->d_tickets, 0, LDPC_TICKET_RING * sizeof(uint32_t))) !=
-                   hipSuccess)
-    what = "hipMemset(tickets)";
-  if (!what && (e = hipMemcpy(ctx->d_erow, erecs.data(), erecs.size() * sizeof(EdgeRowRec),
-                              hipMemcpyHostToDevice)) != hipSuccess)
-    what = "hipMemcpy(erow)";
-  if (!what && (e = hipMemcpy(ctx->d_ecol, crecs.data(), crecs.size() * sizeof(EdgeColRec),
-                              hipMemcpyHostToDevice)) != hipSuccess)
-    what = "hipMemcpy(ecol)";
-  if (!what && (e = hipMemcpy(ctx->d_cols, cols.data(), cols.size() * sizeof(ColRec),
-                              hipMemcpyHostToDevice)) != hipSuccess)
-    what = "hipMemcpy(cols)";
-  if (!what && (e = hipMemcpy(ctx->d_rowmask, rowmask.data(), rowmask.size() * 8,
-                              hipMemcpyHostToDevice)) != hipSuccess)
-    what = "hipMemcpy(rowmask)";
+  if (ctx->graph) {
+    upload(ctx, &ctx->d_rp, ctx->rp, "upload(row_ptr)", what, e);
+    upload(ctx, &ctx->d_ci, ctx->ci, "upload(col_idx)", what, e);
+    upload(ctx, &ctx->d_cp, cp, "upload(col_ptr)", what, e);
+    upload(ctx, &ctx->d_ce, ce, "upload(col_edges)", what, e);
+    upload(ctx, &ctx->d_cr, cr, "upload(col_rows)", what, e);
+  } else {
+    upload(ctx, &ctx->d_erow, erecs, "upload(erow)", what, e);
+    upload(ctx, &ctx->d_ecol, crecs, "upload(ecol)", what, e);
+    upload(ctx, &ctx->d_cols, cols, "upload(cols)", what, e);
+    upload(ctx, &ctx->d_rowmask, rowmask, "upload(rowmask)", what, e);
+    std::vector<uint32_t> zeros(LDPC_TICKET_RING, 0);
+    upload(ctx, &ctx->d_tickets, zeros, "upload(tickets)", what, e);
+  }
   if (what) {
     g_create_error = std::string(what) + ": " + hipGetErrorString(e);
     ldpc_destroy(ctx);
     return nullptr;
   }
   return ctx;
+}
+
+}  // namespace
+
+extern "C" {
+
+ldpc_ctx *ldpc_create(const uint8_t *H, int M, int N, int flags, int device) {
+  g_create_error.clear();
+  if (!valid_h(H, M, N)) {
+    set_err(nullptr, LDPC_EINVAL, "H must be M x N (M < N) with 0/1 entries");
+    return nullptr;
+  }
+  ldpc_ctx *ctx = new ldpc_ctx();
+  ctx->M = M;
+  ctx->N = N;
+  ctx->H.assign(H, H + (size_t)M * N);
+  if (!(flags & LDPC_FLAG_NO_REORDER)) reorder_columns(ctx->H.data(), M, N, nullptr, nullptr, nullptr);
+  dense_to_csr(ctx->H.data(), M, N, ctx->rp, ctx->ci);
+  return finish_create(ctx, flags, device);
+}
+
+ldpc_ctx *ldpc_create_csr(int M, int N, const int32_t *row_ptr, const int32_t *col_idx,
+                          int flags, int device) {
+  g_create_error.clear();
+  if (!valid_csr(M, N, row_ptr, col_idx)) {
+    set_err(nullptr, LDPC_EINVAL,
+            "CSR H must be M x N (M < N), row_ptr[0] == 0, non-decreasing, columns ascending "
+            "and in range");
+    return nullptr;
+  }
+  ldpc_ctx *ctx = new ldpc_ctx();
+  ctx->M = M;
+  ctx->N = N;
+  ctx->rp.assign(row_ptr, row_ptr + M + 1);
+  ctx->ci.assign(col_idx, col_idx + row_ptr[M]);
+  if (N <= ldpc::kNMax && M <= ldpc::kMMax) {  // small enough for the register kernel
+    ctx->H.assign((size_t)M * N, 0);
+    for (int j = 0; j < M; ++j)
+      for (int32_t e = row_ptr[j]; e < row_ptr[j + 1]; ++e) ctx->H[(size_t)j * N + col_idx[e]] = 1;
+  }
+  return finish_create(ctx, flags, device);
 }
 
 void ldpc_destroy(ldpc_ctx *ctx) {
@@ -383,6 +553,9 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->d_rowmask) (void)hipFree(ctx->d_rowmask);
   if (ctx->d_stage) (void)hipFree(ctx->d_stage);
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
+  for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
+    if (p) (void)hipFree(p);
+  if (ctx->d_work) (void)hipFree(ctx->d_work);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -406,7 +579,27 @@ int ldpc_ctx_info(const ldpc_ctx *ctx, int *M, int *N, int *E, int *K, int *KB, 
 
 int ldpc_ctx_h(const ldpc_ctx *ctx, uint8_t *H_out) {
   if (!ctx || !H_out) return LDPC_EINVAL;
-  memcpy(H_out, ctx->H.data(), ctx->H.size());
+  memset(H_out, 0, (size_t)ctx->M * ctx->N);
+  for (int j = 0; j < ctx->M; ++j)
+    for (int32_t e = ctx->rp[j]; e < ctx->rp[j + 1]; ++e) H_out[(size_t)j * ctx->N + ctx->ci[e]] = 1;
+  return LDPC_OK;
+}
+
+int ldpc_ctx_csr(const ldpc_ctx *ctx, int32_t *row_ptr_out, int32_t *col_idx_out) {
+  if (!ctx) return LDPC_EINVAL;
+  if (row_ptr_out) memcpy(row_ptr_out, ctx->rp.data(), ctx->rp.size() * sizeof(int32_t));
+  if (col_idx_out) memcpy(col_idx_out, ctx->ci.data(), ctx->ci.size() * sizeof(int32_t));
+  return LDPC_OK;
+}
+
+int ldpc_ctx_path(const ldpc_ctx *ctx) {
+  if (!ctx) return LDPC_EINVAL;
+  return ctx->graph ? 1 : 0;
+}
+
+int ldpc_set_work_limit(ldpc_ctx *ctx, int64_t bytes) {
+  if (!ctx || bytes < 0) return set_err(ctx, LDPC_EINVAL, "work limit must be >= 0");
+  ctx->work_limit = bytes ? (size_t)bytes : ((size_t)8 << 30);
   return LDPC_OK;
 }
 
@@ -433,12 +626,13 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   a.iters = d_iters_used_opt;
   a.synd = d_syn_weight_opt;
   a.llr = d_llr_out_opt;
-  a.ticket = ctx->d_tickets + (ctx->launch_seq % LDPC_TICKET_RING);
-  a.ticket_next = ctx->d_tickets + ((ctx->launch_seq + 1) % LDPC_TICKET_RING);
-  a.waves = 0;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   void *st = hip_stream ? hip_stream : (void *)ctx->stream;
+  if (ctx->graph) return decode_graph(ctx, a, method, precision, st);
+  a.ticket = ctx->d_tickets + (ctx->launch_seq % LDPC_TICKET_RING);
+  a.ticket_next = ctx->d_tickets + ((ctx->launch_seq + 1) % LDPC_TICKET_RING);
+  a.waves = 0;
   rc = ldpc::launch_decode(code_view(ctx), a, method, precision, ctx->slots, ctx->nw,
                            ctx->waves_per_cu, ctx->schedule, st);
   if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no kernel for this code shape");

@@ -1,0 +1,63 @@
+// ldpc_graph.hpp -- host/device types of the large-code decode path.
+//
+// Codes beyond the small-code kernel's register/LDS budget (SURVEY 8(d)
+// config 4: DVB-S2-size N = 64800, E = 226799) keep their messages in HBM.
+// H is held as CSR (edges numbered row-major, ascending column) plus a CSC
+// permutation of those edge ids (ascending row within a column): the two
+// orders the reference's dense scans visit a row's and a column's ones in
+// (lib/ldpc_decoder_cb_impl.cc:350-403, :503-553).
+//
+// Every per-frame array is frame-minor: element x of frame b sits at
+// x * Bp + b, Bp = the group's frame count rounded up to 64, so one wave
+// (64 lanes = 64 consecutive frames) moves 64 consecutive values of one
+// edge / column / row.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ldpc_kernels.hpp"
+
+namespace ldpc {
+
+constexpr int kGraphDcMax = 32;  // check degree limit of the large-code kernels
+constexpr int kGraphDvMax = 16;  // variable degree limit
+
+struct GraphView {
+  const int32_t *rp;  // M + 1 row offsets into the CSR edge list
+  const int32_t *ci;  // E: column of CSR edge e
+  const int32_t *cp;  // N + 1 column offsets into ce / cr
+  const int32_t *ce;  // E: CSR edge ids, column by column, rows ascending
+  const int32_t *cr;  // E: the row of ce[k]
+  int M, N, E, KB, dc_max, dv_max;
+};
+
+struct GraphWork {
+  void *Q;             // E x Bp Real: variable -> check messages
+  void *R;             // E x Bp Real: check -> variable messages
+  float *L;            // N x Bp: -tx (Lci of min-sum, r of sum-product; exact in
+                       //   float because tx is a float)
+  // bit-packed per 64-frame chunk: word x * chunks + k, bit = lane (frame)
+  uint64_t *hard;      // N words per chunk: current hard decision
+  uint64_t *y;         // N: bit-flip's received hard decision
+  uint64_t *rowpar;    // M: bit-flip's row parities
+  uint64_t *synd_part; // check waves x chunks: "this wave saw an odd row" per frame
+  uint64_t *done_w;    // chunks: frames that stopped (early exit or padding)
+  uint8_t *chunk_done; // chunks: all 64 frames stopped
+  int32_t *used;       // Bp: iterations executed
+  int32_t *synd;       // Bp: final syndrome weight
+  float *post;         // N x Bp: final posterior (only with an llr output)
+  int Bp, chunks, check_waves;
+};
+
+// Bytes of workspace for Bp frames (Bp a multiple of 64).
+size_t graph_work_bytes(const GraphView &g, int Bp, int prec, int method, bool want_post);
+// Lays a workspace of graph_work_bytes() bytes out at base.
+void graph_work_carve(GraphWork &w, void *base, const GraphView &g, int Bp, int prec,
+                      int method, bool want_post);
+// Decodes args.B <= w.Bp frames (all launches enqueued on `stream`).
+// Returns 0, -2 for an unsupported degree, or -1 on a launch error.
+int launch_graph_decode(const GraphView &g, const GraphWork &w, const DecodeArgs &args,
+                        int method, int prec, void *stream);
+
+}  // namespace ldpc

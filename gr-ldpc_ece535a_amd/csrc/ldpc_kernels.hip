@@ -31,8 +31,8 @@
 
 #include <algorithm>
 
+#include "ldpc_device.hpp"
 #include "ldpc_kernels.hpp"
-#include "ldpc_math.hpp"
 
 namespace ldpc {
 
@@ -50,40 +50,6 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 #endif
-}
-
-// Arithmetic per precision mode (include/ldpc_hip.h LDPC_PREC_*):
-//   0 F64       double, compact tanh/log of ldpc_math.hpp (<= 3 ulp of glibc)
-//   1 F32       float, ROCm libm
-//   2 F64_LIBM  double, fdlibm tanh bit-identical to glibc's, fdlibm log
-template <int PREC>
-struct Math;
-template <>
-struct Math<0> {
-  typedef double Real;
-  static __device__ __forceinline__ double tanh_(double x) { return fm::tanh_fast_f64(x); }
-  static __device__ __forceinline__ double log_(double x) { return fm::log_fast_f64(x); }
-  static __device__ __forceinline__ double abs_(double x) { return ::fabs(x); }
-  static __device__ __forceinline__ double max_() { return DBL_MAX; }
-};
-template <>
-struct Math<2> : Math<0> {
-  static __device__ __forceinline__ double tanh_(double x) { return fm::tanh_f64_bf(x); }
-  static __device__ __forceinline__ double log_(double x) { return fm::log_f64_bf(x); }
-};
-template <>
-struct Math<1> {
-  typedef float Real;
-  static __device__ __forceinline__ float tanh_(float x) { return ::tanhf(x); }
-  static __device__ __forceinline__ float log_(float x) { return ::logf(x); }
-  static __device__ __forceinline__ float abs_(float x) { return ::fabsf(x); }
-  static __device__ __forceinline__ float max_() { return FLT_MAX; }
-};
-
-// sign(), lib/ldpc_decoder_cb_impl.cc:574-578 (sign(0) == 0).
-template <typename Real>
-__device__ __forceinline__ int sgn(Real v) {
-  return (v > Real(0)) - (v < Real(0));
 }
 
 template <int NW>

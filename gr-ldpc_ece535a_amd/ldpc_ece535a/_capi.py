@@ -17,6 +17,8 @@ HIP_LIB = os.path.join(LIB_DIR, "libldpc_hip.so")
 METHOD_LOGDOMAIN, METHOD_SUMPRODUCT, METHOD_BITFLIP, METHOD_HARD = 0, 1, 2, 3
 PREC_F64, PREC_F32, PREC_F64_LIBM = 0, 1, 2
 FLAG_NO_REORDER = 1
+FLAG_GRAPH = 2
+PATH_SMALL, PATH_GRAPH = 0, 1
 ERRORS = {0: "LDPC_OK", -1: "LDPC_EINVAL", -2: "LDPC_EUNSUPPORTED", -3: "LDPC_EDEVICE",
           -4: "LDPC_ESINGULAR", -5: "LDPC_ENOMEM"}
 
@@ -34,6 +36,10 @@ SIGNATURES = {
     "ldpc_check_frame": (_i, [_u8p, _i, _i, _u8p, _i]),
     "ldpc_encode": (_i, [_u8p, _i, _i, _u8p, _i, _u8p]),
     "ldpc_create": (_vp, [_u8p, _i, _i, _i, _i]),
+    "ldpc_create_csr": (_vp, [_i, _i, _i32p, _i32p, _i, _i]),
+    "ldpc_ctx_csr": (_i, [_vp, _i32p, _i32p]),
+    "ldpc_ctx_path": (_i, [_vp]),
+    "ldpc_set_work_limit": (_i, [_vp, _i64]),
     "ldpc_destroy": (None, [_vp]),
     "ldpc_last_error": (ctypes.c_char_p, [_vp]),
     "ldpc_ctx_info": (_i, [_vp, _i32p, _i32p, _i32p, _i32p, _i32p, _i32p, _i32p]),
@@ -118,22 +124,48 @@ def encode(Hr, data_bits):
 
 
 class Decoder:
-    """One decode context (device tables + stream) for one H."""
+    """One decode context (device tables + stream) for one H.
 
-    def __init__(self, H=None, reorder=True, device=0):
-        if H is None:
-            H = default_h()
-        H = np.ascontiguousarray(H, np.uint8)
-        M, N = H.shape
-        flags = 0 if reorder else FLAG_NO_REORDER
-        self._ctx = lib().ldpc_create(_p(H, _u8p), M, N, flags, int(device))
+    H: dense (M, N) 0/1 matrix (reorderHMatrix applied unless reorder=False),
+    or csr=(M, N, row_ptr, col_idx) for a sparse H used as given.
+    force_graph=True selects the large-code (HBM message) kernels even for a
+    code the small-code kernel could take."""
+
+    def __init__(self, H=None, reorder=True, device=0, csr=None, force_graph=False):
+        flags = (0 if reorder else FLAG_NO_REORDER) | (FLAG_GRAPH if force_graph else 0)
+        if csr is not None:
+            M, N, rp, ci = csr
+            rp = np.ascontiguousarray(rp, np.int32)
+            ci = np.ascontiguousarray(ci, np.int32)
+            self._ctx = lib().ldpc_create_csr(int(M), int(N), _p(rp, _i32p), _p(ci, _i32p),
+                                              flags, int(device))
+            what = "ldpc_create_csr"
+        else:
+            if H is None:
+                H = default_h()
+            H = np.ascontiguousarray(H, np.uint8)
+            M, N = H.shape
+            self._ctx = lib().ldpc_create(_p(H, _u8p), M, N, flags, int(device))
+            what = "ldpc_create"
         if not self._ctx:
-            raise LdpcError("ldpc_create failed: %s" % lib().ldpc_last_error(None).decode())
+            raise LdpcError("%s failed: %s" % (what, lib().ldpc_last_error(None).decode()))
         v = [ctypes.c_int32(0) for _ in range(7)]
         _check(lib().ldpc_ctx_info(self._ctx, *[ctypes.byref(x) for x in v]), self._ctx)
         self.M, self.N, self.E, self.K, self.KB, self.dc_max, self.dv_max = [x.value for x in v]
-        self.H = np.zeros((M, N), np.uint8)
-        _check(lib().ldpc_ctx_h(self._ctx, _p(self.H, _u8p)), self._ctx)
+        self.path = _check(lib().ldpc_ctx_path(self._ctx), self._ctx)
+        self.row_ptr = np.zeros(self.M + 1, np.int32)
+        self.col_idx = np.zeros(self.E, np.int32)
+        _check(lib().ldpc_ctx_csr(self._ctx, _p(self.row_ptr, _i32p), _p(self.col_idx, _i32p)),
+               self._ctx)
+        self._H = None
+
+    @property
+    def H(self):
+        """The decoder's (reordered) H as a dense (M, N) array (built on demand)."""
+        if self._H is None:
+            self._H = np.zeros((self.M, self.N), np.uint8)
+            _check(lib().ldpc_ctx_h(self._ctx, _p(self._H, _u8p)), self._ctx)
+        return self._H
 
     def close(self):
         if getattr(self, "_ctx", None):
@@ -191,6 +223,10 @@ class Decoder:
 
     def set_waves_per_cu(self, n):
         _check(lib().ldpc_set_waves_per_cu(self._ctx, int(n)), self._ctx)
+
+    def set_work_limit(self, nbytes):
+        """Large-code path: device workspace cap (0 = default 8 GiB)."""
+        _check(lib().ldpc_set_work_limit(self._ctx, int(nbytes)), self._ctx)
 
     def set_schedule(self, mode):
         """0 auto, 1 one wave per frame, 2 one workgroup per frame."""

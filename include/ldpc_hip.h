@@ -7,9 +7,11 @@
  * functions.  Each entry point below names the reference interface it
  * replaces (paths relative to the reference repository root):
  *
- *   ldpc_create / ldpc_destroy
+ *   ldpc_create / ldpc_create_csr / ldpc_destroy
  *       ldpc_decoder_cb_impl::ldpc_decoder_cb_impl(method)
- *       lib/ldpc_decoder_cb_impl.cc:35-117 (H setup + reorderHMatrix :104-106)
+ *       lib/ldpc_decoder_cb_impl.cc:35-117 (H setup + reorderHMatrix :104-106);
+ *       ldpc_create_csr takes H as a sparse row list, for codes whose dense
+ *       M x N matrix the reference could not hold
  *   ldpc_decode, ldpc_decode_strided, ldpc_decode_device
  *       decodeLogDomainSimple :309-412, decodeSumProductSoft :478-557,
  *       decodeBitFlipping :414-476, decodeHard :559-572 and the early-exit
@@ -55,6 +57,7 @@ extern "C" {
 
 /* ldpc_create flags */
 #define LDPC_FLAG_NO_REORDER 1 /* use H as given (skip reorderHMatrix) */
+#define LDPC_FLAG_GRAPH 2      /* force the large-code (HBM message) kernels */
 
 /* error codes */
 #define LDPC_OK 0
@@ -93,6 +96,16 @@ int ldpc_encode(const uint8_t *H_reordered, int M, int N,
  * LDPC_FLAG_NO_REORDER), uploads its edge tables to `device`.  Returns NULL
  * on failure; ldpc_last_error(NULL) then says why. */
 ldpc_ctx *ldpc_create(const uint8_t *H, int M, int N, int flags, int device);
+
+/* The same from a CSR H: row j's ones are at columns
+ * col_idx[row_ptr[j] .. row_ptr[j+1]-1], strictly ascending.  H is used as
+ * given (no reorderHMatrix: the decoder does not need it, and the reference's
+ * dense elimination is infeasible at DVB-S2 size).  The packed output holds
+ * columns M..N-1, so put the information bits last.  Codes within the
+ * small-code kernel's limits (N, M <= 256, E <= 512, dc <= 8, dv <= 4) use
+ * it; larger ones (dc <= 32, dv <= 16) keep their messages in HBM. */
+ldpc_ctx *ldpc_create_csr(int M, int N, const int32_t *row_ptr, const int32_t *col_idx,
+                          int flags, int device);
 void ldpc_destroy(ldpc_ctx *ctx);
 const char *ldpc_last_error(const ldpc_ctx *ctx);
 
@@ -102,6 +115,11 @@ int ldpc_ctx_info(const ldpc_ctx *ctx, int *M, int *N, int *E, int *K, int *KB,
                   int *dc_max, int *dv_max);
 /* Copies the context's (reordered) H, M x N bytes. */
 int ldpc_ctx_h(const ldpc_ctx *ctx, uint8_t *H_out);
+/* Copies the context's H as CSR (row_ptr: M+1, col_idx: E); either may be NULL. */
+int ldpc_ctx_csr(const ldpc_ctx *ctx, int32_t *row_ptr_out, int32_t *col_idx_out);
+/* 0: small-code kernel (frame per wave / workgroup, registers + LDS);
+ * 1: large-code kernels (messages in HBM). */
+int ldpc_ctx_path(const ldpc_ctx *ctx);
 
 /* ---- decode ------------------------------------------------------- */
 /* Common parameters:
@@ -159,6 +177,10 @@ int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu);
  * ceil(E/64) waves, one edge per lane (latency regime, small batches).
  * Results are identical across schedules. */
 int ldpc_set_schedule(ldpc_ctx *ctx, int schedule);
+
+/* Large-code path: device workspace cap in bytes (0 = default 8 GiB).  A
+ * batch larger than the cap allows is decoded in consecutive groups. */
+int ldpc_set_work_limit(ldpc_ctx *ctx, int64_t bytes);
 
 /* Blocks until the context's stream is idle. */
 int ldpc_synchronize(ldpc_ctx *ctx);

@@ -391,6 +391,269 @@ int orc_decode_batch(int method, const uint8_t *H, int M, int N, int iterations,
 }
 
 /* ------------------------------------------------------------------ */
+/* sparse restatements (large codes)                                    */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  int M, N, E;
+  const int32_t *rp, *ci;  /* CSR */
+  int32_t *cp, *ce;        /* CSC: column offsets, edge ids (ascending row) */
+  int32_t *erow;           /* row of each edge */
+} orc_graph;
+
+static void orc_graph_build(orc_graph *g, const int32_t *rp, const int32_t *ci, int M, int N) {
+  g->M = M;
+  g->N = N;
+  g->E = rp[M];
+  g->rp = rp;
+  g->ci = ci;
+  g->cp = (int32_t *)calloc((size_t)N + 1, sizeof(int32_t));
+  g->ce = (int32_t *)malloc(sizeof(int32_t) * (size_t)(g->E > 0 ? g->E : 1));
+  g->erow = (int32_t *)malloc(sizeof(int32_t) * (size_t)(g->E > 0 ? g->E : 1));
+  for (int e = 0; e < g->E; e++) g->cp[ci[e] + 1]++;
+  for (int c = 0; c < N; c++) g->cp[c + 1] += g->cp[c];
+  int32_t *fill = (int32_t *)malloc(sizeof(int32_t) * (size_t)N);
+  for (int c = 0; c < N; c++) fill[c] = g->cp[c];
+  for (int r = 0; r < M; r++)
+    for (int e = rp[r]; e < rp[r + 1]; e++) {
+      g->erow[e] = r;
+      g->ce[fill[ci[e]]++] = e; /* rows ascend because r ascends */
+    }
+  free(fill);
+}
+
+static void orc_graph_free(orc_graph *g) {
+  free(g->cp);
+  free(g->ce);
+  free(g->erow);
+}
+
+int orc_check_frame_sparse(const int32_t *row_ptr, const int32_t *col_idx, int M,
+                           const int *u, int threshold) {
+  int unsatisfied = 0;
+  for (int k = 0; k < M; k++) {
+    int dot = 0;
+    for (int e = row_ptr[k]; e < row_ptr[k + 1]; e++) dot += u[col_idx[e]];
+    if (dot % 2 != 0) unsatisfied++;
+    if (unsatisfied > threshold) break;
+  }
+  return unsatisfied;
+}
+
+/* decodeLogDomainSimple (:309-412) on adjacency lists */
+static int orc_minsum_sparse(const orc_graph *g, const double *rx, int iterations, int *vhat,
+                             double *post_opt) {
+  const int N = g->N, M = g->M, E = g->E;
+  double *Lci = (double *)malloc(sizeof(double) * N);
+  double *Lq = (double *)malloc(sizeof(double) * (size_t)(E > 0 ? E : 1));
+  double *Lr = (double *)calloc((size_t)(E > 0 ? E : 1), sizeof(double));
+  for (int i = 0; i < N; i++) Lci[i] = -rx[i];
+  for (int e = 0; e < E; e++) Lq[e] = Lci[g->ci[e]];
+  for (int i = 0; i < N; i++) vhat[i] = 0;
+  int used = iterations;
+  for (int it = 0; it < iterations; it++) {
+    for (int r = 0; r < M; r++) { /* horizontal step, :350-376 */
+      int sgn = 1;
+      for (int e = g->rp[r]; e < g->rp[r + 1]; e++) sgn *= orc_sign(Lq[e]);
+      for (int e = g->rp[r]; e < g->rp[r + 1]; e++) {
+        double lo = DBL_MAX;
+        for (int k = g->rp[r]; k < g->rp[r + 1]; k++)
+          if (k != e && fabs(Lq[k]) < lo) lo = fabs(Lq[k]);
+        Lr[e] = (double)(sgn * orc_sign(Lq[e])) * lo;
+      }
+    }
+    for (int c = 0; c < N; c++) { /* vertical step, :379-403 */
+      double s = 0.0;
+      for (int k = g->cp[c]; k < g->cp[c + 1]; k++) s += Lr[g->ce[k]];
+      for (int k = g->cp[c]; k < g->cp[c + 1]; k++) {
+        const int e = g->ce[k];
+        Lq[e] = Lci[c] + s - Lr[e];
+      }
+      const double LQ = Lci[c] + s;
+      vhat[c] = (LQ < 0) ? 1 : 0;
+      if (post_opt) post_opt[c] = LQ;
+    }
+    if (it + 1 < iterations && orc_check_frame_sparse(g->rp, g->ci, M, vhat, 0) == 0) {
+      used = it + 1;
+      break;
+    }
+  }
+  free(Lci);
+  free(Lq);
+  free(Lr);
+  return used;
+}
+
+/* decodeSumProductSoft (:478-557) on adjacency lists */
+static int orc_sumproduct_sparse(const orc_graph *g, const double *rx, int iterations,
+                                 int *vhat, double *post_opt) {
+  const int N = g->N, M = g->M, E = g->E;
+  double *r = (double *)malloc(sizeof(double) * N);
+  double *Q = (double *)malloc(sizeof(double) * (size_t)(E > 0 ? E : 1));
+  double *Ec = (double *)calloc((size_t)(E > 0 ? E : 1), sizeof(double));
+  for (int i = 0; i < N; i++) r[i] = -rx[i];
+  for (int e = 0; e < E; e++) Q[e] = r[g->ci[e]];
+  for (int i = 0; i < N; i++) vhat[i] = 0;
+  int used = iterations;
+  for (int it = 0; it < iterations; it++) {
+    for (int j = 0; j < M; j++) /* :503-516 */
+      for (int e = g->rp[j]; e < g->rp[j + 1]; e++) {
+        double T = 1.0;
+        for (int k = g->rp[j]; k < g->rp[j + 1]; k++)
+          if (k != e) T *= tanh(Q[k] / 2.0);
+        Ec[e] = log((1.0 + T) / (1.0 - T));
+      }
+    for (int i = 0; i < N; i++) { /* :519-532 */
+      double L = 0.0;
+      for (int k = g->cp[i]; k < g->cp[i + 1]; k++) L += Ec[g->ce[k]] + r[i];
+      vhat[i] = (L <= 0) ? 1 : 0;
+      if (post_opt) post_opt[i] = L;
+    }
+    if (orc_check_frame_sparse(g->rp, g->ci, M, vhat, 0) == 0) {
+      used = it + 1;
+      break;
+    }
+    for (int i = 0; i < N; i++) /* :540-553 */
+      for (int k = g->cp[i]; k < g->cp[i + 1]; k++) {
+        double T = 0.0;
+        for (int k2 = g->cp[i]; k2 < g->cp[i + 1]; k2++)
+          if (k2 != k) T += Ec[g->ce[k2]] + r[i];
+        Q[g->ce[k]] = T;
+      }
+  }
+  free(r);
+  free(Q);
+  free(Ec);
+  return used;
+}
+
+/* decodeBitFlipping (:414-476): E(i,j) for an edge is the parity of the
+ * other row members, i.e. row parity ^ ci(j) */
+static int orc_bitflip_sparse(const orc_graph *g, const double *rx, int iterations, int *vhat) {
+  const int N = g->N, M = g->M;
+  int *y = (int *)malloc(sizeof(int) * N);
+  int *rowpar = (int *)malloc(sizeof(int) * (M > 0 ? M : 1));
+  int *next = (int *)malloc(sizeof(int) * N);
+  for (int i = 0; i < N; i++) vhat[i] = y[i] = (rx[i] < 0.0) ? 0 : 1;
+  const int half = (int)((unsigned)M / 2u);
+  int used = iterations;
+  for (int it = 0; it < iterations; it++) {
+    for (int r = 0; r < M; r++) {
+      int p = 0;
+      for (int e = g->rp[r]; e < g->rp[r + 1]; e++) p += vhat[g->ci[e]];
+      rowpar[r] = p % 2;
+    }
+    for (int c = 0; c < N; c++) {
+      int votes = 0;
+      for (int k = g->cp[c]; k < g->cp[c + 1]; k++)
+        if ((rowpar[g->erow[g->ce[k]]] ^ vhat[c]) != y[c]) votes++;
+      next[c] = votes > half ? (y[c] + 1) % 2 : vhat[c];
+    }
+    for (int c = 0; c < N; c++) vhat[c] = next[c];
+    if (it + 1 < iterations && orc_check_frame_sparse(g->rp, g->ci, M, vhat, 0) == 0) {
+      used = it + 1;
+      break;
+    }
+  }
+  free(y);
+  free(rowpar);
+  free(next);
+  return used;
+}
+
+static int orc_decode_graph(int method, const orc_graph *g, const double *rx, int iterations,
+                            int *vhat, double *post_opt) {
+  if (method == 3) {
+    orc_decode_hard(rx, g->N, vhat);
+    if (post_opt)
+      for (int i = 0; i < g->N; i++) post_opt[i] = rx[i];
+    return 0;
+  }
+  if (method == 2) {
+    if (post_opt)
+      for (int i = 0; i < g->N; i++) post_opt[i] = rx[i];
+    return orc_bitflip_sparse(g, rx, iterations, vhat);
+  }
+  if (method == 1) return orc_sumproduct_sparse(g, rx, iterations, vhat, post_opt);
+  return orc_minsum_sparse(g, rx, iterations, vhat, post_opt);
+}
+
+int orc_decode_sparse(int method, const int32_t *row_ptr, const int32_t *col_idx, int M, int N,
+                      const double *rx, int iterations, int *vhat, double *post_opt) {
+  orc_graph g;
+  orc_graph_build(&g, row_ptr, col_idx, M, N);
+  const int used = orc_decode_graph(method, &g, rx, iterations, vhat, post_opt);
+  orc_graph_free(&g);
+  return used;
+}
+
+typedef struct {
+  int method, M, N, iterations, B, stride_threads, first;
+  const orc_graph *g;
+  const float *in;
+  long cw_stride;
+  int elem_stride;
+  float polarity;
+  uint8_t *bits, *packed;
+  int32_t *iters, *synd;
+} orc_sparse_job;
+
+static void *orc_sparse_worker(void *arg) {
+  orc_sparse_job *jb = (orc_sparse_job *)arg;
+  const int N = jb->N, M = jb->M, K = N - M, KB = (K + 7) / 8;
+  double *rx = (double *)malloc(sizeof(double) * N);
+  int *v = (int *)malloc(sizeof(int) * N);
+  for (int b = jb->first; b < jb->B; b += jb->stride_threads) {
+    const float *src = jb->in + (long)b * jb->cw_stride;
+    for (int i = 0; i < N; i++) rx[i] = (double)(src[(long)i * jb->elem_stride] * jb->polarity);
+    const int used = orc_decode_graph(jb->method, jb->g, rx, jb->iterations, v, NULL);
+    if (jb->iters) jb->iters[b] = used;
+    if (jb->synd) jb->synd[b] = orc_check_frame_sparse(jb->g->rp, jb->g->ci, M, v, M);
+    if (jb->bits)
+      for (int i = 0; i < N; i++) jb->bits[(long)b * N + i] = (uint8_t)v[i];
+    if (jb->packed)
+      for (int q = 0; q < KB; q++) {
+        uint8_t o = 0;
+        for (int j = 0; j < 8; j++) {
+          const int c = M + q * 8 + j;
+          if (c < N && v[c] == 1) o |= (uint8_t)(1u << (7 - j));
+        }
+        jb->packed[(long)b * KB + q] = o;
+      }
+  }
+  free(rx);
+  free(v);
+  return NULL;
+}
+
+int orc_decode_batch_sparse(int method, const int32_t *row_ptr, const int32_t *col_idx, int M,
+                            int N, int iterations, const float *in, long cw_stride,
+                            int elem_stride, float polarity, int B, uint8_t *bits_opt,
+                            uint8_t *packed_opt, int32_t *iters_opt, int32_t *synd_opt,
+                            int nthreads) {
+  orc_graph g;
+  orc_graph_build(&g, row_ptr, col_idx, M, N);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > B) nthreads = B > 0 ? B : 1;
+  orc_sparse_job *jobs = (orc_sparse_job *)malloc(sizeof(orc_sparse_job) * (size_t)nthreads);
+  pthread_t *tids = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  for (int t = 0; t < nthreads; t++) {
+    orc_sparse_job j = {method, M, N, iterations, B, nthreads, t, &g, in, cw_stride,
+                        elem_stride, polarity, bits_opt, packed_opt, iters_opt, synd_opt};
+    jobs[t] = j;
+  }
+  if (nthreads == 1) {
+    orc_sparse_worker(&jobs[0]);
+  } else {
+    for (int t = 0; t < nthreads; t++) pthread_create(&tids[t], NULL, orc_sparse_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(tids[t], NULL);
+  }
+  free(jobs);
+  free(tids);
+  orc_graph_free(&g);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ */
 /* general_work -- lib/ldpc_decoder_cb_impl.cc:133-234                  */
 /* ------------------------------------------------------------------ */
 void orc_block_init(orc_block *blk, int method, int iterations,

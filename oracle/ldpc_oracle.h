@@ -82,6 +82,22 @@ int orc_decode_batch(int method, const uint8_t *H, int M, int N, int iterations,
                      uint8_t *packed_opt, int32_t *iters_opt, int32_t *synd_opt,
                      float *post_opt, int nthreads);
 
+/* Sparse (CSR) restatements for codes too large for the reference's dense
+ * M x N arrays: the same per-edge arithmetic in the
+ * same order -- row edges in ascending column, column edges in ascending
+ * row -- on adjacency lists.  For a code small enough for both, the results
+ * equal orc_decode's bit for bit (tests/test_oracle.py).
+ * row_ptr: M+1 offsets; col_idx: E column indices, ascending within a row. */
+int orc_decode_sparse(int method, const int32_t *row_ptr, const int32_t *col_idx, int M,
+                      int N, const double *rx, int iterations, int *vhat, double *post_opt);
+int orc_check_frame_sparse(const int32_t *row_ptr, const int32_t *col_idx, int M,
+                           const int *u, int threshold);
+int orc_decode_batch_sparse(int method, const int32_t *row_ptr, const int32_t *col_idx, int M,
+                            int N, int iterations, const float *in, long cw_stride,
+                            int elem_stride, float polarity, int B, uint8_t *bits_opt,
+                            uint8_t *packed_opt, int32_t *iters_opt, int32_t *synd_opt,
+                            int nthreads);
+
 /* general_work restatement, lib/ldpc_decoder_cb_impl.cc:133-234 + forecast
  * :126-130.  `in` is interleaved gr_complex (re, im).  State lives in the
  * struct (d_state, d_errors); the block's constants are d_M, d_N from H. */

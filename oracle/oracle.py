@@ -43,6 +43,11 @@ def lib():
                                        _f32p, ctypes.c_long, ctypes.c_int, ctypes.c_float,
                                        ctypes.c_int, _u8p, _u8p, _i32p, _i32p, _f32p, ctypes.c_int]
         L.orc_decode_batch.restype = ctypes.c_int
+        L.orc_decode_batch_sparse.argtypes = [ctypes.c_int, _i32p, _i32p, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, _f32p, ctypes.c_long,
+                                              ctypes.c_int, ctypes.c_float, ctypes.c_int, _u8p,
+                                              _u8p, _i32p, _i32p, ctypes.c_int]
+        L.orc_decode_batch_sparse.restype = ctypes.c_int
         L.orc_block_init.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _u8p,
                                      ctypes.c_int, ctypes.c_int]
         L.orc_block_init.restype = None
@@ -133,6 +138,40 @@ def decode_batch(method, Hr, llr, iterations, polarity=1.0, nthreads=1, cw_strid
     if want_post:
         out["post"] = post
     return out
+
+
+def decode_batch_sparse(method, row_ptr, col_idx, M, N, llr, iterations, polarity=1.0,
+                        nthreads=1, cw_stride=None, elem_stride=1, B=None, want_bits=True):
+    """Sparse (CSR) restatement for large codes; same outputs as decode_batch."""
+    rp = np.ascontiguousarray(row_ptr, np.int32)
+    ci = np.ascontiguousarray(col_idx, np.int32)
+    llr = np.ascontiguousarray(llr, np.float32)
+    if cw_stride is None:
+        cw_stride = N * elem_stride
+    if B is None:
+        B = llr.size // cw_stride if llr.ndim == 1 else llr.shape[0]
+    KB = (N - M + 7) // 8
+    bits = np.zeros((B, N), np.uint8) if want_bits else None
+    packed = np.zeros((B, KB), np.uint8)
+    iters = np.zeros(B, np.int32)
+    synd = np.zeros(B, np.int32)
+    lib().orc_decode_batch_sparse(int(method), _p(rp, _i32p), _p(ci, _i32p), int(M), int(N),
+                                  int(iterations), _p(llr, _f32p), int(cw_stride),
+                                  int(elem_stride), float(polarity), int(B), _p(bits, _u8p),
+                                  _p(packed, _u8p), _p(iters, _i32p), _p(synd, _i32p),
+                                  int(nthreads))
+    out = dict(packed=packed, iters=iters, synd=synd)
+    if want_bits:
+        out["bits"] = bits
+    return out
+
+
+def dense_to_csr(H):
+    H = np.asarray(H, np.uint8)
+    rows, cols = np.nonzero(H)
+    row_ptr = np.zeros(H.shape[0] + 1, np.int32)
+    np.add.at(row_ptr, rows + 1, 1)
+    return np.cumsum(row_ptr).astype(np.int32), cols.astype(np.int32)
 
 
 class _OrcBlock(ctypes.Structure):

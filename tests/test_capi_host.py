@@ -94,3 +94,31 @@ def test_no_cpu_fallback_without_gpu():
         L.Decoder()
     with pytest.raises(L.LdpcError):
         L.ldpc_decoder_cb(1)
+
+
+def test_create_csr_validates_and_has_no_cpu_fallback():
+    import torch
+    rp = np.array([0, 2, 4], np.int32)
+    bad = [  # (M, N, row_ptr, col_idx)
+        (2, 4, rp, np.array([1, 0, 2, 3], np.int32)),   # not ascending
+        (2, 4, rp, np.array([0, 1, 2, 4], np.int32)),   # out of range
+        (2, 4, np.array([0, 3, 2], np.int32), np.array([0, 1, 2, 3], np.int32)),
+        (4, 4, np.array([0, 1, 2, 3, 4], np.int32), np.arange(4, dtype=np.int32)),  # M >= N
+    ]
+    for csr in bad:
+        with pytest.raises(L.LdpcError, match="CSR H must be"):
+            L.Decoder(csr=csr)
+    if not torch.cuda.is_available():
+        with pytest.raises(L.LdpcError, match="no CPU fallback"):
+            L.Decoder(csr=(2, 4, rp, np.array([0, 1, 2, 3], np.int32)))
+        from ldpc_ece535a import codes
+        with pytest.raises(L.LdpcError, match="no CPU fallback"):
+            L.Decoder(csr=codes.dvbs2_like(0))
+
+
+def test_degree_limits_reported_before_device_lookup():
+    H = np.zeros((300, 600), np.uint8)
+    H[np.arange(300), np.arange(300)] = 1
+    H[:, 300] = 1  # column degree 300 > the large-code kernels' 16
+    with pytest.raises(L.LdpcError, match="outside the large-code kernels"):
+        L.Decoder(H)

@@ -150,5 +150,5 @@ def test_unsupported_code_shape():
     H = np.zeros((300, 600), np.uint8)
     H[np.arange(300), np.arange(300)] = 1
     H[:, 300] = 1  # column degree 300
-    with pytest.raises(L.LdpcError, match="outside the small-code kernel"):
+    with pytest.raises(L.LdpcError, match="outside the large-code kernels"):
         L.Decoder(H)
