@@ -75,6 +75,33 @@ __device__ __forceinline__ int field(const uint32_t (&p)[W], int k) {
   return (int)((p[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
 }
 
+// LDS access by absolute byte address (the relocated tables hold addresses,
+// so a gather is one field extract + one ds_read).
+template <typename T>
+__device__ __forceinline__ T lds_ld(uint32_t addr) {
+  typedef const __attribute__((address_space(3))) T *lds_ptr;
+  return *(lds_ptr)(uintptr_t)addr;
+}
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr(const T *p) {
+  typedef const __attribute__((address_space(3))) T *lds_ptr;
+  return (uint32_t)(uintptr_t)(lds_ptr)p;  // generic -> LDS address-space cast
+}
+
+// Rewrites the 16-bit edge/column ids of a packed record (fields 0..nf-1)
+// as LDS byte addresses base + id * size; kNone becomes the dummy element.
+template <int W>
+__device__ __forceinline__ void relocate(uint32_t (&p)[W], int nf, uint32_t base, uint32_t size,
+                                         uint32_t dummy) {
+#pragma unroll
+  for (int k = 0; k < 2 * W; ++k) {
+    if (k >= nf) break;
+    const uint32_t id = (p[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
+    const uint32_t ad = id == kNone ? base + dummy * size : base + id * size;
+    p[k >> 1] = (p[k >> 1] & ~(0xffffu << ((k & 1) * 16))) | (ad << ((k & 1) * 16));
+  }
+}
+
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 // Per-wave LDS slice (the workgroup's waves never share LDS):
@@ -138,19 +165,26 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
   };
 
   if constexpr (METHOD == 1 || METHOD == 0) {
-    if (lane == 0) tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
-    int col[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      col[s] = field(wt.rn[s], 7);
-      col[s] = col[s] != kNone ? col[s] : 0;  // padding edges: any column
+    // the tables were relocated to LDS byte addresses (decode_small_kernel):
+    // rn -> tb, cn / ce -> eb, rn field 7 -> rb (sb = rb + 64 NW elements);
+    // missing neighbours point at the dummy elements tb[64S] (1.0 for the
+    // tanh product, DBL_MAX for the minimum) and eb[64S] (0.0: an exact no-op
+    // for the min-sum column sum, whose running value is never -0.0).
+    const uint32_t eb_dummy = lds_addr(eb + kDummy);
+    if (lane == 0) {
+      tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
+      eb[kDummy] = Real(0);
     }
-    wave_lds_sync();  // rb and the dummy visible to every lane
+    uint32_t col[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) col[s] = (uint32_t)field(wt.rn[s], 7);
+    constexpr uint32_t kSb = 64 * NW * sizeof(Real);  // sb - rb in bytes
+    wave_lds_sync();  // rb and the dummies visible to every lane
     Real msg[S];      // SP: M(j,i) (:489-496); min-sum: L(q_ij) (:328-331)
     Real lr[S];       // min-sum: L(r_ji)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      msg[s] = rb[col[s]];
+      msg[s] = lds_ld<Real>(col[s]);
       lr[s] = Real(0);
     }
 
@@ -176,10 +210,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
-        for (int k = 0; k < kDcMax - 1; ++k) {
-          const int n = field(wt.rn[s], k);
-          nb[s][k] = tb[n == kNone ? kDummy : n];
-        }
+        for (int k = 0; k < kDcMax - 1; ++k) nb[s][k] = lds_ld<Real>((uint32_t)field(wt.rn[s], k));
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         if constexpr (METHOD == 1) {
@@ -214,12 +245,9 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       if constexpr (METHOD == 1) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          rcs[s] = rb[col[s]];
+          rcs[s] = lds_ld<Real>(col[s]);
 #pragma unroll
-          for (int k = 0; k < kDvMax - 1; ++k) {
-            const int n = field(wt.cn[s], k);
-            cv[s][k] = eb[n == kNone ? kDummy : n];
-          }
+          for (int k = 0; k < kDvMax - 1; ++k) cv[s][k] = lds_ld<Real>((uint32_t)field(wt.cn[s], k));
         }
       }
       // ---- per-column totals and the hard decision ----------------------
@@ -228,10 +256,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         const int c = lane + 64 * q;
         Real ev[kDvMax];
 #pragma unroll
-        for (int k = 0; k < kDvMax; ++k) {
-          const int n = field(wt.ce[q], k);
-          ev[k] = eb[n == kNone ? kDummy : n];
-        }
+        for (int k = 0; k < kDvMax; ++k) ev[k] = lds_ld<Real>((uint32_t)field(wt.ce[q], k));
         const Real rc = rb[c];
         Real acc = Real(0);
         bool bit;
@@ -239,14 +264,13 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           // L = sum_j (E(j,i) + r(i)), ascending j; 1 iff L <= 0 (:519-532)
 #pragma unroll
           for (int k = 0; k < kDvMax; ++k)
-            acc = field(wt.ce[q], k) != kNone ? acc + (ev[k] + rc) : acc;
+            acc = (uint32_t)field(wt.ce[q], k) != eb_dummy ? acc + (ev[k] + rc) : acc;
           bit = acc <= Real(0);
           post[q] = acc;
         } else {
           // s = sum_i L(r_ji) (:380-385); L(Q) = Lci + s; 1 iff L(Q) < 0 (:395-402)
 #pragma unroll
-          for (int k = 0; k < kDvMax; ++k)
-            acc = field(wt.ce[q], k) != kNone ? acc + ev[k] : acc;
+          for (int k = 0; k < kDvMax; ++k) acc = acc + ev[k];
           const Real LQ = rc + acc;
           sb[c] = LQ;
           bit = LQ < Real(0);
@@ -268,14 +292,14 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           Real acc = Real(0);
 #pragma unroll
           for (int k = 0; k < kDvMax - 1; ++k)
-            acc = field(wt.cn[s], k) != kNone ? acc + (cv[s][k] + rcs[s]) : acc;
+            acc = (uint32_t)field(wt.cn[s], k) != eb_dummy ? acc + (cv[s][k] + rcs[s]) : acc;
           msg[s] = acc;
         }
       } else {
         wave_lds_sync();  // sb visible
         // L(q_ij) = Lci(j) + s_j - L(r_ji)  (:387-392)
 #pragma unroll
-        for (int s = 0; s < S; ++s) msg[s] = sb[col[s]] - lr[s];
+        for (int s = 0; s < S; ++s) msg[s] = lds_ld<Real>(col[s] + kSb) - lr[s];
       }
     }
   } else {
@@ -403,6 +427,20 @@ __global__ void __launch_bounds__(kThreads)
   Real *eb = tb + (64 * S + 2);
   Real *rb = eb + (64 * S + 2);
   Real *sb = rb + 64 * NW;
+  if constexpr (METHOD <= 1) {
+    // ids -> LDS byte addresses of this wave's slice (see decode_frame)
+    constexpr uint32_t R = sizeof(Real), kDummy = 64 * S;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const uint32_t cid = (uint32_t)field(wt.rn[s], 7);
+      relocate(wt.rn[s], kDcMax - 1, lds_addr(tb), R, kDummy);
+      const uint32_t ca = lds_addr(rb) + (cid == kNone ? 0u : cid) * R;
+      wt.rn[s][3] = (wt.rn[s][3] & 0xffffu) | (ca << 16);
+      relocate(wt.cn[s], kDvMax - 1, lds_addr(eb), R, kDummy);
+    }
+#pragma unroll
+    for (int q = 0; q < NW; ++q) relocate(wt.ce[q], kDvMax, lds_addr(eb), R, kDummy);
+  }
 
   while (b < a.B) {
     decode_frame<PREC, METHOD, S, NW>(code, a, b, wt, tb, eb, rb, sb, lane);
