@@ -13,29 +13,35 @@
 namespace ldpc {
 
 // Arithmetic per precision mode (include/ldpc_hip.h LDPC_PREC_*):
-//   0 F64       double, compact tanh/log of ldpc_math.hpp (<= 3 ulp of glibc)
+//   0 F64       double, compact tanh/log of ldpc_math.hpp (<= 3 ulp of glibc,
+//               reciprocal-based divisions)
 //   1 F32       float, ROCm libm
 //   2 F64_LIBM  double, fdlibm tanh bit-identical to glibc's, fdlibm log
 template <int PREC>
 struct Math;
+// tanh_half(m) = tanh(m / 2) (:509); check_msg(T) = log((1+T)/(1-T)) (:513).
 template <>
 struct Math<0> {
   typedef double Real;
-  static __device__ __forceinline__ double tanh_(double x) { return fm::tanh_fast_f64(x); }
-  static __device__ __forceinline__ double log_(double x) { return fm::log_fast_f64(x); }
+  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_fast(m); }
+  static __device__ __forceinline__ double check_msg(double T) { return fm::log_ratio_fast(T); }
   static __device__ __forceinline__ double abs_(double x) { return ::fabs(x); }
   static __device__ __forceinline__ double max_() { return DBL_MAX; }
 };
 template <>
 struct Math<2> : Math<0> {
-  static __device__ __forceinline__ double tanh_(double x) { return fm::tanh_f64_bf(x); }
-  static __device__ __forceinline__ double log_(double x) { return fm::log_f64_bf(x); }
+  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_f64_bf(m / 2.0); }
+  static __device__ __forceinline__ double check_msg(double T) {
+    return fm::log_f64_bf((1.0 + T) / (1.0 - T));  // IEEE division
+  }
 };
 template <>
 struct Math<1> {
   typedef float Real;
-  static __device__ __forceinline__ float tanh_(float x) { return ::tanhf(x); }
-  static __device__ __forceinline__ float log_(float x) { return ::logf(x); }
+  static __device__ __forceinline__ float tanh_half(float m) { return ::tanhf(m / 2.0f); }
+  static __device__ __forceinline__ float check_msg(float T) {
+    return ::logf((1.0f + T) / (1.0f - T));
+  }
   static __device__ __forceinline__ float abs_(float x) { return ::fabsf(x); }
   static __device__ __forceinline__ float max_() { return FLT_MAX; }
 };

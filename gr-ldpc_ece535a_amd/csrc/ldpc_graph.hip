@@ -149,12 +149,12 @@ __global__ void __launch_bounds__(256) g_check(GraphView g, GraphWork w, int h) 
       // ascending k (:503-516)
 #pragma unroll
       for (int t = 0; t < DC; ++t)
-        if (t < d) q[t] = Math<PREC>::tanh_(q[t] / Real(2));
+        if (t < d) q[t] = Math<PREC>::tanh_half(q[t]);
       for (int e = 0; e < d; ++e) {
         Real T = Real(1);
 #pragma unroll
         for (int t = 0; t < DC; ++t) T = (t != e && t < d) ? T * q[t] : T;
-        R[(int64_t)(e0 + e) * 64] = Math<PREC>::log_((Real(1) + T) / (Real(1) - T));
+        R[(int64_t)(e0 + e) * 64] = Math<PREC>::check_msg(T);
       }
     } else {
       // L(r_ji) = (prod_k sign(L(q_jk))) * sign(L(q_ji)) * min_{k != i} |L(q_jk)|

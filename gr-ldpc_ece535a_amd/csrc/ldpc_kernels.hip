@@ -200,7 +200,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         if constexpr (METHOD == 1)
-          tb[lane + 64 * s] = Math<PREC>::tanh_(msg[s] / Real(2));  // :509
+          tb[lane + 64 * s] = Math<PREC>::tanh_half(msg[s]);  // :509
         else
           tb[lane + 64 * s] = msg[s];
       }
@@ -219,7 +219,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           Real T = Real(1);
 #pragma unroll
           for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[s][k];
-          eb[lane + 64 * s] = Math<PREC>::log_((Real(1) + T) / (Real(1) - T));
+          eb[lane + 64 * s] = Math<PREC>::check_msg(T);
         } else {
           // min-sum horizontal step (:350-376): sign product over the row
           // times the minimum |L(q)| of the other edges.  Padding neighbours
@@ -534,7 +534,7 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
       opaque(rn);
       opaque(cn);
       if constexpr (METHOD == 1)
-        tb[tid] = Math<PREC>::tanh_(msg / Real(2));  // :509
+        tb[tid] = Math<PREC>::tanh_half(msg);  // :509
       else
         tb[tid] = msg;
       __syncthreads();
@@ -548,7 +548,7 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
         Real T = Real(1);  // ascending column; dummies are exact 1.0 (:506-511)
 #pragma unroll
         for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[k];
-        eb[tid] = Math<PREC>::log_((Real(1) + T) / (Real(1) - T));  // :513
+        eb[tid] = Math<PREC>::check_msg(T);  // :513
       } else {
         const int self = sgn(msg);  // :350-376
         int prod = self;

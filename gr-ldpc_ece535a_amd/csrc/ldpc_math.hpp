@@ -451,5 +451,55 @@ LDPC_HD double log_fast_f64(double q) {
   return (q == __builtin_inf() || q != q) ? q + q : r;
 }
 
+// tanh(m / 2), the sum-product check pass's operand (:509), in the compact
+// two-range form of tanh_fast_f64 evaluated on |m| = 2|x| directly: the same
+// z = min(|m|, 44) / -|m| and therefore the same value as tanh_fast_f64(m/2)
+// for every normal m, without the halving and doubling.  Saturation needs no
+// select (for |m| >= 44, 1 - 2/(expm1(44)+2) rounds to 1.0), NaN propagates,
+// and the sign is copied (tanh(-0) = -0 as in glibc).
+LDPC_HD double tanh_half_fast(double m) {
+  const double a2 = __builtin_fabs(m);
+  const bool big = a2 >= 2.0;
+  const double z = big ? (a2 < 44.0 ? a2 : 44.0) : -a2;
+  const double t = expm1_mid_f64(z);
+  const double q = div_fast(big ? 2.0 : -t, t + 2.0);
+  const double r = big ? 1.0 - q : q;
+  return __builtin_copysign(r, m);
+}
+
+// log((1+T)/(1-T)), the sum-product check message (:513), for T in [-1, 1]
+// (a product of tanh values) or NaN.  The ratio q is then 0 only for T = -1,
+// +inf only for T = 1 and never subnormal or negative, so log_fast_f64's
+// special cases reduce to |T| == 1 -> +-inf; NaN propagates through the
+// polynomial.  The division is the reciprocal-based div_fast.
+LDPC_HD double log_ratio_fast(double T) {
+  const double ln2_hi = 6.93147180369123816490e-01;
+  const double ln2_lo = 1.90821492927058770002e-10;
+  const double Lg1 = 6.666666666666735130e-01;
+  const double Lg2 = 3.999999999940941908e-01;
+  const double Lg3 = 2.857142874366239149e-01;
+  const double Lg4 = 2.222219843214978396e-01;
+  const double Lg5 = 1.818357216161805012e-01;
+  const double Lg6 = 1.531383769920937332e-01;
+  const double Lg7 = 1.479819860511658591e-01;
+  const double q = div_fast(1.0 + T, 1.0 - T);
+  int k;
+  double m = frexp_(q, &k);  // m in [0.5, 1)
+  const bool lo = m < 0.70710678118654752440;
+  m = lo ? m + m : m;
+  k = lo ? k - 1 : k;
+  const double f = m - 1.0;  // exact
+  const double s = div_fast(f, 2.0 + f);
+  const double z = s * s;
+  const double w = z * z;
+  const double t1 = w * fma_(w, fma_(w, Lg6, Lg4), Lg2);
+  const double t2 = z * fma_(w, fma_(w, fma_(w, Lg7, Lg5), Lg3), Lg1);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  const double r = dk * ln2_hi - ((hfsq - fma_(s, hfsq + R, dk * ln2_lo)) - f);
+  return __builtin_fabs(T) == 1.0 ? __builtin_copysign(__builtin_inf(), T) : r;
+}
+
 }  // namespace fm
 }  // namespace ldpc

@@ -70,3 +70,22 @@ void check_fast(int fn, const double *x, int64_t n, int64_t *out) {
   out[0] = mism; out[1] = maxu;
 }
 }
+extern "C" {
+// the check-pass forms vs glibc: fn 0 tanh_half_fast(m) vs tanh(m/2),
+// fn 1 log_ratio_fast(T) vs log((1+T)/(1-T)), fn 2 tanh_half_fast(m) vs
+// tanh_fast_f64(m/2) (must be identical for normal m).
+// out[0] = mismatches, out[1] = max ulp
+void check_pass(int fn, const double *x, int64_t n, int64_t *out) {
+  int64_t mism = 0, maxu = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double a, b;
+    if (fn == 0) { a = ldpc::fm::tanh_half_fast(x[i]); b = tanh(x[i] / 2.0); }
+    else if (fn == 1) { a = ldpc::fm::log_ratio_fast(x[i]); b = log((1.0 + x[i]) / (1.0 - x[i])); }
+    else { a = ldpc::fm::tanh_half_fast(x[i]); b = ldpc::fm::tanh_fast_f64(x[i] / 2.0); }
+    int64_t u = ulps(a, b);
+    if (u) ++mism;
+    if (u > maxu) maxu = u;
+  }
+  out[0] = mism; out[1] = maxu;
+}
+}

@@ -71,3 +71,37 @@ def test_log_within_one_ulp(mc):
               1 + rng.uniform(-1e-3, 1e-3, 400_000)):
         _, maxulp = _run(mc, "check_fn", 2, x)
         assert maxulp <= 1
+
+
+def test_compact_tanh_within_3ulp(mc):
+    """LDPC_PREC_F64 (compact) tanh: within 3 ulp of glibc."""
+    for i, x in enumerate(_inputs(11)):
+        _, maxulp = _run(mc, "check_fast", 0, x)
+        assert maxulp <= 3, (i, maxulp)
+
+
+def test_compact_log_within_3ulp(mc):
+    rng = np.random.default_rng(12)
+    for x in (np.exp(rng.uniform(-40, 40, 400_000)), rng.uniform(0, 3, 400_000),
+              1 + rng.uniform(-1e-3, 1e-3, 400_000)):
+        _, maxulp = _run(mc, "check_fast", 2, x)
+        assert maxulp <= 3
+
+
+def test_check_pass_forms(mc):
+    """tanh_half_fast(m) == tanh_fast_f64(m/2) for normal m and within 3 ulp
+    of glibc tanh(m/2); log_ratio_fast(T) within 3 ulp of glibc
+    log((1+T)/(1-T)) over T in [-1, 1] incl. the +-1 / +-0 / NaN edges."""
+    for x in _inputs(13):
+        normal = x[np.isfinite(x) & (np.abs(x) > 1e-300)]
+        mism, _ = _run(mc, "check_pass", 2, normal)
+        assert mism == 0
+        _, maxulp = _run(mc, "check_pass", 0, x)
+        assert maxulp <= 3
+    rng = np.random.default_rng(14)
+    Ts = [rng.uniform(-1, 1, 400_000), np.tanh(rng.normal(0, 10, 400_000)),
+          1 - 10.0 ** rng.uniform(-16, 0, 200_000), -1 + 10.0 ** rng.uniform(-16, 0, 200_000),
+          np.array([1.0, -1.0, 0.0, -0.0, np.nan, 0.5, -0.5, 1 - 2.0 ** -53, -1 + 2.0 ** -53])]
+    for T in Ts:
+        _, maxulp = _run(mc, "check_pass", 1, T)
+        assert maxulp <= 3
