@@ -316,6 +316,8 @@ ldpc::CodeView code_view(const ldpc_ctx *ctx) {
   v.E = ctx->E;
   v.KB = ctx->KB;
   v.rs = ctx->rs;
+  v.dc_max = ctx->dc_max;
+  v.dv_max = ctx->dv_max;
   return v;
 }
 

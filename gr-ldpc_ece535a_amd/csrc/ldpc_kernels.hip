@@ -127,7 +127,11 @@ struct WaveTables {
   uint64_t rowmask[NW][NW];  // rows lane + 64 q, words k (M < N <= 64 NW)
 };
 
-template <int PREC, int METHOD, int S, int NW, typename Real = typename Math<PREC>::Real>
+// DCN / DVN: row neighbours / column entries the loops visit (compile-time
+// degree bounds: DCN >= dc_max - 1, DVN >= dv_max); fewer than the record
+// sizes for codes of low degree, e.g. the reference's H (dc <= 6, dv <= 3).
+template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax,
+          typename Real = typename Math<PREC>::Real>
 __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeArgs &a,
                                              const int64_t b, WaveTables<S, NW> &wt,
                                              Real *tb, Real *eb, Real *rb, Real *sb,
@@ -206,11 +210,11 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       }
       wave_lds_sync();
       // gather the row neighbours of every slot (unconditional loads)
-      Real nb[S][kDcMax - 1];
+      Real nb[S][DCN];
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
-        for (int k = 0; k < kDcMax - 1; ++k) nb[s][k] = lds_ld<Real>((uint32_t)field(wt.rn[s], k));
+        for (int k = 0; k < DCN; ++k) nb[s][k] = lds_ld<Real>((uint32_t)field(wt.rn[s], k));
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         if constexpr (METHOD == 1) {
@@ -218,7 +222,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           // (:506-513).  Padding neighbours read the 1.0 dummy: exact no-op.
           Real T = Real(1);
 #pragma unroll
-          for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[s][k];
+          for (int k = 0; k < DCN; ++k) T = T * nb[s][k];
           eb[lane + 64 * s] = Math<PREC>::check_msg(T);
         } else {
           // min-sum horizontal step (:350-376): sign product over the row
@@ -228,7 +232,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           int prod = self;
           Real lo = Math<PREC>::max_();
 #pragma unroll
-          for (int k = 0; k < kDcMax - 1; ++k) {
+          for (int k = 0; k < DCN; ++k) {
             prod *= sgn(nb[s][k]);
             const Real beta = Math<PREC>::abs_(nb[s][k]);
             lo = beta < lo ? beta : lo;
@@ -240,37 +244,37 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       wave_lds_sync();
       // the variable pass's gathers go out with the column gathers (one
       // wait); they are simply unused when the frame stops here
-      Real cv[S][kDvMax - 1];
+      Real cv[S][DVN - 1];
       Real rcs[S];
       if constexpr (METHOD == 1) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
           rcs[s] = lds_ld<Real>(col[s]);
 #pragma unroll
-          for (int k = 0; k < kDvMax - 1; ++k) cv[s][k] = lds_ld<Real>((uint32_t)field(wt.cn[s], k));
+          for (int k = 0; k < DVN - 1; ++k) cv[s][k] = lds_ld<Real>((uint32_t)field(wt.cn[s], k));
         }
       }
       // ---- per-column totals and the hard decision ----------------------
 #pragma unroll
       for (int q = 0; q < NW; ++q) {
         const int c = lane + 64 * q;
-        Real ev[kDvMax];
+        Real ev[DVN];
 #pragma unroll
-        for (int k = 0; k < kDvMax; ++k) ev[k] = lds_ld<Real>((uint32_t)field(wt.ce[q], k));
+        for (int k = 0; k < DVN; ++k) ev[k] = lds_ld<Real>((uint32_t)field(wt.ce[q], k));
         const Real rc = rb[c];
         Real acc = Real(0);
         bool bit;
         if constexpr (METHOD == 1) {
           // L = sum_j (E(j,i) + r(i)), ascending j; 1 iff L <= 0 (:519-532)
 #pragma unroll
-          for (int k = 0; k < kDvMax; ++k)
+          for (int k = 0; k < DVN; ++k)
             acc = (uint32_t)field(wt.ce[q], k) != eb_dummy ? acc + (ev[k] + rc) : acc;
           bit = acc <= Real(0);
           post[q] = acc;
         } else {
           // s = sum_i L(r_ji) (:380-385); L(Q) = Lci + s; 1 iff L(Q) < 0 (:395-402)
 #pragma unroll
-          for (int k = 0; k < kDvMax; ++k) acc = acc + ev[k];
+          for (int k = 0; k < DVN; ++k) acc = acc + ev[k];
           const Real LQ = rc + acc;
           sb[c] = LQ;
           bit = LQ < Real(0);
@@ -291,7 +295,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         for (int s = 0; s < S; ++s) {
           Real acc = Real(0);
 #pragma unroll
-          for (int k = 0; k < kDvMax - 1; ++k)
+          for (int k = 0; k < DVN - 1; ++k)
             acc = (uint32_t)field(wt.cn[s], k) != eb_dummy ? acc + (cv[s][k] + rcs[s]) : acc;
           msg[s] = acc;
         }
@@ -382,7 +386,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 // a.waves + ticket++ until the batch is exhausted.  Frames stop after 1..cap
 // iterations, so pulling work keeps every SIMD busy to the end instead of
 // leaving it with a fixed share of the batch.
-template <int PREC, int METHOD, int S, int NW>
+template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax>
 __global__ void __launch_bounds__(kThreads)
     decode_small_kernel(CodeView code, DecodeArgs a) {
   typedef typename Math<PREC>::Real Real;
@@ -433,17 +437,17 @@ __global__ void __launch_bounds__(kThreads)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const uint32_t cid = (uint32_t)field(wt.rn[s], 7);
-      relocate(wt.rn[s], kDcMax - 1, lds_addr(tb), R, kDummy);
+      relocate(wt.rn[s], DCN, lds_addr(tb), R, kDummy);
       const uint32_t ca = lds_addr(rb) + (cid == kNone ? 0u : cid) * R;
       wt.rn[s][3] = (wt.rn[s][3] & 0xffffu) | (ca << 16);
-      relocate(wt.cn[s], kDvMax - 1, lds_addr(eb), R, kDummy);
+      relocate(wt.cn[s], DVN - 1, lds_addr(eb), R, kDummy);
     }
 #pragma unroll
-    for (int q = 0; q < NW; ++q) relocate(wt.ce[q], kDvMax, lds_addr(eb), R, kDummy);
+    for (int q = 0; q < NW; ++q) relocate(wt.ce[q], DVN, lds_addr(eb), R, kDummy);
   }
 
   while (b < a.B) {
-    decode_frame<PREC, METHOD, S, NW>(code, a, b, wt, tb, eb, rb, sb, lane);
+    decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane);
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(a.ticket, 1u);
     b = (int64_t)a.waves + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
@@ -657,17 +661,17 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
 // ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
-template <int PREC, int METHOD, int S, int NW>
+template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax>
 static int launch_one(const CodeView &code, const DecodeArgs &a, hipStream_t st) {
   typedef typename Math<PREC>::Real Real;
   const size_t lds = Layout<Real, S, NW>().total;
   if (lds > 65536 &&
-      hipFuncSetAttribute((const void *)decode_small_kernel<PREC, METHOD, S, NW>,
+      hipFuncSetAttribute((const void *)decode_small_kernel<PREC, METHOD, S, NW, DCN, DVN>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -3;
   const dim3 grid((unsigned)((a.waves + kWavesPerBlock - 1) / kWavesPerBlock));
-  hipLaunchKernelGGL((decode_small_kernel<PREC, METHOD, S, NW>), grid, dim3(kThreads), lds, st,
-                     code, a);
+  hipLaunchKernelGGL((decode_small_kernel<PREC, METHOD, S, NW, DCN, DVN>), grid, dim3(kThreads),
+                     lds, st, code, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -701,6 +705,19 @@ static int launch_mw_slots(const CodeView &code, const DecodeArgs &a, int slots,
 
 template <int PREC, int METHOD, int NW>
 static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots, hipStream_t st) {
+  // low-degree codes (dc <= 6, dv <= 3: the reference's H) with one column
+  // slot get loops sized to their degrees
+  if constexpr (NW == 1 && METHOD <= 1) {
+    if (code.dc_max <= 6 && code.dv_max <= 3) {
+      switch (slots) {
+        case 1: return launch_one<PREC, METHOD, 1, NW, 5, 3>(code, a, st);
+        case 2: return launch_one<PREC, METHOD, 2, NW, 5, 3>(code, a, st);
+        case 3: return launch_one<PREC, METHOD, 3, NW, 5, 3>(code, a, st);
+        case 4: return launch_one<PREC, METHOD, 4, NW, 5, 3>(code, a, st);
+        default: break;
+      }
+    }
+  }
   switch (slots) {
     case 1: return launch_one<PREC, METHOD, 1, NW>(code, a, st);
     case 2: return launch_one<PREC, METHOD, 2, NW>(code, a, st);

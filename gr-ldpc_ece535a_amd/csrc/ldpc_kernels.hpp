@@ -48,6 +48,7 @@ struct CodeView {
   const ColRec *cols;        // 64 * NW records; records >= N are all kNone
   const uint64_t *rowmask;   // M x NW words: bit c of row j <=> H(j, c) == 1
   int M, N, E, KB, rs;       // rs = ceil(M / 64)
+  int dc_max, dv_max;        // largest check / variable degree
 };
 
 struct DecodeArgs {
