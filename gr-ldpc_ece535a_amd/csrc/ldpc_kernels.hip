@@ -179,9 +179,21 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
       eb[kDummy] = Real(0);
     }
-    uint32_t col[S];
+    // unpacked once per frame into full registers: a gather is then one
+    // ds_read with no address arithmetic in the iteration loop
+    uint32_t col[S], ra[S][DCN], ca[S][DVN - 1], ea[NW][DVN];
 #pragma unroll
-    for (int s = 0; s < S; ++s) col[s] = (uint32_t)field(wt.rn[s], 7);
+    for (int s = 0; s < S; ++s) {
+      col[s] = (uint32_t)field(wt.rn[s], 7);
+#pragma unroll
+      for (int k = 0; k < DCN; ++k) ra[s][k] = (uint32_t)field(wt.rn[s], k);
+#pragma unroll
+      for (int k = 0; k < DVN - 1; ++k) ca[s][k] = (uint32_t)field(wt.cn[s], k);
+    }
+#pragma unroll
+    for (int q = 0; q < NW; ++q)
+#pragma unroll
+      for (int k = 0; k < DVN; ++k) ea[q][k] = (uint32_t)field(wt.ce[q], k);
     constexpr uint32_t kSb = 64 * NW * sizeof(Real);  // sb - rb in bytes
     wave_lds_sync();  // rb and the dummies visible to every lane
     Real msg[S];      // SP: M(j,i) (:489-496); min-sum: L(q_ij) (:328-331)
@@ -193,13 +205,6 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
     }
 
     for (int h = 0; h < a.max_iters; ++h) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        opaque(wt.rn[s]);
-        opaque(wt.cn[s]);
-      }
-#pragma unroll
-      for (int q = 0; q < NW; ++q) opaque(wt.ce[q]);
       // ---- check-pass operand of every edge -> LDS ----------------------
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -214,7 +219,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
-        for (int k = 0; k < DCN; ++k) nb[s][k] = lds_ld<Real>((uint32_t)field(wt.rn[s], k));
+        for (int k = 0; k < DCN; ++k) nb[s][k] = lds_ld<Real>(ra[s][k]);
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         if constexpr (METHOD == 1) {
@@ -251,7 +256,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         for (int s = 0; s < S; ++s) {
           rcs[s] = lds_ld<Real>(col[s]);
 #pragma unroll
-          for (int k = 0; k < DVN - 1; ++k) cv[s][k] = lds_ld<Real>((uint32_t)field(wt.cn[s], k));
+          for (int k = 0; k < DVN - 1; ++k) cv[s][k] = lds_ld<Real>(ca[s][k]);
         }
       }
       // ---- per-column totals and the hard decision ----------------------
@@ -260,7 +265,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         const int c = lane + 64 * q;
         Real ev[DVN];
 #pragma unroll
-        for (int k = 0; k < DVN; ++k) ev[k] = lds_ld<Real>((uint32_t)field(wt.ce[q], k));
+        for (int k = 0; k < DVN; ++k) ev[k] = lds_ld<Real>(ea[q][k]);
         const Real rc = rb[c];
         Real acc = Real(0);
         bool bit;
@@ -268,7 +273,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           // L = sum_j (E(j,i) + r(i)), ascending j; 1 iff L <= 0 (:519-532)
 #pragma unroll
           for (int k = 0; k < DVN; ++k)
-            acc = (uint32_t)field(wt.ce[q], k) != eb_dummy ? acc + (ev[k] + rc) : acc;
+            acc = ea[q][k] != eb_dummy ? acc + (ev[k] + rc) : acc;
           bit = acc <= Real(0);
           post[q] = acc;
         } else {
@@ -296,7 +301,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           Real acc = Real(0);
 #pragma unroll
           for (int k = 0; k < DVN - 1; ++k)
-            acc = (uint32_t)field(wt.cn[s], k) != eb_dummy ? acc + (cv[s][k] + rcs[s]) : acc;
+            acc = ca[s][k] != eb_dummy ? acc + (cv[s][k] + rcs[s]) : acc;
           msg[s] = acc;
         }
       } else {
