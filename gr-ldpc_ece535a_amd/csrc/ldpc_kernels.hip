@@ -220,6 +220,11 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       for (int s = 0; s < S; ++s)
 #pragma unroll
         for (int k = 0; k < DCN; ++k) nb[s][k] = lds_ld<Real>(ra[s][k]);
+      // all of them in flight before the first use (one LDS wait, not three)
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int k = 0; k < DCN; ++k) asm volatile("" ::"v"(nb[s][k]));
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         if constexpr (METHOD == 1) {
@@ -286,6 +291,16 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           post[q] = LQ;
         }
         hard[q] = __ballot(bit && c < N);
+      }
+      if constexpr (METHOD == 1) {
+        // keep the variable pass's gathers above the exit test (the compiler
+        // would otherwise sink them below it: one more LDS round trip)
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          asm volatile("" ::"v"(rcs[s]));
+#pragma unroll
+          for (int k = 0; k < DVN - 1; ++k) asm volatile("" ::"v"(cv[s][k]));
+        }
       }
       // ---- early exit: SP every iteration (:535-537); min-sum only when
       // h+1 < max_iters (:406-408); et_period > 1 thins the checks.
