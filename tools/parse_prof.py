@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--kernel", default="decode_small_kernel")
     ap.add_argument("--json", default=None)
     ap.add_argument("--key", default=None)
+    ap.add_argument("--per-decode", default=None,
+                    help="large-code path: sum the traffic of every kernel whose name contains "
+                         "this substring and divide by the number of decodes (g_reset dispatches)")
     a = ap.parse_args()
     res = {}
     kt = rows(os.path.join(a.dir, "kt", "**", "*kernel_trace.csv"))
@@ -65,6 +68,25 @@ def main():
         write = pmc["WRITE_SIZE"] * 1024.0
         res["hbm_bytes_per_launch"] = fetch + write
         print("HBM bytes/launch (2*FETCH_SIZE + WRITE_SIZE, KiB->B): %.0f" % (fetch + write))
+    if a.per_decode:
+        tot = collections.defaultdict(float)
+        for p in ("pmc3", "pmc4"):
+            for r in rows(os.path.join(a.dir, p, "**", "*counter_collection.csv")):
+                if a.per_decode in r["Kernel_Name"]:
+                    tot[r["Counter_Name"]] += float(r["Counter_Value"])
+        decodes = sum(1 for r in kt if "g_reset" in r["Kernel_Name"])
+        span = collections.defaultdict(float)
+        for r in kt:
+            if a.per_decode in r["Kernel_Name"]:
+                span["ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        nd_pmc = decodes  # each pass re-runs the same bench command
+        fetch = 2.0 * tot["FETCH_SIZE"] * 1024.0 / max(1, nd_pmc)
+        write = tot["WRITE_SIZE"] * 1024.0 / max(1, nd_pmc)
+        res["per_decode"] = {"decodes": decodes, "kernel_ns_per_decode": span["ns"] / max(1, decodes),
+                             "fetch_bytes": fetch, "write_bytes": write}
+        res["hbm_bytes_per_launch"] = fetch + write
+        print("per decode (%d decodes): kernel time %.3f ms, HBM bytes %.4g (fetch %.4g, write %.4g)"
+              % (decodes, span["ns"] / max(1, decodes) / 1e6, fetch + write, fetch, write))
     if a.json and a.key:
         try:
             allj = json.load(open(a.json))
