@@ -35,7 +35,8 @@ import time
 import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(REPO, "gr-ldpc_ece535a_amd"))
+# LDPC_PKG_DIR: an alternative build of the package (tools/ab.sh A/B runs)
+sys.path.insert(0, os.environ.get("LDPC_PKG_DIR", os.path.join(REPO, "gr-ldpc_ece535a_amd")))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 

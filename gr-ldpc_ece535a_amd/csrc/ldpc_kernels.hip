@@ -108,11 +108,13 @@ __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size
 //   tb[64S + 2]  check-pass operand per edge (+ dummy at 64S)
 //   eb[64S + 2]  check->variable message per edge (+ dummy at 64S)
 //   rb[64 NW]    -tx per column;  sb[64 NW] min-sum column totals
+//   nr[64S + 64NW]  sum-product: -r of each edge slot's / column slot's column
 template <typename Real, int S, int NW>
 struct Layout {
   size_t per_wave, total;
   __host__ __device__ Layout() {
-    per_wave = align16((2 * (64 * S + 2) + 2 * 64 * NW) * sizeof(Real));
+    // tb, eb, rb, sb, then nr[64 S + 64 NW]: per-lane negated channel values
+    per_wave = align16((2 * (64 * S + 2) + 2 * 64 * NW + 64 * (S + NW)) * sizeof(Real));
     total = (size_t)kWavesPerBlock * per_wave;
   }
 };
@@ -130,8 +132,13 @@ struct WaveTables {
 // DCN / DVN: row neighbours / column entries the loops visit (compile-time
 // degree bounds: DCN >= dc_max - 1, DVN >= dv_max); fewer than the record
 // sizes for codes of low degree, e.g. the reference's H (dc <= 6, dv <= 3).
+// FIN (sum-product): every sample of the frame is finite, so a missing
+// neighbour of a column / variable sum can read -r from the lane's own nr
+// slot: its term (-r) + r is exactly +0.0 and adding it is an exact no-op
+// (the running sum starts at +0.0 and never becomes -0.0) -- no selects.
+// Frames with a non-finite sample keep the selects (FIN = false).
 template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax,
-          typename Real = typename Math<PREC>::Real>
+          bool FIN = false, typename Real = typename Math<PREC>::Real>
 __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeArgs &a,
                                              const int64_t b, WaveTables<S, NW> &wt,
                                              Real *tb, Real *eb, Real *rb, Real *sb,
@@ -194,6 +201,19 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
     for (int q = 0; q < NW; ++q)
 #pragma unroll
       for (int k = 0; k < DVN; ++k) ea[q][k] = (uint32_t)field(wt.ce[q], k);
+    if constexpr (METHOD == 1 && FIN) {
+      Real *nr = sb + 64 * NW;
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int k = 0; k < DVN - 1; ++k)
+          ca[s][k] = ca[s][k] == eb_dummy ? lds_addr(nr + lane + 64 * s) : ca[s][k];
+#pragma unroll
+      for (int q = 0; q < NW; ++q)
+#pragma unroll
+        for (int k = 0; k < DVN; ++k)
+          ea[q][k] = ea[q][k] == eb_dummy ? lds_addr(nr + 64 * S + lane + 64 * q) : ea[q][k];
+    }
     constexpr uint32_t kSb = 64 * NW * sizeof(Real);  // sb - rb in bytes
     wave_lds_sync();  // rb and the dummies visible to every lane
     Real msg[S];      // SP: M(j,i) (:489-496); min-sum: L(q_ij) (:328-331)
@@ -202,6 +222,13 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
     for (int s = 0; s < S; ++s) {
       msg[s] = lds_ld<Real>(col[s]);
       lr[s] = Real(0);
+    }
+    if constexpr (METHOD == 1 && FIN) {
+      Real *nr = sb + 64 * NW;  // read by later gathers of this wave (in order)
+#pragma unroll
+      for (int s = 0; s < S; ++s) nr[lane + 64 * s] = -msg[s];
+#pragma unroll
+      for (int q = 0; q < NW; ++q) nr[64 * S + lane + 64 * q] = -rb[lane + 64 * q];
     }
 
     for (int h = 0; h < a.max_iters; ++h) {
@@ -277,8 +304,12 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         if constexpr (METHOD == 1) {
           // L = sum_j (E(j,i) + r(i)), ascending j; 1 iff L <= 0 (:519-532)
 #pragma unroll
-          for (int k = 0; k < DVN; ++k)
-            acc = ea[q][k] != eb_dummy ? acc + (ev[k] + rc) : acc;
+          for (int k = 0; k < DVN; ++k) {
+            if constexpr (FIN)
+              acc = acc + (ev[k] + rc);
+            else
+              acc = ea[q][k] != eb_dummy ? acc + (ev[k] + rc) : acc;
+          }
           bit = acc <= Real(0);
           post[q] = acc;
         } else {
@@ -315,8 +346,12 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         for (int s = 0; s < S; ++s) {
           Real acc = Real(0);
 #pragma unroll
-          for (int k = 0; k < DVN - 1; ++k)
-            acc = ca[s][k] != eb_dummy ? acc + (cv[s][k] + rcs[s]) : acc;
+          for (int k = 0; k < DVN - 1; ++k) {
+            if constexpr (FIN)
+              acc = acc + (cv[s][k] + rcs[s]);
+            else
+              acc = ca[s][k] != eb_dummy ? acc + (cv[s][k] + rcs[s]) : acc;
+          }
           msg[s] = acc;
         }
       } else {
@@ -467,7 +502,21 @@ __global__ void __launch_bounds__(kThreads)
   }
 
   while (b < a.B) {
-    decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane);
+    if constexpr (METHOD == 1) {
+      bool bad = false;
+      const float *src = a.in + b * a.cw_stride;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int c = lane + 64 * q;
+        if (c < code.N) bad |= !__builtin_isfinite(src[(int64_t)c * a.elem_stride] * a.polarity);
+      }
+      if (__ballot(bad) == 0)
+        decode_frame<PREC, METHOD, S, NW, DCN, DVN, true>(code, a, b, wt, tb, eb, rb, sb, lane);
+      else
+        decode_frame<PREC, METHOD, S, NW, DCN, DVN, false>(code, a, b, wt, tb, eb, rb, sb, lane);
+    } else {
+      decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane);
+    }
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(a.ticket, 1u);
     b = (int64_t)a.waves + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
