@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--sweep-schedules", default="0", help="comma list for --sweep-batch")
     ap.add_argument("--sweep-modes", default="1:f64,1:f32,0:f64",
                     help="method:precision list for the sweeps")
+    ap.add_argument("--sweep-config5", default="",
+                    help="comma list of B: config 5 (syndrome check every 5 iterations, mixed "
+                         "Eb/N0 0..4 dB per frame) latency/throughput table to stderr")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -233,6 +236,28 @@ def main():
                            Bs * dec.K / (k0 * 1e-3) / 1e6, k0 * 1e3 / max(1, it0.max())),
                           file=sys.stderr, flush=True)
             dec.set_schedule(args.schedule)
+
+    if args.sweep_config5:
+        # config 5: et_period 5, each frame at its own Eb/N0 drawn from {0,1,2,3,4} dB
+        for Bs in [int(x) for x in args.sweep_config5.split(",")]:
+            rng = np.random.Generator(np.random.PCG64(args.seed + 5))
+            dbs = rng.integers(0, 5, size=Bs)
+            parts = []
+            for db in range(5):
+                n = int((dbs == db).sum())
+                parts.append(synth(Hr, n, float(db), args.seed + 100 + db)[0] if n else
+                             np.zeros((0, Hr.shape[1]), np.float32))
+            y = np.zeros((Bs, Hr.shape[1]), np.float32)
+            for db in range(5):
+                y[dbs == db] = parts[db]
+            d_y = torch.from_numpy(y).to(dev)
+            for m, p in ((1, 0), (1, 1), (0, 0)):
+                w0, k0, it0, _ = time_decoder(dec, torch, d_y, Bs, m, args.iters, 5, p,
+                                              args.steps, args.warmup)
+                print("config5 method=%d prec=%d B=%7d et=5 mean_it=%6.2f max_it=%2d "
+                      "latency_ms=%8.4f Mbit/s=%9.2f" % (m, p, Bs, it0.mean(), it0.max(), k0,
+                                                          Bs * dec.K / (k0 * 1e-3) / 1e6),
+                      file=sys.stderr, flush=True)
 
     if args.sweep_wpc:
         for m, p in ((args.method, prec), (1, 1), (0, 0)):

@@ -1,0 +1,20 @@
+// ldpc_aux.hpp -- host entry points of ldpc_aux.hip (encoder, channel, counts).
+#pragma once
+
+#include <stdint.h>
+
+namespace ldpc {
+
+int launch_random_bits(uint8_t *out, int64_t n, uint64_t seed, void *stream);
+int launch_bpsk_awgn(const uint8_t *bits, int64_t n, float sigma, uint64_t seed, float *out,
+                     void *stream);
+int launch_count_errors(const uint8_t *a, const uint8_t *b, int64_t per_frame, int B,
+                        int32_t *counts, void *stream);
+// A: M x ceil(K/64) words (see ldpc_aux.hip); K <= 256.
+int launch_encode_small(const uint64_t *A, int M, int K, const uint8_t *data, int B, uint8_t *cw,
+                        void *stream);
+// CSR H whose columns 0..M-1 form the accumulator staircase.
+int launch_encode_ira(const int32_t *rp, const int32_t *ci, int M, int K, const uint8_t *data,
+                      int B, uint8_t *cw, void *stream);
+
+}  // namespace ldpc

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/ldpc_hip.h"
+#include "ldpc_aux.hpp"
 #include "ldpc_graph.hpp"
 #include "ldpc_kernels.hpp"
 
@@ -45,6 +46,11 @@ struct ldpc_ctx {
   void *d_work = nullptr;
   size_t work_bytes = 0;
   size_t work_limit = (size_t)8 << 30;
+  // device encoder (built on first ldpc_encode_device): 1 small (A = H_p^-1 H_d
+  // bit rows in d_encA), 2 IRA staircase, -1 no systematic encoder
+  int enc_kind = 0;
+  uint64_t *d_encA = nullptr;
+  std::string enc_err;
   std::string err;
 };
 
@@ -360,6 +366,69 @@ int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int preci
   return LDPC_OK;
 }
 
+// Systematic encoder of the context's H (codeword = [parity (M) | data (K)]):
+// small codes get A = H_p^-1 H_d by Gauss-Jordan over GF(2) (unique when the
+// first M columns are independent, which reorderHMatrix ensures); large codes
+// must have the accumulator staircase in columns 0..M-1 (IRA / DVB-S2).
+int prepare_encoder(ldpc_ctx *ctx) {
+  if (ctx->enc_kind > 0) return LDPC_OK;
+  if (ctx->enc_kind < 0) return set_err(ctx, LDPC_EUNSUPPORTED, ctx->enc_err);
+  const int M = ctx->M, N = ctx->N, K = N - M;
+  if (!ctx->H.empty() && K <= 256) {
+    const int W = (N + 63) / 64;
+    std::vector<uint64_t> rows((size_t)M * W, 0);
+    for (int j = 0; j < M; ++j)
+      for (int i = 0; i < N; ++i)
+        if (ctx->H[(size_t)j * N + i]) rows[(size_t)j * W + i / 64] |= 1ull << (i % 64);
+    for (int c = 0; c < M; ++c) {
+      int piv = -1;
+      for (int r = c; r < M; ++r)
+        if ((rows[(size_t)r * W + c / 64] >> (c % 64)) & 1) {
+          piv = r;
+          break;
+        }
+      if (piv < 0) {
+        ctx->enc_kind = -1;
+        ctx->enc_err = "the first M columns of H are dependent: no systematic encoder";
+        return set_err(ctx, LDPC_EUNSUPPORTED, ctx->enc_err);
+      }
+      if (piv != c)
+        for (int w = 0; w < W; ++w) std::swap(rows[(size_t)piv * W + w], rows[(size_t)c * W + w]);
+      for (int r = 0; r < M; ++r)
+        if (r != c && ((rows[(size_t)r * W + c / 64] >> (c % 64)) & 1))
+          for (int w = 0; w < W; ++w) rows[(size_t)r * W + w] ^= rows[(size_t)c * W + w];
+    }
+    const int KW = (K + 63) / 64;
+    std::vector<uint64_t> A((size_t)M * KW, 0);
+    for (int j = 0; j < M; ++j)
+      for (int i = 0; i < K; ++i)
+        if ((rows[(size_t)j * W + (M + i) / 64] >> ((M + i) % 64)) & 1)
+          A[(size_t)j * KW + i / 64] |= 1ull << (i % 64);
+    hipError_t e = hipMalloc(&ctx->d_encA, A.size() * 8);
+    if (e == hipSuccess) e = hipMemcpy(ctx->d_encA, A.data(), A.size() * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_err(ctx, e, "encoder upload");
+    ctx->enc_kind = 1;
+    return LDPC_OK;
+  }
+  for (int j = 0; j < M; ++j) {
+    int want[2] = {j - 1, j}, n = 0;
+    bool ok = true;
+    for (int32_t e = ctx->rp[j]; e < ctx->rp[j + 1] && ctx->ci[e] < M; ++e) {
+      const int c = ctx->ci[e];
+      if (n >= 2 || (j == 0 ? c != 0 : c != want[n])) ok = false;
+      ++n;
+    }
+    if (!ok || n != (j == 0 ? 1 : 2)) {
+      ctx->enc_kind = -1;
+      ctx->enc_err =
+          "large code without the accumulator staircase in columns 0..M-1: no device encoder";
+      return set_err(ctx, LDPC_EUNSUPPORTED, ctx->enc_err);
+    }
+  }
+  ctx->enc_kind = 2;
+  return LDPC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -558,6 +627,7 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
     if (p) (void)hipFree(p);
   if (ctx->d_work) (void)hipFree(ctx->d_work);
+  if (ctx->d_encA) (void)hipFree(ctx->d_encA);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -597,6 +667,51 @@ int ldpc_ctx_csr(const ldpc_ctx *ctx, int32_t *row_ptr_out, int32_t *col_idx_out
 int ldpc_ctx_path(const ldpc_ctx *ctx) {
   if (!ctx) return LDPC_EINVAL;
   return ctx->graph ? 1 : 0;
+}
+
+int ldpc_encode_device(ldpc_ctx *ctx, const uint8_t *d_data_bits, int B, uint8_t *d_codewords,
+                       void *hip_stream) {
+  if (!ctx) return LDPC_EINVAL;
+  if (B < 0 || (B > 0 && (!d_data_bits || !d_codewords)))
+    return set_err(ctx, LDPC_EINVAL, "bad encoder arguments");
+  if (B == 0) return LDPC_OK;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  int rc = prepare_encoder(ctx);
+  if (rc != LDPC_OK) return rc;
+  void *st = hip_stream ? hip_stream : (void *)ctx->stream;
+  const int K = ctx->N - ctx->M;
+  if (ctx->enc_kind == 1)
+    rc = ldpc::launch_encode_small(ctx->d_encA, ctx->M, K, d_data_bits, B, d_codewords, st);
+  else
+    rc = ldpc::launch_encode_ira(ctx->d_rp ? ctx->d_rp : nullptr, ctx->d_ci, ctx->M, K,
+                                 d_data_bits, B, d_codewords, st);
+  return rc == 0 ? LDPC_OK : hip_err(ctx, hipGetLastError(), "encoder launch");
+}
+
+int ldpc_random_bits(uint8_t *d_out, int64_t n, uint64_t seed, void *hip_stream) {
+  if (n < 0 || (n > 0 && !d_out)) return set_err(nullptr, LDPC_EINVAL, "bad arguments");
+  return ldpc::launch_random_bits(d_out, n, seed, hip_stream) == 0
+             ? LDPC_OK
+             : hip_err(nullptr, hipGetLastError(), "random_bits launch");
+}
+
+int ldpc_bpsk_awgn(const uint8_t *d_bits, int64_t n, float sigma, uint64_t seed, float *d_out,
+                   void *hip_stream) {
+  if (n < 0 || (n > 0 && (!d_bits || !d_out)) || !(sigma >= 0.0f))
+    return set_err(nullptr, LDPC_EINVAL, "bad arguments");
+  return ldpc::launch_bpsk_awgn(d_bits, n, sigma, seed, d_out, hip_stream) == 0
+             ? LDPC_OK
+             : hip_err(nullptr, hipGetLastError(), "bpsk_awgn launch");
+}
+
+int ldpc_count_bit_errors(const uint8_t *d_a, const uint8_t *d_b, int64_t per_frame, int B,
+                          int32_t *d_counts, void *hip_stream) {
+  if (B < 0 || per_frame < 0 || (B > 0 && (!d_a || !d_b || !d_counts)))
+    return set_err(nullptr, LDPC_EINVAL, "bad arguments");
+  return ldpc::launch_count_errors(d_a, d_b, per_frame, B, d_counts, hip_stream) == 0
+             ? LDPC_OK
+             : hip_err(nullptr, hipGetLastError(), "count_errors launch");
 }
 
 int ldpc_set_work_limit(ldpc_ctx *ctx, int64_t bytes) {

@@ -40,6 +40,10 @@ SIGNATURES = {
     "ldpc_ctx_csr": (_i, [_vp, _i32p, _i32p]),
     "ldpc_ctx_path": (_i, [_vp]),
     "ldpc_set_work_limit": (_i, [_vp, _i64]),
+    "ldpc_encode_device": (_i, [_vp, _vp, _i, _vp, _vp]),
+    "ldpc_random_bits": (_i, [_vp, _i64, ctypes.c_uint64, _vp]),
+    "ldpc_bpsk_awgn": (_i, [_vp, _i64, ctypes.c_float, ctypes.c_uint64, _vp, _vp]),
+    "ldpc_count_bit_errors": (_i, [_vp, _vp, _i64, _i, _vp, _vp]),
     "ldpc_destroy": (None, [_vp]),
     "ldpc_last_error": (ctypes.c_char_p, [_vp]),
     "ldpc_ctx_info": (_i, [_vp, _i32p, _i32p, _i32p, _i32p, _i32p, _i32p, _i32p]),
@@ -224,6 +228,12 @@ class Decoder:
     def set_waves_per_cu(self, n):
         _check(lib().ldpc_set_waves_per_cu(self._ctx, int(n)), self._ctx)
 
+    def encode_device(self, d_data, B, d_codewords, stream=None):
+        """Enqueue a systematic encode of B frames (device pointers): (B, K)
+        0/1 bytes -> (B, N) codewords [parity | data]."""
+        _check(lib().ldpc_encode_device(self._ctx, d_data, int(B), d_codewords, stream),
+               self._ctx)
+
     def set_work_limit(self, nbytes):
         """Large-code path: device workspace cap (0 = default 8 GiB)."""
         _check(lib().ldpc_set_work_limit(self._ctx, int(nbytes)), self._ctx)
@@ -234,3 +244,19 @@ class Decoder:
 
     def synchronize(self):
         _check(lib().ldpc_synchronize(self._ctx), self._ctx)
+
+
+def random_bits(d_out, n, seed, stream=None):
+    """n seeded random 0/1 bytes into device memory (Philox4x32-10)."""
+    _check(lib().ldpc_random_bits(d_out, int(n), int(seed) & 0xFFFFFFFFFFFFFFFF, stream))
+
+
+def bpsk_awgn(d_bits, n, sigma, seed, d_out, stream=None):
+    """d_out = 2 * bits - 1 + sigma * N(0, 1) (float32, device pointers)."""
+    _check(lib().ldpc_bpsk_awgn(d_bits, int(n), float(sigma), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                d_out, stream))
+
+
+def count_bit_errors(d_a, d_b, per_frame, B, d_counts, stream=None):
+    """Per-frame count of differing 0/1 bytes (device pointers)."""
+    _check(lib().ldpc_count_bit_errors(d_a, d_b, int(per_frame), int(B), d_counts, stream))

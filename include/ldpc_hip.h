@@ -22,6 +22,11 @@
  *   ldpc_check_frame        checkFrame :236-253
  *   ldpc_encode             makeParityCheck, lib/ldpc_encoder_bc_impl.cc:275-294
  *   ldpc_default_h          the hard-coded 32x64 H, lib/ldpc_decoder_cb_impl.cc:60-96
+ *   ldpc_encode_device      makeParityCheck on the GPU (lib/ldpc_encoder_bc_impl.cc:275-294;
+ *                           IRA accumulator codes for SURVEY config 4)
+ *   ldpc_random_bits, ldpc_bpsk_awgn, ldpc_count_bit_errors
+ *                           the BER program's source bits, BPSK + AWGN and
+ *                           biterr (apps/ldpc_lapack.cpp:603-650, :508-517) on the GPU
  *
  * Conventions: plain pointers and sizes only; errors are negative return
  * codes (LDPC_E*), never exceptions; ldpc_last_error() gives the text.  One
@@ -181,6 +186,34 @@ int ldpc_set_schedule(ldpc_ctx *ctx, int schedule);
 /* Large-code path: device workspace cap in bytes (0 = default 8 GiB).  A
  * batch larger than the cap allows is decoded in consecutive groups. */
 int ldpc_set_work_limit(ldpc_ctx *ctx, int64_t bytes);
+
+/* ---- encoder, channel, error counting (device buffers) ------------ */
+
+/* Systematic encode of B frames: d_data_bits B x (N-M) bytes 0/1 ->
+ * d_codewords B x N bytes = [parity (M) | data (N-M)] in the context's column
+ * order (for a reordered H the encoder block's [parity; data] output,
+ * lib/ldpc_encoder_bc_impl.cc:153-165).  Small codes: any H whose first M
+ * columns are independent; large codes: IRA / DVB-S2-style H (columns
+ * 0..M-1 the accumulator staircase), else LDPC_EUNSUPPORTED.  Enqueued on
+ * hip_stream (NULL = the context's stream). */
+int ldpc_encode_device(ldpc_ctx *ctx, const uint8_t *d_data_bits, int B,
+                       uint8_t *d_codewords, void *hip_stream);
+
+/* n bytes of seeded pseudo-random bits 0/1 (Philox4x32-10; the same seed
+ * gives the same bits).  Current device; NULL stream = the null stream.
+ * Errors: ldpc_last_error(NULL). */
+int ldpc_random_bits(uint8_t *d_out, int64_t n, uint64_t seed, void *hip_stream);
+
+/* BPSK + AWGN: d_out[i] = (2 d_bits[i] - 1) + sigma * n_i, n_i ~ N(0,1)
+ * (Philox + Box-Muller, seeded); sigma = sqrt(10^(-EbN0/10)) reproduces the
+ * reference's convention (apps/ldpc_lapack.cpp:629-636). */
+int ldpc_bpsk_awgn(const uint8_t *d_bits, int64_t n, float sigma, uint64_t seed,
+                   float *d_out, void *hip_stream);
+
+/* d_counts[b] = number of i < per_frame with d_a[b*per_frame+i] !=
+ * d_b[b*per_frame+i] (low bits), b < B. */
+int ldpc_count_bit_errors(const uint8_t *d_a, const uint8_t *d_b, int64_t per_frame, int B,
+                          int32_t *d_counts, void *hip_stream);
 
 /* Blocks until the context's stream is idle. */
 int ldpc_synchronize(ldpc_ctx *ctx);

@@ -122,3 +122,15 @@ def test_degree_limits_reported_before_device_lookup():
     H[:, 300] = 1  # column degree 300 > the large-code kernels' 16
     with pytest.raises(L.LdpcError, match="outside the large-code kernels"):
         L.Decoder(H)
+
+
+def test_ber_octave_format_and_grid():
+    from ldpc_ece535a import ber
+    g = ber.parse_range("-7:10:0.5")
+    assert len(g) == 35 and g[0] == -7.0 and g[-1] == 10.0 and g == ber.DEFAULT_EBN0
+    assert abs(ber.sigma_of(2.0) - np.sqrt(10 ** -0.2)) < 1e-15
+    res = {n: {"ber": [0.5, 0.25], "fer": [3, 0]} for n, _ in ber.METHODS}
+    txt = ber.octave([0.0, 1.5], res)
+    lines = txt.splitlines()
+    assert lines[0] == "EbN0=[0 1.5 ];" and lines[2] == "ber0=[0.5 0.25 ];"
+    assert "fer3=[" in txt and "3, 0" in txt
