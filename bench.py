@@ -182,8 +182,34 @@ def time_decoder(dec, torch, d_in, B, method, iters, et, prec, steps, warmup, di
     return wall, kern_ms, d_iters.cpu().numpy(), (d_packed, d_iters, d_synd)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def relaunch_distributed(args):
+    """`python bench.py --gpus N` (N > 1) outside torchrun: run torchrun as a
+    child process (no exec; nothing has touched the GPU yet) and return its
+    exit code.  The driver's own torchrun launch sets WORLD_SIZE and never
+    gets here."""
+    import random
+    import subprocess
+    port = str(29500 + random.randint(0, 2000))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", port, os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -393,7 +419,8 @@ def main():
             line["cpu_baseline"] = {
                 "value": round(nb * dec.K / cpu_s / 1e6, 5), "unit": "Mbit/s", "cores": threads,
                 "kind": "port",
-                "sample": "first %d of rank 0's %d frames, sparse oracle, %d threads" % (nb, B, threads)}
+                "sample": "first %d of rank 0's %d frames, sparse oracle, %d threads on %s"
+                          % (nb, B, threads, cpu_model())}
             line["parity"] = {"frames": nb,
                               "packed_mismatch_frames": int((ref["packed"] != packed[:nb]).any(axis=1).sum()),
                               "iters_mismatch_frames": int((ref["iters"] != iters_b[:nb]).sum()),
@@ -415,8 +442,9 @@ def main():
             "unit": "Mbit/s",
             "cores": threads,
             "kind": "port",
-            "sample": "the same %d frames (rank 0's batch), %d threads; 1-core: %.5f Mbit/s on "
-                      "the first %d frames" % (B, threads, nsample * dec.K / cpu1_s / 1e6, nsample),
+            "sample": "the same %d frames (rank 0's batch), %d threads on %s; 1-core: %.5f "
+                      "Mbit/s on the first %d frames" % (B, threads, cpu_model(),
+                                                          nsample * dec.K / cpu1_s / 1e6, nsample),
         }
         line["parity"] = {"frames": B, "packed_mismatch_frames": mism,
                           "iters_mismatch_frames": int((ref["iters"] != iters_b).sum()),
