@@ -33,6 +33,10 @@
 // Math<PREC> as the small-code kernel (ldpc_device.hpp).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
+#include <stdlib.h>
+
 #include "ldpc_device.hpp"
 #include "ldpc_graph.hpp"
 
@@ -57,16 +61,48 @@ __device__ __forceinline__ int64_t at(int64_t x, int k, int64_t n, int lane) {
   return ((int64_t)k * n + x) * 64 + lane;
 }
 
+// The group's live buffers (compaction swaps them on the device).
+__device__ __forceinline__ GraphWork live(GraphWork w) {
+  const GraphState *st = w.st;
+  w.Q = st->Q;
+  w.R = st->R;
+  w.L = st->L;
+  w.post = st->post;
+  w.hard = st->hard;
+  w.perm = st->perm;
+  return w;
+}
+
+// Slot b holds a frame of this group (compaction empties slots).
+__device__ __forceinline__ bool valid_slot(const GraphWork &w, int64_t b) { return w.perm[b] >= 0; }
+
 // One wave per chunk: counters, padding frames (b >= B) marked stopped.
 __global__ void __launch_bounds__(64) g_reset(GraphWork w, int B, int used0) {
   const int k = blockIdx.x, lane = threadIdx.x;
   const int b = k * 64 + lane;
   w.used[b] = used0;
   w.synd[b] = 0;
+  w.perm[b] = b < B ? b : -1;
   const uint64_t pad = __ballot(b >= B);
   if (lane == 0) {
     w.done_w[k] = pad;
     w.chunk_done[k] = 0;
+  }
+  if (k == 0 && lane == 0) {
+    GraphState *st = w.st;
+    st->Q = w.Q;
+    st->R = w.R;
+    st->L = w.L;
+    st->post = w.post;
+    st->hard = w.hard;
+    st->perm = w.perm;
+    st->L2 = w.L2;
+    st->post2 = w.post2;
+    st->hard2 = w.hard2;
+    st->perm2 = w.perm2;
+    st->slots = w.Bp;
+    st->n_new = 0;
+    st->flag = 0;
   }
 }
 
@@ -77,9 +113,10 @@ __global__ void __launch_bounds__(64) g_reset(GraphWork w, int B, int used0) {
 //        of the column (:328-331, :489-496);
 //   else (methods 2/3): y = hard decision of tx (:424-431, :563-569).
 template <typename Real, bool SOFT>
-__global__ void __launch_bounds__(256) g_load(GraphView g, GraphWork w, const float *in,
+__global__ void __launch_bounds__(256) g_load(GraphView g, GraphWork w_, const float *in,
                                               int64_t cw_stride, int elem_stride,
                                               float polarity, int B) {
+  const GraphWork w = live(w_);
   __shared__ float tile[64][65];
   const int c0 = blockIdx.x * 64, k = blockIdx.y, b0 = k * 64;
   const int lane = threadIdx.x & 63, wv = wave_in_block();
@@ -115,7 +152,8 @@ __global__ void __launch_bounds__(256) g_load(GraphView g, GraphWork w, const fl
 // same pass evaluates checkFrame's rows (:236-253) on the hard decision of
 // iteration h-1: 64 frames per XOR of packed words.
 template <int PREC, int METHOD, int DC>
-__global__ void __launch_bounds__(256) g_check(GraphView g, GraphWork w, int h) {
+__global__ void __launch_bounds__(256) g_check(GraphView g, GraphWork w_, int h) {
+  const GraphWork w = live(w_);
   typedef typename Math<PREC>::Real Real;
   const int k = blockIdx.y;
   if (w.chunk_done[k]) return;
@@ -187,7 +225,8 @@ __global__ void __launch_bounds__(256) g_check(GraphView g, GraphWork w, int h) 
 
 // Bit-flip: parity words of each row over the hard decision of iteration h-1
 // (the received y for h == 0), :443-452; E(i,j) of an edge is parity ^ ci(j).
-__global__ void __launch_bounds__(256) g_check_bf(GraphView g, GraphWork w, int h) {
+__global__ void __launch_bounds__(256) g_check_bf(GraphView g, GraphWork w_, int h) {
+  const GraphWork w = live(w_);
   const int k = blockIdx.y;
   if (w.chunk_done[k]) return;
   const int64_t chunks = w.chunks;
@@ -242,7 +281,8 @@ __global__ void __launch_bounds__(256) g_decide(GraphWork w, int h, int max_iter
 //   sum-product: L = sum_j (E(j,i) + r) (:519-532), vhat = L <= 0, and
 //     M(j,i) = sum_{k != j} (E(k,i) + r) (:540-553), both ascending.
 template <typename Real, int METHOD, int DV>
-__global__ void __launch_bounds__(256) g_var(GraphView g, GraphWork w) {
+__global__ void __launch_bounds__(256) g_var(GraphView g, GraphWork w_) {
+  const GraphWork w = live(w_);
   const int k = blockIdx.y;
   if (w.chunk_done[k]) return;
   const int lane = threadIdx.x & 63;
@@ -306,7 +346,8 @@ __global__ void __launch_bounds__(256) g_var(GraphView g, GraphWork w) {
 // Bit-flip vote (:453-467): column i becomes 1 - y(i) when more than M/2 of
 // its checks disagree with y(i) (parity ^ vhat(i) != y(i)), else keeps vhat(i).
 template <int DV>
-__global__ void __launch_bounds__(256) g_var_bf(GraphView g, GraphWork w) {
+__global__ void __launch_bounds__(256) g_var_bf(GraphView g, GraphWork w_) {
+  const GraphWork w = live(w_);
   const int k = blockIdx.y;
   if (w.chunk_done[k]) return;
   const int lane = threadIdx.x & 63;
@@ -330,7 +371,8 @@ __global__ void __launch_bounds__(256) g_var_bf(GraphView g, GraphWork w) {
 }
 
 // Final syndrome weight (uncapped checkFrame) of every frame's decision.
-__global__ void __launch_bounds__(256) g_synd(GraphView g, GraphWork w, int B) {
+__global__ void __launch_bounds__(256) g_synd(GraphView g, GraphWork w_, int B) {
+  const GraphWork w = live(w_);
   const int k = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const int64_t chunks = w.chunks;
@@ -345,14 +387,19 @@ __global__ void __launch_bounds__(256) g_synd(GraphView g, GraphWork w, int B) {
     for (int t = 0; t < d; ++t) par ^= w.hard[(int64_t)g.ci[e0 + t] * chunks + k];
     cnt += (int)bit_of(par, lane);
   }
-  if (cnt && b < B) atomicAdd(&w.synd[b], cnt);
+  if (cnt && b < B && valid_slot(w, b)) atomicAdd(&w.synd[b], cnt);
 }
 
 // Outputs, transposed back to frame-major through LDS: packed info bytes
 // (bits M.., MSB first, :207-219), and the per-frame counters.
-__global__ void __launch_bounds__(256) g_store_packed(GraphView g, GraphWork w, DecodeArgs a) {
+// flush = 1: only frames that stopped, written before a compaction drops them.
+__global__ void __launch_bounds__(256) g_store_packed(GraphView g, GraphWork w_, DecodeArgs a,
+                                                      int flush) {
+  const GraphWork w = live(w_);
+  if (flush && !w.st->flag) return;
   __shared__ uint8_t tile[64][65];
   const int q0 = blockIdx.x * 64, k = blockIdx.y, b0 = k * 64;
+  const uint64_t sel = flush ? w.done_w[k] : ~0ull;
   const int lane = threadIdx.x & 63, wv = wave_in_block();
   const int64_t chunks = w.chunks;
   for (int qq = wv; qq < 64; qq += 4) {
@@ -368,22 +415,26 @@ __global__ void __launch_bounds__(256) g_store_packed(GraphView g, GraphWork w, 
   __syncthreads();
   for (int i = threadIdx.x; i < 64 * 64; i += 256) {
     const int f = i >> 6, qq = i & 63;
-    const int b = b0 + f, q = q0 + qq;
-    if (b < a.B && q < g.KB) a.packed[(int64_t)b * g.KB + q] = tile[f][qq];
+    const int fr = w.perm[b0 + f], q = q0 + qq;
+    if (fr >= 0 && bit_of(sel, f) && q < g.KB) a.packed[(int64_t)fr * g.KB + q] = tile[f][qq];
   }
   if (blockIdx.x == 0 && threadIdx.x < 64) {
-    const int b = b0 + threadIdx.x;
-    if (b < a.B) {
-      if (a.iters) a.iters[b] = w.used[b];
-      if (a.synd) a.synd[b] = w.synd[b];
+    const int b = b0 + threadIdx.x, fr = w.perm[b];
+    if (fr >= 0 && bit_of(sel, threadIdx.x)) {
+      if (a.iters) a.iters[fr] = w.used[b];
+      if (a.synd) a.synd[fr] = w.synd[b];  // 0 for a frame that stopped
     }
   }
 }
 
 // Full hard decision, B x N bytes.
-__global__ void __launch_bounds__(256) g_store_bits(GraphView g, GraphWork w, uint8_t *dst, int B) {
+__global__ void __launch_bounds__(256) g_store_bits(GraphView g, GraphWork w_, uint8_t *dst, int B,
+                                                    int flush) {
+  const GraphWork w = live(w_);
+  if (flush && !w.st->flag) return;
   __shared__ uint8_t tile[64][65];
   const int c0 = blockIdx.x * 64, k = blockIdx.y, b0 = k * 64;
+  const uint64_t sel = flush ? w.done_w[k] : ~0ull;
   const int lane = threadIdx.x & 63, wv = wave_in_block();
   for (int cc = wv; cc < 64; cc += 4) {
     const int c = c0 + cc;
@@ -392,15 +443,19 @@ __global__ void __launch_bounds__(256) g_store_bits(GraphView g, GraphWork w, ui
   __syncthreads();
   for (int i = threadIdx.x; i < 64 * 64; i += 256) {
     const int f = i >> 6, cc = i & 63;
-    const int b = b0 + f, c = c0 + cc;
-    if (b < B && c < g.N) dst[(int64_t)b * g.N + c] = tile[f][cc];
+    const int fr = w.perm[b0 + f], c = c0 + cc;
+    if (fr >= 0 && fr < B && bit_of(sel, f) && c < g.N) dst[(int64_t)fr * g.N + c] = tile[f][cc];
   }
 }
 
 // Posterior, B x N floats.
-__global__ void __launch_bounds__(256) g_store_post(GraphView g, GraphWork w, float *dst, int B) {
+__global__ void __launch_bounds__(256) g_store_post(GraphView g, GraphWork w_, float *dst, int B,
+                                                    int flush) {
+  const GraphWork w = live(w_);
+  if (flush && !w.st->flag) return;
   __shared__ float tile[64][65];
   const int c0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
+  const uint64_t sel = flush ? w.done_w[blockIdx.y] : ~0ull;
   const int lane = threadIdx.x & 63, wv = wave_in_block();
   for (int cc = wv; cc < 64; cc += 4) {
     const int c = c0 + cc;
@@ -409,8 +464,145 @@ __global__ void __launch_bounds__(256) g_store_post(GraphView g, GraphWork w, fl
   __syncthreads();
   for (int i = threadIdx.x; i < 64 * 64; i += 256) {
     const int f = i >> 6, cc = i & 63;
-    const int b = b0 + f, c = c0 + cc;
-    if (b < B && c < g.N) dst[(int64_t)b * g.N + c] = tile[f][cc];
+    const int fr = w.perm[b0 + f], c = c0 + cc;
+    if (fr >= 0 && fr < B && bit_of(sel, f) && c < g.N) dst[(int64_t)fr * g.N + c] = tile[f][cc];
+  }
+}
+
+// ---- compaction --------------------------------------------------------
+// A 64-frame chunk runs until its slowest frame stops, so without
+// compaction a frame that stopped keeps costing memory traffic.  After an
+// iteration's variable pass (Q live, R dead), when the running frames fit in
+// fewer chunks and fill at most 3/4 of the occupied slots, they move, in
+// order, to the lowest slots of the spare buffers: their outputs are
+// unaffected (every frame's arithmetic is independent of its slot), and the
+// frames that stopped are flushed to the caller's buffers first.
+
+// One block: count running frames, decide, and list new slot -> old slot.
+__global__ void __launch_bounds__(1024) g_plan(GraphWork w) {
+  __shared__ int part[16];
+  __shared__ int run_base;
+  GraphState *st = w.st;
+  const int live_chunks = st->slots / 64;
+  int mine = 0;
+  for (int k = threadIdx.x; k < live_chunks; k += 1024) mine += __popcll(~w.done_w[k]);
+  for (int off = 32; off > 0; off >>= 1) mine += __shfl_xor(mine, off);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = mine;
+  __syncthreads();
+  int active = 0;
+  for (int i = 0; i < 16; ++i) active += part[i];
+  const int new_chunks = (active + 63) / 64;
+  const bool go = active > 0 && new_chunks < live_chunks && 4 * active <= 3 * st->slots;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st->flag = go ? 1 : 0;
+    st->n_new = active;
+    run_base = 0;
+  }
+  if (!go) return;
+  __syncthreads();
+  // tiles of 1024 chunks: exclusive scan of per-chunk counts, then scatter
+  for (int k0 = 0; k0 < live_chunks; k0 += 1024) {
+    const int k = k0 + (int)threadIdx.x;
+    const uint64_t act = k < live_chunks ? ~w.done_w[k] : 0ull;
+    const int c = __popcll(act);
+    int incl = c;  // inclusive scan within the wave
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off);
+      if ((threadIdx.x & 63) >= off) incl += v;
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 63) part[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    int wave_base = 0;
+    for (int i = 0; i < (int)(threadIdx.x >> 6); ++i) wave_base += part[i];
+    int pos = run_base + wave_base + incl - c;
+    for (uint64_t m = act; m; m &= m - 1) w.src[pos++] = k * 64 + __builtin_ctzll(m);
+    __syncthreads();
+    if (threadIdx.x == 1023) run_base += wave_base + incl;
+    __syncthreads();
+  }
+}
+
+// Live Q of the running frames -> the R buffer (dead between the variable
+// pass and the next check pass), new slot t <- old slot src[t].
+template <typename Real>
+__global__ void __launch_bounds__(256) g_move_msgs(GraphView g, GraphWork w_) {
+  const GraphWork w = live(w_);
+  const GraphState *st = w.st;
+  if (!st->flag) return;
+  const int kn = blockIdx.y, lane = threadIdx.x & 63;
+  const int t = kn * 64 + lane;
+  if (kn * 64 >= st->n_new) return;
+  const bool ok = t < st->n_new;
+  const int s = ok ? w.src[t] : 0;
+  const Real *Q = (const Real *)w.Q + at(0, s >> 6, g.E, s & 63);
+  Real *D = (Real *)w.R + at(0, kn, g.E, lane);
+  const int per = (g.E + gridDim.x - 1) / gridDim.x;
+  const int e0 = blockIdx.x * per, e1 = min(g.E, e0 + per);
+  if (ok)
+    for (int e = e0 + wave_in_block(); e < e1; e += 4) D[(int64_t)e * 64] = Q[(int64_t)e * 64];
+}
+
+// Channel values, posteriors and hard bits of the running frames -> spares.
+__global__ void __launch_bounds__(256) g_move_cols(GraphView g, GraphWork w_) {
+  const GraphWork w = live(w_);
+  const GraphState *st = w.st;
+  if (!st->flag) return;
+  const int kn = blockIdx.y, lane = threadIdx.x & 63;
+  if (kn * 64 >= st->n_new) return;
+  const int t = kn * 64 + lane;
+  const bool ok = t < st->n_new;
+  const int s = ok ? w.src[t] : 0;
+  const int per = (g.N + gridDim.x - 1) / gridDim.x;
+  const int c0 = blockIdx.x * per, c1 = min(g.N, c0 + per);
+  for (int c = c0 + wave_in_block(); c < c1; c += 4) {
+    if (ok) {
+      st->L2[at(c, kn, g.N, lane)] = w.L[at(c, s >> 6, g.N, s & 63)];
+      if (w.post) st->post2[at(c, kn, g.N, lane)] = w.post[at(c, s >> 6, g.N, s & 63)];
+    }
+    const bool bit = ok && bit_of(w.hard[(int64_t)c * w.chunks + (s >> 6)], s & 63);
+    const uint64_t bw = __ballot(bit);
+    if (lane == 0) st->hard2[(int64_t)c * w.chunks + kn] = bw;
+  }
+}
+
+// Swap to the compacted buffers and rewrite the per-slot state.
+__global__ void __launch_bounds__(256) g_commit(GraphWork w, int used0) {
+  GraphState *st = w.st;
+  if (!st->flag) return;
+  const int n = st->n_new;
+  // every slot of the spare map: slots past the old occupied range still
+  // hold entries from an earlier use of the buffer
+  for (int t = threadIdx.x; t < w.Bp; t += 256) {
+    st->perm2[t] = t < n ? st->perm[w.src[t]] : -1;
+    if (t < n) w.used[t] = used0;  // still running
+  }
+  for (int k = threadIdx.x; k < w.chunks; k += 256) {
+    const int lo = k * 64;
+    const uint64_t empty = lo + 64 <= n ? 0ull : (lo >= n ? ~0ull : (~0ull << (n - lo)));
+    w.done_w[k] = empty;
+    w.chunk_done[k] = lo >= n ? 1 : 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    void *q = st->Q;
+    st->Q = st->R;
+    st->R = q;
+    float *l = st->L;
+    st->L = st->L2;
+    st->L2 = l;
+    float *p = st->post;
+    st->post = st->post2;
+    st->post2 = p;
+    uint64_t *hd = st->hard;
+    st->hard = st->hard2;
+    st->hard2 = hd;
+    int32_t *pm = st->perm;
+    st->perm = st->perm2;
+    st->perm2 = pm;
+    st->slots = (n + 63) / 64 * 64;
+    st->flag = 0;
   }
 }
 
@@ -434,6 +626,31 @@ void launch_var(const GraphView &g, const GraphWork &w, dim3 grid, hipStream_t s
     g_var<Real, METHOD, 16><<<grid, 256, 0, st>>>(g, w);
 }
 
+// LDPC_GRAPH_COMPACT=0 disables compaction (A/B and debugging knob).
+bool compaction_enabled() {
+  const char *e = getenv("LDPC_GRAPH_COMPACT");
+  return !(e && e[0] == '0');
+}
+
+// Compaction after the variable pass of iteration h (every other iteration
+// from h = 3 while more than one iteration remains; a no-op unless g_plan
+// finds the running frames fit in fewer chunks and <= 3/4 of the slots).
+template <typename Real>
+void launch_compaction(const GraphView &g, const GraphWork &w, const DecodeArgs &a, int used0,
+                       hipStream_t st) {
+  const int chunks = w.chunks;
+  g_plan<<<1, 1024, 0, st>>>(w);
+  g_store_packed<<<dim3((g.KB + 63) / 64, chunks), 256, 0, st>>>(g, w, a, 1);
+  if (a.bits) g_store_bits<<<dim3((g.N + 63) / 64, chunks), 256, 0, st>>>(g, w, a.bits, a.B, 1);
+  if (a.llr && w.post)
+    g_store_post<<<dim3((g.N + 63) / 64, chunks), 256, 0, st>>>(g, w, a.llr, a.B, 1);
+  const unsigned eb = (unsigned)std::min<int64_t>(128, (g.E + 255) / 256);
+  const unsigned cb = (unsigned)std::min<int64_t>(64, (g.N + 255) / 256);
+  g_move_msgs<Real><<<dim3(eb, chunks), 256, 0, st>>>(g, w);
+  g_move_cols<<<dim3(cb, chunks), 256, 0, st>>>(g, w);
+  g_commit<<<1, 256, 0, st>>>(w, used0);
+}
+
 template <int PREC, int METHOD>
 void run_soft(const GraphView &g, const GraphWork &w, const DecodeArgs &a, dim3 rgrid,
               dim3 cgrid, hipStream_t st) {
@@ -444,6 +661,8 @@ void run_soft(const GraphView &g, const GraphWork &w, const DecodeArgs &a, dim3 
     launch_check<CP, METHOD>(g, w, h, rgrid, st);
     if (h > 0) g_decide<<<w.chunks, 256, 0, st>>>(w, h, a.max_iters, a.et_period);
     launch_var<Real, METHOD>(g, w, cgrid, st);
+    if (compaction_enabled() && w.chunks > 1 && h >= 3 && (h & 1) && h + 1 < a.max_iters)
+      launch_compaction<Real>(g, w, a, a.max_iters, st);
   }
 }
 
@@ -464,6 +683,9 @@ size_t graph_work_bytes(const GraphView &g, int Bp, int prec, int method, bool w
   n += al256((size_t)check_waves(g) * chunks * 8) + al256(chunks * 8) + al256(chunks);
   n += 2 * al256((size_t)Bp * 4);
   if (want_post) n += al256((size_t)g.N * Bp * 4);
+  // compaction: state, perm x2, src, spare L / post / hard
+  n += al256(sizeof(GraphState)) + 3 * al256((size_t)Bp * 4) + al256((size_t)g.N * chunks * 8);
+  if (soft) n += al256((size_t)g.N * Bp * 4) + (want_post ? al256((size_t)g.N * Bp * 4) : 0);
   return n;
 }
 
@@ -498,6 +720,15 @@ void graph_work_carve(GraphWork &w, void *base, const GraphView &g, int Bp, int 
   w.used = (int32_t *)take((size_t)Bp * 4);
   w.synd = (int32_t *)take((size_t)Bp * 4);
   w.post = want_post ? (float *)take((size_t)g.N * Bp * 4) : nullptr;
+  w.st = (GraphState *)take(sizeof(GraphState));
+  w.perm = (int32_t *)take((size_t)Bp * 4);
+  w.perm2 = (int32_t *)take((size_t)Bp * 4);
+  w.src = (int32_t *)take((size_t)Bp * 4);
+  w.hard2 = (uint64_t *)take((size_t)g.N * chunks * 8);
+  if (soft) {
+    w.L2 = (float *)take((size_t)g.N * Bp * 4);
+    w.post2 = want_post ? (float *)take((size_t)g.N * Bp * 4) : nullptr;
+  }
 }
 
 int launch_graph_decode(const GraphView &g, const GraphWork &w, const DecodeArgs &a, int method,
@@ -547,9 +778,9 @@ int launch_graph_decode(const GraphView &g, const GraphWork &w, const DecodeArgs
     }
   }
   g_synd<<<rgrid, 256, 0, st>>>(g, w, a.B);
-  g_store_packed<<<dim3((g.KB + 63) / 64, chunks), 256, 0, st>>>(g, w, a);
-  if (a.bits) g_store_bits<<<tgrid, 256, 0, st>>>(g, w, a.bits, a.B);
-  if (a.llr && w.post) g_store_post<<<tgrid, 256, 0, st>>>(g, w, a.llr, a.B);
+  g_store_packed<<<dim3((g.KB + 63) / 64, chunks), 256, 0, st>>>(g, w, a, 0);
+  if (a.bits) g_store_bits<<<tgrid, 256, 0, st>>>(g, w, a.bits, a.B, 0);
+  if (a.llr && w.post) g_store_post<<<tgrid, 256, 0, st>>>(g, w, a.llr, a.B, 0);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

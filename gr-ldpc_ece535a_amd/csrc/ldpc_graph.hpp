@@ -32,6 +32,20 @@ struct GraphView {
   int M, N, E, KB, dc_max, dv_max;
 };
 
+// Live buffers of a group in flight.  Compaction (ldpc_graph.hip) moves the
+// still-running frames into the lowest slots of spare buffers and swaps these
+// pointers on the device, so every kernel resolves them at entry.
+struct GraphState {
+  void *Q, *R;             // live variable->check messages; the other buffer
+  float *L, *L2;           // live / spare channel values
+  float *post, *post2;     // live / spare posteriors (optional)
+  uint64_t *hard, *hard2;  // live / spare packed hard decisions
+  int32_t *perm, *perm2;   // slot -> frame index of the group (-1: empty)
+  int32_t slots;           // slots still holding frames (multiple of 64)
+  int32_t n_new;           // plan: running frames
+  int32_t flag;            // plan: compact now
+};
+
 struct GraphWork {
   void *Q;             // E x Bp Real: variable -> check messages
   void *R;             // E x Bp Real: check -> variable messages
@@ -47,6 +61,12 @@ struct GraphWork {
   int32_t *used;       // Bp: iterations executed
   int32_t *synd;       // Bp: final syndrome weight
   float *post;         // N x Bp: final posterior (only with an llr output)
+  int32_t *perm;       // Bp: slot -> frame index (live copy from st)
+  GraphState *st;      // device-resident live pointers
+  int32_t *src;        // Bp: compaction plan, new slot -> old slot
+  float *L2, *post2;   // spares the compaction moves into (soft methods)
+  uint64_t *hard2;
+  int32_t *perm2;
   int Bp, chunks, check_waves;
 };
 

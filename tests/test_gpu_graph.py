@@ -157,3 +157,24 @@ def test_dvbs2_like_full_batch_roundtrip(dvb):
             ref = orc.decode_batch_sparse(0, rp, ci, M, N, y[:64], 50, nthreads=16,
                                           want_bits=False)
             np.testing.assert_array_equal(out["iters"][:64], ref["iters"])
+
+
+@pytest.mark.parametrize("method,db", [(0, 2), (1, 2), (0, 4), (1, 1)])
+def test_graph_path_repeated_compaction(method, db):
+    """Thousands of frames on the large-code kernels: running frames are
+    compacted several times as others stop; every output (bits, iterations,
+    syndromes, posteriors) must still be the oracle's."""
+    import bench
+    import ldpc_ece535a as L
+    from oracle import oracle as orc
+    d = L.Decoder(force_graph=True)
+    y, _ = bench.synth(d.H, 4096, db, 50 + db)
+    out = d.decode(y, method=method, max_iters=50, precision=2, want_llr=True)
+    ref = orc.decode_batch(method, d.H, y, 50, nthreads=16, want_post=True)
+    np.testing.assert_array_equal(out["iters"], ref["iters"])
+    np.testing.assert_array_equal(out["synd"], ref["synd"])
+    np.testing.assert_array_equal(out["bits"], ref["bits"])
+    if method == 0:
+        np.testing.assert_array_equal(out["llr"], ref["post"])
+    else:
+        np.testing.assert_allclose(out["llr"], ref["post"], rtol=1e-6, atol=1e-6)
