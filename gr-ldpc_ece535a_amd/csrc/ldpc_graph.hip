@@ -156,6 +156,11 @@ __global__ void __launch_bounds__(256) g_check(GraphView g, GraphWork w_, int h)
   const GraphWork w = live(w_);
   typedef typename Math<PREC>::Real Real;
   const int k = blockIdx.y;
+  __shared__ fm::LogTabEntry logtab[1 << fm::kLogTabBits];
+  if constexpr (METHOD == 1 && PREC == 0) {
+    if (w.chunk_done[k]) return;  // uniform per block: no thread misses the barrier
+    stage_logtab(logtab);
+  }
   if (w.chunk_done[k]) return;
   const int lane = threadIdx.x & 63;
   const int64_t chunks = w.chunks;
@@ -192,7 +197,7 @@ __global__ void __launch_bounds__(256) g_check(GraphView g, GraphWork w_, int h)
         Real T = Real(1);
 #pragma unroll
         for (int t = 0; t < DC; ++t) T = (t != e && t < d) ? T * q[t] : T;
-        R[(int64_t)(e0 + e) * 64] = Math<PREC>::check_msg(T);
+        R[(int64_t)(e0 + e) * 64] = Math<PREC>::check_msg(T, logtab);
       }
     } else {
       // L(r_ji) = (prod_k sign(L(q_jk))) * sign(L(q_ji)) * min_{k != i} |L(q_jk)|

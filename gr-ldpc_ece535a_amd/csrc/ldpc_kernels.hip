@@ -142,7 +142,7 @@ template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = k
 __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeArgs &a,
                                              const int64_t b, WaveTables<S, NW> &wt,
                                              Real *tb, Real *eb, Real *rb, Real *sb,
-                                             const int lane) {
+                                             const int lane, const fm::LogTabEntry *logtab) {
   const int M = code.M, N = code.N;
   constexpr int kDummy = 64 * S;  // index of the per-wave identity element
   // Channel samples: tx = Re(in) * polarity (:149-153); r = -tx (:486,
@@ -260,7 +260,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           Real T = Real(1);
 #pragma unroll
           for (int k = 0; k < DCN; ++k) T = T * nb[s][k];
-          eb[lane + 64 * s] = Math<PREC>::check_msg(T);
+          eb[lane + 64 * s] = Math<PREC>::check_msg(T, logtab);
         } else {
           // min-sum horizontal step (:350-376): sign product over the row
           // times the minimum |L(q)| of the other edges.  Padding neighbours
@@ -451,6 +451,8 @@ __global__ void __launch_bounds__(kThreads)
   const int M = code.M;
   const Layout<Real, S, NW> L;
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.ticket_next = 0u;  // next launch's queue head
+  __shared__ fm::LogTabEntry logtab[1 << fm::kLogTabBits];
+  if constexpr (METHOD == 1 && PREC == 0) stage_logtab(logtab);
 
   int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave;
   if (b >= a.waves || b >= a.B) return;
@@ -511,11 +513,13 @@ __global__ void __launch_bounds__(kThreads)
         if (c < code.N) bad |= !__builtin_isfinite(src[(int64_t)c * a.elem_stride] * a.polarity);
       }
       if (__ballot(bad) == 0)
-        decode_frame<PREC, METHOD, S, NW, DCN, DVN, true>(code, a, b, wt, tb, eb, rb, sb, lane);
+        decode_frame<PREC, METHOD, S, NW, DCN, DVN, true>(code, a, b, wt, tb, eb, rb, sb, lane,
+                                                           logtab);
       else
-        decode_frame<PREC, METHOD, S, NW, DCN, DVN, false>(code, a, b, wt, tb, eb, rb, sb, lane);
+        decode_frame<PREC, METHOD, S, NW, DCN, DVN, false>(code, a, b, wt, tb, eb, rb, sb, lane,
+                                                            logtab);
     } else {
-      decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane);
+      decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane, logtab);
     }
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(a.ticket, 1u);
@@ -560,6 +564,8 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
   Real *sb = rb + 64 * NW;
   int *fslot = reinterpret_cast<int *>(smem + L.fslot);
   if (blockIdx.x == 0 && tid == 0) *a.ticket_next = 0u;  // next launch's queue head
+  __shared__ fm::LogTabEntry logtab[1 << fm::kLogTabBits];
+  if constexpr (METHOD == 1 && PREC == 0) stage_logtab(logtab);
   if (tid == 0) tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
 
   // this lane's edge, and (every wave) the columns lane + 64 q
@@ -621,7 +627,7 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
         Real T = Real(1);  // ascending column; dummies are exact 1.0 (:506-511)
 #pragma unroll
         for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[k];
-        eb[tid] = Math<PREC>::check_msg(T);  // :513
+        eb[tid] = Math<PREC>::check_msg(T, logtab);  // :513
       } else {
         const int self = sgn(msg);  // :350-376
         int prod = self;

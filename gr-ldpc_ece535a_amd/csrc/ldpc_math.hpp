@@ -24,6 +24,8 @@
 #endif
 #endif
 
+#include "ldpc_logtab.hpp"
+
 namespace ldpc {
 namespace fm {
 
@@ -499,6 +501,45 @@ LDPC_HD double log_ratio_fast(double T) {
   const double dk = (double)k;
   const double r = dk * ln2_hi - ((hfsq - fma_(s, hfsq + R, dk * ln2_lo)) - f);
   return __builtin_fabs(T) == 1.0 ? __builtin_copysign(__builtin_inf(), T) : r;
+}
+
+// log((1+T)/(1-T)) with a table-driven log (tools/gen_logtab.py): the same
+// ratio q as log_ratio_fast, then q = 2^k z, z in [0.6875, 1.375), bucket i
+// from the top 7 bits, r = z invc_i - 1 (|r| < 1/128), log(q) = k ln2 +
+// logc_i + log1p(r) with log1p(r) - r = r^2 (-1/2 + r/3 - ... + r^7/9).  The
+// buckets touching 1.0 use c = 1 (logc = 0, r = z - 1 exact), so results near
+// 0 keep full relative accuracy.  `tab` is the 128-entry table (in LDS on the
+// GPU).  |T| == 1 -> +-inf, NaN -> NaN.
+LDPC_HD double log_ratio_tab(double T, const LogTabEntry *tab) {
+  const double ln2_hi = 6.93147180369123816490e-01;  // 21 trailing zero bits
+  const double ln2_lo = 1.90821492927058770002e-10;
+  const double q = div_fast(1.0 + T, 1.0 - T);
+  uint64_t ix;
+  __builtin_memcpy(&ix, &q, 8);
+  const uint64_t tmp = ix - 0x3FE6000000000000ull;
+  const int i = (int)((tmp >> (52 - kLogTabBits)) & ((1u << kLogTabBits) - 1));
+  const int k = (int)((int64_t)tmp >> 52);
+  const uint64_t iz = ix - (tmp & (0xFFFull << 52));
+  double z;
+  __builtin_memcpy(&z, &iz, 8);
+  const LogTabEntry e = tab[i];
+  const double r = fma_(z, e.invc, -1.0);
+  const double kd = (double)k;
+  const double w = kd * ln2_hi + e.logc;  // kd * ln2_hi is exact
+  const double hi = w + r;
+  const double lo = w - hi + r + kd * ln2_lo;
+  const double r2 = r * r;
+  double p = 1.0 / 9.0;
+  p = fma_(p, r, -1.0 / 8.0);
+  p = fma_(p, r, 1.0 / 7.0);
+  p = fma_(p, r, -1.0 / 6.0);
+  p = fma_(p, r, 1.0 / 5.0);
+  p = fma_(p, r, -1.0 / 4.0);
+  p = fma_(p, r, 1.0 / 3.0);
+  p = fma_(p, r, -0.5);
+  const double y = fma_(r2, p, lo) + hi;
+  const double special = T != T ? T : __builtin_copysign(__builtin_inf(), T);
+  return __builtin_fabs(T) < 1.0 ? y : special;
 }
 
 }  // namespace fm

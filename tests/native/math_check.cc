@@ -89,3 +89,18 @@ void check_pass(int fn, const double *x, int64_t n, int64_t *out) {
   out[0] = mism; out[1] = maxu;
 }
 }
+extern "C" {
+static const ldpc::fm::LogTabEntry kTab[] = {LDPC_LOGTAB_ENTRIES};
+// table-driven log((1+T)/(1-T)) vs glibc.  out[0] mismatches, out[1] max ulp
+void check_logtab(const double *x, int64_t n, int64_t *out) {
+  int64_t mism = 0, maxu = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const double a = ldpc::fm::log_ratio_tab(x[i], kTab);
+    const double b = log((1.0 + x[i]) / (1.0 - x[i]));
+    const int64_t u = ulps(a, b);
+    if (u) ++mism;
+    if (u > maxu) maxu = u;
+  }
+  out[0] = mism; out[1] = maxu;
+}
+}

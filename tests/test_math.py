@@ -105,3 +105,32 @@ def test_check_pass_forms(mc):
     for T in Ts:
         _, maxulp = _run(mc, "check_pass", 1, T)
         assert maxulp <= 3
+
+
+def test_table_log_within_1ulp(mc):
+    """LDPC_PREC_F64's table-driven log((1+T)/(1-T)) (tools/gen_logtab.py):
+    within 1 ulp of glibc over T in [-1, 1], near +-1, near 0 and the edges."""
+    rng = np.random.default_rng(15)
+    Ts = [rng.uniform(-1, 1, 400_000), np.tanh(rng.normal(0, 10, 400_000)),
+          1 - 10.0 ** rng.uniform(-16, 0, 200_000), -1 + 10.0 ** rng.uniform(-16, 0, 200_000),
+          10.0 ** rng.uniform(-300, -1, 200_000),
+          np.array([1.0, -1.0, 0.0, -0.0, np.nan, 0.5, -0.5, 1 - 2.0 ** -53, -1 + 2.0 ** -53])]
+    for T in Ts:
+        x = np.ascontiguousarray(T, np.float64)
+        out = np.zeros(2, np.int64)
+        mc.check_logtab(x.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(x.size),
+                        out.ctypes.data_as(ctypes.c_void_p))
+        assert out[1] <= 1
+
+
+def test_logtab_header_is_generated():
+    """The committed table equals what tools/gen_logtab.py produces."""
+    import importlib.util
+    root = os.path.dirname(HERE)
+    spec = importlib.util.spec_from_file_location("gen_logtab",
+                                                  os.path.join(root, "tools", "gen_logtab.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    hdr = open(os.path.join(root, "gr-ldpc_ece535a_amd", "csrc", "ldpc_logtab.hpp")).read()
+    for invc, logc, _, _ in g.table():
+        assert "{%s, %s}" % (invc.hex(), logc.hex()) in hdr
