@@ -43,8 +43,14 @@
 namespace ldpc {
 namespace {
 
-constexpr int kRowsPerWave = 8;
-constexpr int kColsPerWave = 8;
+#ifndef LDPC_GRAPH_ROWS_PER_WAVE
+#define LDPC_GRAPH_ROWS_PER_WAVE 4
+#endif
+#ifndef LDPC_GRAPH_COLS_PER_WAVE
+#define LDPC_GRAPH_COLS_PER_WAVE 4
+#endif
+constexpr int kRowsPerWave = LDPC_GRAPH_ROWS_PER_WAVE;
+constexpr int kColsPerWave = LDPC_GRAPH_COLS_PER_WAVE;
 
 __device__ __forceinline__ int wave_in_block() {
   return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));

@@ -11,6 +11,14 @@ for p in (REPO, PKG):
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
+# torch before libldpc_hip.so: the process then has one HIP runtime, torch's
+# (INTEGRATION.md section 4); otherwise a test file that loads the library
+# first leaves torch unable to see the GPU.
+try:
+    import torch  # noqa: F401,E402
+except ImportError:  # pragma: no cover
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")

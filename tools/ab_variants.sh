@@ -1,0 +1,30 @@
+#!/bin/bash
+# Builds the working tree's decode library once per variant (extra hipcc
+# defines) into ab/V<i>/ and writes ab/runv.sh, which benches each variant in
+# turn (twice) on the GPU box.
+#   tools/ab_variants.sh "<bench args>" "<defines 1>" "<defines 2>" ...
+set -e
+args=$1; shift
+root=$(cd "$(dirname "$0")/.." && pwd)
+rm -rf "$root/ab" && mkdir -p "$root/ab"
+i=0
+for defs in "$@"; do
+  i=$((i + 1))
+  mkdir -p "$root/ab/V$i"
+  cp -r "$root/gr-ldpc_ece535a_amd/ldpc_ece535a" "$root/ab/V$i/"
+  make -s -j8 -C "$root/gr-ldpc_ece535a_amd" hip OUT="$root/ab/V$i/lib" \
+    HIPFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wall $defs"
+  echo "V$i: $defs" >> "$root/ab/variants.txt"
+done
+cat > "$root/ab/runv.sh" <<EOS
+#!/bin/bash
+cat ab/variants.txt
+for r in 1 2; do
+  for d in ab/V*; do
+    v=\$(basename \$d)
+    LDPC_PKG_DIR=\$PWD/\$d timeout -k 10 200 python bench.py $args > ab/\$v.\$r.json 2> gpurun_out/ab_\$v.\$r.err || { tail -5 gpurun_out/ab_\$v.\$r.err; exit 1; }
+    python3 -c "import json;d=json.load(open('ab/\$v.\$r.json'));print('\$v', \$r, d['value'], d['roofline']['kernel_ms'])"
+  done
+done
+EOS
+echo "built $i variants; run: bash ab/runv.sh"
