@@ -441,8 +441,11 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 // a.waves + ticket++ until the batch is exhausted.  Frames stop after 1..cap
 // iterations, so pulling work keeps every SIMD busy to the end instead of
 // leaving it with a fixed share of the batch.
+#ifndef LDPC_SMALL_MIN_BLOCKS
+#define LDPC_SMALL_MIN_BLOCKS 1
+#endif
 template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
     decode_small_kernel(CodeView code, DecodeArgs a) {
   typedef typename Math<PREC>::Real Real;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -837,7 +840,10 @@ int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int 
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (waves_per_cu <= 0) waves_per_cu = 12;
+#ifndef LDPC_SMALL_WPC
+#define LDPC_SMALL_WPC 12
+#endif
+  if (waves_per_cu <= 0) waves_per_cu = LDPC_SMALL_WPC;
   // schedule: 1 one wave per frame, 2 one workgroup of `slots` waves per
   // frame, 0 auto.  Measured (bench.py --sweep-batch): the workgroup form
   // wins for min-sum until the batch fills the persistent grid several times

@@ -453,20 +453,18 @@ LDPC_HD double log_fast_f64(double q) {
   return (q == __builtin_inf() || q != q) ? q + q : r;
 }
 
-// tanh(m / 2), the sum-product check pass's operand (:509), in the compact
-// two-range form of tanh_fast_f64 evaluated on |m| = 2|x| directly: the same
-// z = min(|m|, 44) / -|m| and therefore the same value as tanh_fast_f64(m/2)
-// for every normal m, without the halving and doubling.  Saturation needs no
-// select (for |m| >= 44, 1 - 2/(expm1(44)+2) rounds to 1.0), NaN propagates,
-// and the sign is copied (tanh(-0) = -0 as in glibc).
+// tanh(m / 2), the sum-product check pass's operand (:509), in one range:
+// t = expm1(-|m|), tanh(|m|/2) = -t / (t + 2).  fdlibm switches to
+// 1 - 2/(expm1(|m|) + 2) above |m| = 2, but for t in (-1, -0.86] both -t and
+// t + 2 are within half an ulp, so the single form stays within 3 ulp of glibc
+// (tests/test_math.py) with no range selects.  |m| is capped at 44 (t rounds
+// to -1 from 38 on, so the result saturates to 1 as tanh does); NaN
+// propagates, and the sign is copied (tanh(-0) = -0 as in glibc).  For
+// |m| < 2 this is exactly tanh_fast_f64(m/2).
 LDPC_HD double tanh_half_fast(double m) {
-  const double a2 = __builtin_fabs(m);
-  const bool big = a2 >= 2.0;
-  const double z = big ? (a2 < 44.0 ? a2 : 44.0) : -a2;
-  const double t = expm1_mid_f64(z);
-  const double q = div_fast(big ? 2.0 : -t, t + 2.0);
-  const double r = big ? 1.0 - q : q;
-  return __builtin_copysign(r, m);
+  const double a = __builtin_fabs(m);
+  const double t = expm1_mid_f64(-(a > 44.0 ? 44.0 : a));
+  return __builtin_copysign(div_fast(-t, t + 2.0), m);
 }
 
 // log((1+T)/(1-T)), the sum-product check message (:513), for T in [-1, 1]
@@ -538,8 +536,8 @@ LDPC_HD double log_ratio_tab(double T, const LogTabEntry *tab) {
   p = fma_(p, r, 1.0 / 3.0);
   p = fma_(p, r, -0.5);
   const double y = fma_(r2, p, lo) + hi;
-  const double special = T != T ? T : __builtin_copysign(__builtin_inf(), T);
-  return __builtin_fabs(T) < 1.0 ? y : special;
+  // |T| == 1 -> T * inf = +-inf; NaN -> NaN
+  return __builtin_fabs(T) < 1.0 ? y : T * __builtin_inf();
 }
 
 }  // namespace fm
