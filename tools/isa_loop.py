@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Instruction mix of a kernel's largest loop in a hipcc --save-temps .s file:
-tools/isa_loop.py <file.s> <kernel-name-regex>..."""
+tools/isa_loop.py <file.s> <kernel-name-regex>...
+ISA_LOOP_RANK=k picks the k-th largest innermost loop instead (a kernel that
+inlines two variants of its iteration loop, e.g. decode_small_kernel's
+finite / non-finite sum-product forms, has one loop per variant)."""
 import collections
+import os
 import re
 import sys
 
@@ -27,7 +31,9 @@ def loop_mix(s, pat):
         return sum(1 for l in lines[a:b] if l.startswith("v_"))
     inner = [(a, b) for a, b in loops
              if not any((a2 > a or b2 < b) and a <= a2 and b2 <= b for a2, b2 in loops)]
-    a, b = max(inner, key=lambda ab: work(*ab))
+    inner.sort(key=lambda ab: -work(*ab))
+    rank = int(os.environ.get("ISA_LOOP_RANK", "0"))  # 1: the second-largest loop, ...
+    a, b = inner[min(rank, len(inner) - 1)]
     ins = [l.split()[0] for l in lines[a:b]
            if l and not l.startswith((".", ";", "s_nop")) and not re.match(r"^\S+:", l)]
     return m.group(1), collections.Counter(ins)
