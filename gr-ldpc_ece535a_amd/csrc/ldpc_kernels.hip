@@ -162,6 +162,15 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
   for (int q = 0; q < NW; ++q) hard[q] = 0;
   int weight = 0, used = 0;
+  // lanes holding a real column / row of each 64-wide slot (wave-uniform):
+  // ballots of a compare are masked with these instead of folding the range
+  // test into the predicate (that form costs two extra VALU per ballot)
+  uint64_t col_ok[NW], row_ok[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    col_ok[q] = __ballot(lane + 64 * q < N);
+    row_ok[q] = __ballot(lane + 64 * q < M);
+  }
 
   auto syndrome = [&]() {
     int w = 0;
@@ -170,7 +179,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       int odd = 0;
 #pragma unroll
       for (int k = 0; k < NW; ++k) odd ^= __popcll(wt.rowmask[q][k] & hard[k]);
-      w += __popcll(__ballot((odd & 1) != 0 && lane + 64 * q < M));
+      w += __popcll(__builtin_amdgcn_ballot_w64((odd & 1) != 0) & row_ok[q]);
     }
     return w;
   };
@@ -321,7 +330,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           bit = LQ < Real(0);
           post[q] = LQ;
         }
-        hard[q] = __ballot(bit && c < N);
+        hard[q] = __builtin_amdgcn_ballot_w64(bit) & col_ok[q];
       }
       if constexpr (METHOD == 1) {
         // keep the variable pass's gathers above the exit test (the compiler
@@ -441,6 +450,13 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 // a.waves + ticket++ until the batch is exhausted.  Frames stop after 1..cap
 // iterations, so pulling work keeps every SIMD busy to the end instead of
 // leaving it with a fixed share of the batch.
+#ifdef LDPC_TIMELINE
+// Diagnostic builds only (tools/timeline.py): per frame the 100 MHz realtime
+// clock at its start and end and the wave's hardware ids.
+constexpr int kTimelineFrames = 65536;
+__device__ uint64_t g_timeline[4 * kTimelineFrames];
+#endif
+
 #ifndef LDPC_SMALL_MIN_BLOCKS
 #define LDPC_SMALL_MIN_BLOCKS 1
 #endif
@@ -507,6 +523,9 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
   }
 
   while (b < a.B) {
+#ifdef LDPC_TIMELINE
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     if constexpr (METHOD == 1) {
       bool bad = false;
       const float *src = a.in + b * a.cw_stride;
@@ -524,6 +543,14 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
     } else {
       decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane, logtab);
     }
+#ifdef LDPC_TIMELINE
+    if (lane == 0 && b < kTimelineFrames) {
+      g_timeline[4 * b] = t_start;
+      g_timeline[4 * b + 1] = __builtin_amdgcn_s_memrealtime();
+      g_timeline[4 * b + 2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      g_timeline[4 * b + 3] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    }
+#endif
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(a.ticket, 1u);
     b = (int64_t)a.waves + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
@@ -864,3 +891,13 @@ int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int 
 }
 
 }  // namespace ldpc
+
+#ifdef LDPC_TIMELINE
+extern "C" int ldpc_debug_timeline(uint64_t *host, int frames) {
+  if (frames > ldpc::kTimelineFrames) frames = ldpc::kTimelineFrames;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ldpc::g_timeline), sizeof(uint64_t) * 4 * frames) ==
+                 hipSuccess
+             ? frames
+             : -1;
+}
+#endif

@@ -517,12 +517,15 @@ LDPC_HD double log_ratio_tab(double T, const LogTabEntry *tab) {
   // bucket, exponent and reduced argument from the high word alone (32-bit ops)
   const uint32_t hx = (uint32_t)(ix >> 32);
   const uint32_t th = hx - 0x3FE60000u;
-  const int i = (int)((th >> (20 - kLogTabBits)) & ((1u << kLogTabBits) - 1));
+  // byte offset of bucket (th >> 13) & 127 in one shift and one mask
+  const uint32_t off = (th >> (20 - kLogTabBits - 4)) & (((1u << kLogTabBits) - 1) << 4);
   const int k = (int)th >> 20;
   const uint64_t iz = ((uint64_t)(hx - (th & 0xFFF00000u)) << 32) | (ix & 0xFFFFFFFFull);
   double z;
   __builtin_memcpy(&z, &iz, 8);
-  const LogTabEntry e = tab[i];
+  static_assert(sizeof(LogTabEntry) == 16, "table entries are 16 bytes");
+  const LogTabEntry e = *reinterpret_cast<const LogTabEntry *>(
+      reinterpret_cast<const char *>(tab) + off);
   const double r = fma_(z, e.invc, -1.0);
   const double kd = (double)k;
   const double w = fma_(kd, ln2_hi, e.logc);  // kd * ln2_hi is exact
