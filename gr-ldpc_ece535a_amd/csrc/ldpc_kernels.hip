@@ -83,6 +83,11 @@ __device__ __forceinline__ T lds_ld(uint32_t addr) {
   return *(lds_ptr)(uintptr_t)addr;
 }
 template <typename T>
+__device__ __forceinline__ void lds_st(uint32_t addr, T v) {
+  typedef __attribute__((address_space(3))) T *lds_ptr;
+  *(lds_ptr)(uintptr_t)addr = v;
+}
+template <typename T>
 __device__ __forceinline__ uint32_t lds_addr(const T *p) {
   typedef const __attribute__((address_space(3))) T *lds_ptr;
   return (uint32_t)(uintptr_t)(lds_ptr)p;  // generic -> LDS address-space cast
@@ -184,7 +189,111 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
     return w;
   };
 
-  if constexpr (METHOD == 1 || METHOD == 0) {
+#ifdef LDPC_NO_COLS
+  constexpr bool kCols = false;
+#else
+  // column-centric sum-product when it computes no more tanh calls than the
+  // edge-centric form (64 NW DVN <= 64 S; the reference's H: 192 = 192)
+  constexpr bool kCols = METHOD == 1 && NW == 1 && DVN <= S;
+#endif
+  if constexpr (kCols) {
+    // Column-centric sum-product.  A column lane has all of its column's
+    // check messages after one gather, so it computes the posterior
+    // (:519-532) and, after the exit test, every bit message of its column,
+    // M(j,i) = sum_{k != j} (E(k,i) + r(i)) in ascending k from +0.0
+    // (:540-553) -- the same additions in the same order as the edge form --
+    // and scatters tanh(M(j,i)/2) to the edges' tb slots.  The edge lanes
+    // then only gather row neighbours.  Saves the edge form's per-edge
+    // column gathers and repeated (E + r) sums.
+    const uint32_t eb_dummy = lds_addr(eb + kDummy);
+    const uint32_t junk = lds_addr(tb + kDummy + 1);  // stores of missing edges
+    constexpr uint32_t kTbEb = (64 * S + 2) * sizeof(Real);  // eb - tb in bytes
+    if (lane == 0) tb[kDummy] = Real(1);  // product identity (missing row neighbours)
+    uint32_t ra[S][DCN], ea[NW][DVN], ta[NW][DVN];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int k = 0; k < DCN; ++k) ra[s][k] = (uint32_t)field(wt.rn[s], k);
+    Real *nr = sb + 64 * NW;  // FIN: -r of the lane's column (missing edges' term)
+#pragma unroll
+    for (int q = 0; q < NW; ++q)
+#pragma unroll
+      for (int k = 0; k < DVN; ++k) {
+        const uint32_t e = (uint32_t)field(wt.ce[q], k);
+        ta[q][k] = e == eb_dummy ? junk : e - kTbEb;
+        ea[q][k] = (FIN && e == eb_dummy) ? lds_addr(nr + lane + 64 * q) : e;
+      }
+    Real rc[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      rc[q] = rb[lane + 64 * q];  // written by this lane above
+      if constexpr (FIN) nr[lane + 64 * q] = -rc[q];
+      // initial bit messages M(j,i) = r(i) (:489-496)
+      const Real t0 = Math<PREC>::tanh_half(rc[q]);
+#pragma unroll
+      for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], t0);
+    }
+    for (int h = 0; h < a.max_iters; ++h) {
+      wave_lds_sync();  // tb complete
+      Real nb[S][DCN];
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int k = 0; k < DCN; ++k) nb[s][k] = lds_ld<Real>(ra[s][k]);
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int k = 0; k < DCN; ++k) asm volatile("" ::"v"(nb[s][k]));
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        // T = prod_{k != i} tanh(M(j,k)/2), ascending k; E = log((1+T)/(1-T))
+        // (:506-513).  Padding neighbours read the 1.0 dummy: exact no-op.
+        Real T = Real(1);
+#pragma unroll
+        for (int k = 0; k < DCN; ++k) T = T * nb[s][k];
+        eb[lane + 64 * s] = Math<PREC>::check_msg(T, logtab);
+      }
+      wave_lds_sync();  // eb complete
+      Real tv[NW][DVN];
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        Real ev[DVN];
+#pragma unroll
+        for (int k = 0; k < DVN; ++k) ev[k] = lds_ld<Real>(ea[q][k]);
+        // L = sum_j (E(j,i) + r(i)), ascending j; 1 iff L <= 0 (:519-532)
+        Real acc = Real(0);
+#pragma unroll
+        for (int k = 0; k < DVN; ++k) {
+          tv[q][k] = ev[k] + rc[q];
+          if constexpr (FIN)
+            acc = acc + tv[q][k];  // a missing edge's term is exactly +0.0
+          else
+            acc = ea[q][k] != eb_dummy ? acc + tv[q][k] : acc;
+        }
+        post[q] = acc;
+        hard[q] = __builtin_amdgcn_ballot_w64(acc <= Real(0)) & col_ok[q];
+      }
+      weight = syndrome();
+      used = h + 1;
+      if (h + 1 == a.max_iters) break;
+      if ((h + 1) % a.et_period == 0 && weight == 0) break;
+#pragma unroll
+      for (int q = 0; q < NW; ++q)
+#pragma unroll
+        for (int k = 0; k < DVN; ++k) {
+          Real m = Real(0);
+#pragma unroll
+          for (int k2 = 0; k2 < DVN; ++k2) {
+            if (k2 == k) continue;
+            if constexpr (FIN)
+              m = m + tv[q][k2];
+            else
+              m = ea[q][k2] != eb_dummy ? m + tv[q][k2] : m;
+          }
+          lds_st<Real>(ta[q][k], Math<PREC>::tanh_half(m));  // :509
+        }
+    }
+  } else if constexpr (METHOD == 1 || METHOD == 0) {
     // the tables were relocated to LDS byte addresses (decode_small_kernel):
     // rn -> tb, cn / ce -> eb, rn field 7 -> rb (sb = rb + 64 NW elements);
     // missing neighbours point at the dummy elements tb[64S] (1.0 for the
