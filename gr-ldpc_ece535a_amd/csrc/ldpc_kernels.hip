@@ -147,20 +147,18 @@ template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = k
 __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeArgs &a,
                                              const int64_t b, WaveTables<S, NW> &wt,
                                              Real *tb, Real *eb, Real *rb, Real *sb,
-                                             const int lane, const fm::LogTabEntry *logtab) {
+                                             const int lane, const fm::LogTabEntry *logtab,
+                                             const float (&xin)[NW]) {
   const int M = code.M, N = code.N;
   constexpr int kDummy = 64 * S;  // index of the per-wave identity element
-  // Channel samples: tx = Re(in) * polarity (:149-153); r = -tx (:486,
-  // :318-321).  Lane l reads sample l of each 64-column slot (coalesced).
-  const float *src = a.in + b * a.cw_stride;
+  // Channel samples xin = tx = Re(in) * polarity (:149-153, loaded by the
+  // caller, 0 past N); r = -tx (:486, :318-321).
   Real post[NW];
 #pragma unroll
   for (int q = 0; q < NW; ++q) {
     const int c = lane + 64 * q;
-    float x = 0.0f;
-    if (c < N) x = src[(int64_t)c * a.elem_stride] * a.polarity;
-    rb[c] = -(Real)x;
-    post[q] = (Real)x;
+    rb[c] = -(Real)xin[q];
+    post[q] = (Real)xin[q];
   }
 
   uint64_t hard[NW];
@@ -631,27 +629,56 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
     for (int q = 0; q < NW; ++q) relocate(wt.ce[q], DVN, lds_addr(eb), R, kDummy);
   }
 
+#ifndef LDPC_NO_PREFETCH
+  // pull the samples of the frames the ticket queue hands out later into L2
+  // (one frame per resident wave); the values are consumed by an empty asm
+  // after the first frame, when the loads have long completed
+  float pf[NW];
+  {
+    const int64_t pb = (int64_t)a.waves + b;
+    const float *ps = a.in + (pb < a.B ? pb : b) * a.cw_stride;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int c = lane + 64 * q;
+      pf[q] = c < code.N ? ps[(int64_t)c * a.elem_stride] : 0.0f;
+    }
+  }
+  bool first = true;
+#endif
   while (b < a.B) {
 #ifdef LDPC_TIMELINE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
+    // the frame's channel samples, one load per lane and 64-column slot
+    // (coalesced); the samples past N are 0
+    float xin[NW];
+    const float *src = a.in + b * a.cw_stride;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int c = lane + 64 * q;
+      xin[q] = c < code.N ? src[(int64_t)c * a.elem_stride] * a.polarity : 0.0f;
+    }
     if constexpr (METHOD == 1) {
       bool bad = false;
-      const float *src = a.in + b * a.cw_stride;
 #pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        const int c = lane + 64 * q;
-        if (c < code.N) bad |= !__builtin_isfinite(src[(int64_t)c * a.elem_stride] * a.polarity);
-      }
+      for (int q = 0; q < NW; ++q) bad |= !__builtin_isfinite(xin[q]);
       if (__ballot(bad) == 0)
         decode_frame<PREC, METHOD, S, NW, DCN, DVN, true>(code, a, b, wt, tb, eb, rb, sb, lane,
-                                                           logtab);
+                                                           logtab, xin);
       else
         decode_frame<PREC, METHOD, S, NW, DCN, DVN, false>(code, a, b, wt, tb, eb, rb, sb, lane,
-                                                            logtab);
+                                                            logtab, xin);
     } else {
-      decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane, logtab);
+      decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane, logtab,
+                                                  xin);
     }
+#ifndef LDPC_NO_PREFETCH
+    if (first) {
+#pragma unroll
+      for (int q = 0; q < NW; ++q) asm volatile("" ::"v"(pf[q]));
+      first = false;
+    }
+#endif
 #ifdef LDPC_TIMELINE
     if (lane == 0 && b < kTimelineFrames) {
       g_timeline[4 * b] = t_start;
