@@ -21,7 +21,10 @@ roofline.achieved uses SURVEY.md 8(d)'s algorithmic byte model per launch:
          + iters_b * (32E + 10N)]  (f64 parity mode; 16E + 6N for f32)
 divided by the kernel's mean duration: one HIP event pair on the launch
 stream around the K timed launches, divided by K.  roofline.traffic is the rocprofv3 PMC measurement
-(profiles/) per launch, when a matching entry exists.
+(profiles/) per launch, when a matching entry exists.  roofline_valu: the
+bound that actually applies to the small-code kernel (messages never leave
+LDS/VGPRs): PMC VALU wave-instructions per launch / kernel time against the
+1024-SIMD issue peak.
 cpu_baseline: the C oracle (oracle/, a dense double restatement of the
 reference decoder) decoding the same frames on the host's cores.
 """
@@ -330,12 +333,14 @@ def main():
     alg_bytes = float(B * (4 * N + dec.KB + 8) + iters_b.sum() * bytes_per_iter(E, N, prec))
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
+    pmc = None
     workload_key = "%s%d_%s_b%d_i%d_db%g" % ("dvb" if dvb else "sp", args.method, args.precision, B,
                                             args.iters, args.ebn0)
     try:
         tj = json.load(open(args.traffic_json))
         if workload_key in tj:
             traffic = tj[workload_key]["hbm_bytes_per_launch"]
+            pmc = tj[workload_key].get("pmc")
     except (OSError, ValueError, KeyError):
         pass
 
@@ -382,6 +387,21 @@ def main():
             "model": "SURVEY 8(d) algorithmic bytes per launch = %d" % int(alg_bytes),
         },
     }
+    if pmc and "SQ_INSTS_VALU" in pmc and not dvb:
+        # The small-code kernel keeps every message in LDS / VGPRs (traffic is
+        # ~0.2 % of the byte model), so HBM does not bound it: VALU issue does.
+        # achieved = PMC VALU wave-instructions per launch (profiles/) / the
+        # live kernel time; peak = 1024 SIMDs x 2.4 GHz / 4 cycles per wave64
+        # VALU instruction (f64 FMA is full rate on gfx950).
+        valu_peak = 256 * 4 * 2.4e9 / 4 / 1e9
+        valu_ach = pmc["SQ_INSTS_VALU"] / (kern_ms * 1e-3) / 1e9
+        line["roofline_valu"] = {
+            "bound": "valu", "achieved": round(valu_ach, 1), "peak": valu_peak,
+            "unit": "G wave-instr/s", "frac": round(valu_ach / valu_peak, 4),
+            "f64_fma_per_launch": pmc.get("SQ_INSTS_VALU_FMA_F64"),
+            "effective_clock_ghz": round(pmc["GRBM_GUI_ACTIVE"] / 8 / (kern_ms * 1e-3) / 1e9, 3)
+            if "GRBM_GUI_ACTIVE" in pmc else None,
+            "source": "SQ_INSTS_VALU per launch from the rocprofv3 PMC pass (profiles/pmc_traffic.json)"}
 
     # ---- variants measured in the same process (not the headline) ----------
     variant_outs = {}

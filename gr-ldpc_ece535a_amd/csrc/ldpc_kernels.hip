@@ -231,7 +231,34 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
       for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], t0);
     }
+#ifdef LDPC_FAIR_T3
+    uint64_t t_prev = __builtin_amdgcn_s_memtime();
+#endif
     for (int h = 0; h < a.max_iters; ++h) {
+#ifdef LDPC_FAIR_T3
+      {
+        // experiment: a wave whose last iteration was slow (starved by the
+        // older waves of its SIMD) issues first for the next one
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        const uint32_t d = (uint32_t)(now - t_prev);
+        t_prev = now;
+        if (d > LDPC_FAIR_T3)
+          __builtin_amdgcn_s_setprio(3);
+        else if (d > LDPC_FAIR_T2)
+          __builtin_amdgcn_s_setprio(2);
+        else if (d > LDPC_FAIR_T1)
+          __builtin_amdgcn_s_setprio(1);
+        else
+          __builtin_amdgcn_s_setprio(0);
+      }
+#endif
+#ifdef LDPC_PRIO_STEP
+      // experiment: frame-age priority (older frames issue first)
+      if (h == 0) __builtin_amdgcn_s_setprio(LDPC_PRIO_BASE);
+      if (h == LDPC_PRIO_STEP) __builtin_amdgcn_s_setprio(LDPC_PRIO_BASE + LDPC_PRIO_DIR);
+      if (h == 2 * LDPC_PRIO_STEP) __builtin_amdgcn_s_setprio(LDPC_PRIO_BASE + 2 * LDPC_PRIO_DIR);
+      if (h == 3 * LDPC_PRIO_STEP) __builtin_amdgcn_s_setprio(LDPC_PRIO_BASE + 3 * LDPC_PRIO_DIR);
+#endif
       wave_lds_sync();  // tb complete
       Real nb[S][DCN];
 #pragma unroll
@@ -659,6 +686,7 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
   while (b < a.B) {
 #ifdef LDPC_TIMELINE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    const uint64_t c_start = __builtin_amdgcn_s_memtime();
 #endif
     // the frame's channel samples, one load per lane and 64-column slot
     // (coalesced); the samples past N are 0
@@ -694,8 +722,9 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
     if (lane == 0 && b < kTimelineFrames) {
       g_timeline[4 * b] = t_start;
       g_timeline[4 * b + 1] = __builtin_amdgcn_s_memrealtime();
-      g_timeline[4 * b + 2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-      g_timeline[4 * b + 3] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+      g_timeline[4 * b + 2] = (uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |  // HW_ID
+                              ((uint64_t)(uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);  // XCC_ID
+      g_timeline[4 * b + 3] = __builtin_amdgcn_s_memtime() - c_start;  // core clocks
     }
 #endif
     uint32_t t = 0;

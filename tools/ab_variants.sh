@@ -19,11 +19,13 @@ done
 cat > "$root/ab/runv.sh" <<EOS
 #!/bin/bash
 cat ab/variants.txt
+mkdir -p ab/out
 for r in 1 2; do
-  for d in ab/V*; do
+  for d in ab/V[0-9]*/; do
+    d=\${d%/}
     v=\$(basename \$d)
-    LDPC_PKG_DIR=\$PWD/\$d timeout -k 10 200 python bench.py $args > ab/\$v.\$r.json 2> gpurun_out/ab_\$v.\$r.err || { tail -5 gpurun_out/ab_\$v.\$r.err; exit 1; }
-    python3 -c "import json;d=json.load(open('ab/\$v.\$r.json'));print('\$v', \$r, d['value'], d['roofline']['kernel_ms'])"
+    LDPC_PKG_DIR=\$PWD/\$d timeout -k 10 200 python bench.py $args > ab/out/\$v.\$r.json 2> gpurun_out/ab_\$v.\$r.err || { tail -5 gpurun_out/ab_\$v.\$r.err; exit 1; }
+    python3 -c "import json;d=json.load(open('ab/out/\$v.\$r.json'));print('\$v', \$r, d['value'], d['roofline']['kernel_ms'])"
   done
 done
 EOS

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--precision", type=int, default=0)
     ap.add_argument("--method", type=int, default=1)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--et", type=int, default=1, help="syndrome check period (50: every frame runs 50)")
     a = ap.parse_args()
     import torch  # first: one HIP runtime
     import bench  # noqa: E402  (sets sys.path from LDPC_PKG_DIR)
@@ -40,7 +41,7 @@ def main():
     dec = L.Decoder()
     y, _ = bench.synth(dec.H, a.batch, a.ebn0, 2024)
     d_in = torch.from_numpy(y).cuda()
-    _, kern_ms, iters, _ = bench.time_decoder(dec, torch, d_in, a.batch, a.method, 50, 1,
+    _, kern_ms, iters, _ = bench.time_decoder(dec, torch, d_in, a.batch, a.method, 50, a.et,
                                               a.precision, 3, 2)
     torch.cuda.synchronize()
     B = a.batch
@@ -51,8 +52,9 @@ def main():
     t = buf.reshape(B, 4)
     start = (t[:, 0] - t[:, 0].min()).astype(np.float64) / 100.0  # us
     end = (t[:, 1] - t[:, 0].min()).astype(np.float64) / 100.0
-    hw = t[:, 2].astype(np.int64)
-    xcc = t[:, 3].astype(np.int64) & 0xF
+    hw = (t[:, 2] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    xcc = (t[:, 2] >> np.uint64(32)).astype(np.int64) & 0xF
+    clk = t[:, 3].astype(np.float64) / np.maximum(end - start, 1e-3) / 1e3  # GHz
     simd = (hw >> 4) & 3
     cu = (hw >> 8) & 15
     sh = (hw >> 12) & 1
@@ -96,8 +98,10 @@ def main():
     for i in late:
         print("  frame %4d simd %5d start %.1f end %.1f iters %d conc %.2f" %
               (i, key[i], start[i], end[i], iters[i], conc_at_frame[i]))
+    print("in-kernel clock GHz (per frame): median %.3f p5 %.3f p95 %.3f" %
+          (np.median(clk), np.percentile(clk, 5), np.percentile(clk, 95)))
     if a.json:
-        json.dump({"start_us": start.tolist(), "end_us": end.tolist(), "simd": key.tolist(),
+        json.dump({"clk_ghz": clk.tolist(), "start_us": start.tolist(), "end_us": end.tolist(), "simd": key.tolist(),
                    "iters": iters.tolist()}, open(a.json, "w"))
 
 
