@@ -52,6 +52,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 #endif
 }
 
+#ifndef LDPC_FAIR_CYCLES
+#define LDPC_FAIR_CYCLES 2200  // ~1.1 us at the ~2 GHz the chip holds under this load
+#endif
+
 template <int NW>
 __device__ __forceinline__ uint64_t word_at(const uint64_t (&w)[NW], int idx) {
   uint64_t r = w[0];
@@ -231,33 +235,27 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
       for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], t0);
     }
-#ifdef LDPC_FAIR_T3
+#ifndef LDPC_NO_FAIR
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
     for (int h = 0; h < a.max_iters; ++h) {
-#ifdef LDPC_FAIR_T3
+#ifndef LDPC_NO_FAIR
       {
-        // experiment: a wave whose last iteration was slow (starved by the
-        // older waves of its SIMD) issues first for the next one
+        // Issue priority for starved waves.  A SIMD's waves issue oldest
+        // first, and two waves already keep its VALU busy, so the third wave
+        // of a SIMD crawls (1.7-2 us per iteration against ~1 us) and a long
+        // frame it holds ends the batch.  A wave whose last iteration took
+        // more than LDPC_FAIR_CYCLES core clocks issues first for the next
+        // one (same-box A/B on the headline: -2.6 %).  Scheduling only: the
+        // arithmetic is untouched.
         const uint64_t now = __builtin_amdgcn_s_memtime();
         const uint32_t d = (uint32_t)(now - t_prev);
         t_prev = now;
-        if (d > LDPC_FAIR_T3)
+        if (d > LDPC_FAIR_CYCLES)
           __builtin_amdgcn_s_setprio(3);
-        else if (d > LDPC_FAIR_T2)
-          __builtin_amdgcn_s_setprio(2);
-        else if (d > LDPC_FAIR_T1)
-          __builtin_amdgcn_s_setprio(1);
         else
           __builtin_amdgcn_s_setprio(0);
       }
-#endif
-#ifdef LDPC_PRIO_STEP
-      // experiment: frame-age priority (older frames issue first)
-      if (h == 0) __builtin_amdgcn_s_setprio(LDPC_PRIO_BASE);
-      if (h == LDPC_PRIO_STEP) __builtin_amdgcn_s_setprio(LDPC_PRIO_BASE + LDPC_PRIO_DIR);
-      if (h == 2 * LDPC_PRIO_STEP) __builtin_amdgcn_s_setprio(LDPC_PRIO_BASE + 2 * LDPC_PRIO_DIR);
-      if (h == 3 * LDPC_PRIO_STEP) __builtin_amdgcn_s_setprio(LDPC_PRIO_BASE + 3 * LDPC_PRIO_DIR);
 #endif
       wave_lds_sync();  // tb complete
       Real nb[S][DCN];

@@ -503,10 +503,10 @@ LDPC_HD double log_ratio_fast(double T) {
 
 // log((1+T)/(1-T)) with a table-driven log (tools/gen_logtab.py): the same
 // ratio q as log_ratio_fast, then q = 2^k z, z in [0.6875, 1.375), bucket i
-// from the top 7 bits, r = z invc_i - 1 (|r| < 1/128), log(q) = k ln2 +
-// logc_i + log1p(r) with log1p(r) - r = r^2 (-1/2 + r/3 - ... - r^6/8).  The
+// from the top 9 bits, r = z invc_i - 1 (|r| < 1/512), log(q) = k ln2 +
+// logc_i + log1p(r) with log1p(r) - r = r^2 (-1/2 + r/3 - ... - r^4/6).  The
 // buckets touching 1.0 use c = 1 (logc = 0, r = z - 1 exact), so results near
-// 0 keep full relative accuracy.  `tab` is the 128-entry table (in LDS on the
+// 0 keep full relative accuracy.  `tab` is the 512-entry table (in LDS on the
 // GPU).  |T| == 1 -> +-inf, NaN -> NaN.
 LDPC_HD double log_ratio_tab(double T, const LogTabEntry *tab) {
   const double ln2_hi = 6.93147180369123816490e-01;  // 21 trailing zero bits
@@ -517,7 +517,7 @@ LDPC_HD double log_ratio_tab(double T, const LogTabEntry *tab) {
   // bucket, exponent and reduced argument from the high word alone (32-bit ops)
   const uint32_t hx = (uint32_t)(ix >> 32);
   const uint32_t th = hx - 0x3FE60000u;
-  // byte offset of bucket (th >> 13) & 127 in one shift and one mask
+  // byte offset of bucket (th >> (20 - kLogTabBits)) % 2^kLogTabBits in one shift and one mask
   const uint32_t off = (th >> (20 - kLogTabBits - 4)) & (((1u << kLogTabBits) - 1) << 4);
   const int k = (int)th >> 20;
   const uint64_t iz = ((uint64_t)(hx - (th & 0xFFF00000u)) << 32) | (ix & 0xFFFFFFFFull);
@@ -532,10 +532,9 @@ LDPC_HD double log_ratio_tab(double T, const LogTabEntry *tab) {
   const double hi = w + r;
   const double lo = fma_(kd, ln2_lo, w - hi + r);
   const double r2 = r * r;
-  // log1p(r) - r for |r| <= 2^-7: the r^9 term is below 2^-59 relative
-  double p = -1.0 / 8.0;
-  p = fma_(p, r, 1.0 / 7.0);
-  p = fma_(p, r, -1.0 / 6.0);
+  // log1p(r) - r for |r| < 2^-9 (512 buckets): the r^7 term is below 2^-65
+  static_assert(kLogTabBits == 9, "the series length assumes 512 buckets");
+  double p = -1.0 / 6.0;
   p = fma_(p, r, 1.0 / 5.0);
   p = fma_(p, r, -1.0 / 4.0);
   p = fma_(p, r, 1.0 / 3.0);

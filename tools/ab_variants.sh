@@ -3,6 +3,7 @@
 # defines) into ab/V<i>/ and writes ab/runv.sh, which benches each variant in
 # turn (twice) on the GPU box.
 #   tools/ab_variants.sh "<bench args>" "<defines 1>" "<defines 2>" ...
+# A variant "@<git rev>" builds that revision instead (e.g. "@HEAD").
 set -e
 args=$1; shift
 root=$(cd "$(dirname "$0")/.." && pwd)
@@ -11,9 +12,18 @@ i=0
 for defs in "$@"; do
   i=$((i + 1))
   mkdir -p "$root/ab/V$i"
-  cp -r "$root/gr-ldpc_ece535a_amd/ldpc_ece535a" "$root/ab/V$i/"
-  make -s -j8 -C "$root/gr-ldpc_ece535a_amd" hip OUT="$root/ab/V$i/lib" \
-    HIPFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wall $defs"
+  src="$root/gr-ldpc_ece535a_amd"
+  if [[ "$defs" == @* ]]; then  # "@<git rev>": that revision's library, default flags
+    rm -rf /tmp/ab_wt && git -C "$root" worktree add -f /tmp/ab_wt "${defs#@}" > /dev/null
+    src=/tmp/ab_wt/gr-ldpc_ece535a_amd
+    cp -r "$src/ldpc_ece535a" "$root/ab/V$i/"
+    make -s -j8 -C "$src" hip OUT="$root/ab/V$i/lib"
+    git -C "$root" worktree remove --force /tmp/ab_wt
+  else
+    cp -r "$src/ldpc_ece535a" "$root/ab/V$i/"
+    make -s -j8 -C "$src" hip OUT="$root/ab/V$i/lib" \
+      HIPFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wall $defs"
+  fi
   echo "V$i: $defs" >> "$root/ab/variants.txt"
 done
 cat > "$root/ab/runv.sh" <<EOS
