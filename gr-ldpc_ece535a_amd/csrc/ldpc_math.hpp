@@ -387,7 +387,11 @@ LDPC_HD double expm1_mid_f64(double z) {
   const double log2e = 1.4426950408889634;
   const double ln2_hi = 6.93147180369123816490e-01;  // low 21 bits zero
   const double ln2_lo = 1.90821492927058770002e-10;
-  const double n = rint_(z * log2e);
+  // n = round(z log2e) by the shifter: the fma rounds the exact product once
+  // and leaves n in the low word, so 2^n needs no float->int conversion
+  const double shifter = 0x1.8p52;
+  const double nd = fma_(z, log2e, shifter);
+  const double n = nd - shifter;
   double r = fma_(-n, ln2_hi, z);
   r = fma_(-n, ln2_lo, r);
   double p = 0x1.af4de76a90952p-26;
@@ -401,7 +405,7 @@ LDPC_HD double expm1_mid_f64(double z) {
   p = fma_(p, r, 0x1.5555555555557p-3);
   p = fma_(p, r, 0x1.0000000000001p-1);
   const double em = fma_(r * r, p, r);  // expm1(r)
-  const double s = ldexp_(1.0, (int)n);  // 2^n, exact
+  const double s = ldexp_(1.0, (int)lo_word(nd));  // 2^n, exact
   return fma_(s, em, s - 1.0);
 }
 
