@@ -385,6 +385,9 @@ def main():
             "traffic": traffic,
             "kernel_ms": round(kern_ms, 5),
             "model": "SURVEY 8(d) algorithmic bytes per launch = %d" % int(alg_bytes),
+            "label": ("equivalent streaming bandwidth: the small-code kernel keeps every message "
+                      "in LDS/VGPRs (traffic = measured HBM bytes per launch); roofline_valu is "
+                      "the bound that applies") if not dvb else "HBM-resident messages",
         },
     }
     if pmc and "SQ_INSTS_VALU" in pmc and not dvb:
@@ -399,8 +402,6 @@ def main():
             "bound": "valu", "achieved": round(valu_ach, 1), "peak": valu_peak,
             "unit": "G wave-instr/s", "frac": round(valu_ach / valu_peak, 4),
             "f64_fma_per_launch": pmc.get("SQ_INSTS_VALU_FMA_F64"),
-            "effective_clock_ghz": round(pmc["GRBM_GUI_ACTIVE"] / 8 / (kern_ms * 1e-3) / 1e9, 3)
-            if "GRBM_GUI_ACTIVE" in pmc else None,
             "source": "SQ_INSTS_VALU per launch from the rocprofv3 PMC pass (profiles/pmc_traffic.json)"}
 
     # ---- variants measured in the same process (not the headline) ----------

@@ -19,7 +19,7 @@ namespace ldpc {
 //   2 F64_LIBM  double, fdlibm tanh bit-identical to glibc's, fdlibm log
 template <int PREC>
 struct Math;
-// The 128-entry log table of LDPC_PREC_F64's check message (ldpc_logtab.hpp);
+// The 512-entry log table of LDPC_PREC_F64's check message (ldpc_logtab.hpp);
 // kernels stage it in LDS (stage_logtab) and pass that copy to check_msg.
 __device__ const fm::LogTabEntry kLogTab[1 << fm::kLogTabBits] = {LDPC_LOGTAB_ENTRIES};
 
