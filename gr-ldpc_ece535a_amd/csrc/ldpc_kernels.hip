@@ -1046,12 +1046,11 @@ int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int 
 #endif
   if (waves_per_cu <= 0) waves_per_cu = LDPC_SMALL_WPC;
   // schedule: 1 one wave per frame, 2 one workgroup of `slots` waves per
-  // frame, 0 auto.  Measured (bench.py --sweep-batch): the workgroup form
-  // wins for min-sum until the batch fills the persistent grid several times
-  // over; sum-product's long per-edge chains keep the one-wave form ahead.
-  bool mw = schedule == 2;
-  if (schedule == 0)
-    mw = method == 0 && slots > 1 && (int64_t)a.B <= (int64_t)4 * waves_per_cu * cus;
+  // frame, 0 auto = 1.  Measured (bench.py --sweep-batch,
+  // profiles/round1/schedules_sweep.txt): the one-wave form is as fast as the
+  // workgroup form for every method at B = 16..256 and faster from B = 1024
+  // on (min-sum f64 at B = 4096: 0.0718 vs 0.0807 ms).
+  const bool mw = schedule == 2;
   if (mw) {
     const int64_t frames_in_flight = std::max<int64_t>(1, (int64_t)waves_per_cu * cus / slots);
     a.waves = (int)std::min<int64_t>((int64_t)a.B, frames_in_flight);

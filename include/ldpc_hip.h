@@ -177,9 +177,9 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
  * Frames are pulled from a per-launch queue by that many resident waves. */
 int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu);
 
-/* Tuning: kernel schedule.  0 (default) chooses by batch size; 1 decodes
- * one frame per wave (throughput regime); 2 one frame per workgroup of
- * ceil(E/64) waves, one edge per lane (latency regime, small batches).
+/* Tuning: kernel schedule.  0 (default) = 1: one frame per wave; 2: one
+ * frame per workgroup of ceil(E/64) waves, one edge per lane (kept for
+ * latency experiments; measured no faster at any batch size on MI355X).
  * Results are identical across schedules. */
 int ldpc_set_schedule(ldpc_ctx *ctx, int schedule);
 
