@@ -240,22 +240,10 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #endif
     for (int h = 0; h < a.max_iters; ++h) {
 #ifndef LDPC_NO_FAIR
-      {
-        // Issue priority for starved waves.  A SIMD's waves issue oldest
-        // first, and two waves already keep its VALU busy, so the third wave
-        // of a SIMD crawls (1.7-2 us per iteration against ~1 us) and a long
-        // frame it holds ends the batch.  A wave whose last iteration took
-        // more than LDPC_FAIR_CYCLES core clocks issues first for the next
-        // one (same-box A/B on the headline: -2.6 %).  Scheduling only: the
-        // arithmetic is untouched.
-        const uint64_t now = __builtin_amdgcn_s_memtime();
-        const uint32_t d = (uint32_t)(now - t_prev);
-        t_prev = now;
-        if (d > LDPC_FAIR_CYCLES)
-          __builtin_amdgcn_s_setprio(3);
-        else
-          __builtin_amdgcn_s_setprio(0);
-      }
+      // read here, used once the row gathers below have been waited for (an
+      // SMEM result needs lgkmcnt(0), which would otherwise also drain the
+      // previous iteration's LDS scatters before any gather could issue)
+      const uint64_t now = __builtin_amdgcn_s_memtime();
 #endif
       wave_lds_sync();  // tb complete
       Real nb[S][DCN];
@@ -276,6 +264,23 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         for (int k = 0; k < DCN; ++k) T = T * nb[s][k];
         eb[lane + 64 * s] = Math<PREC>::check_msg(T, logtab);
       }
+#ifndef LDPC_NO_FAIR
+      {
+        // Issue priority for starved waves.  A SIMD's waves issue oldest
+        // first, and two waves already keep its VALU busy, so the third wave
+        // of a SIMD crawls (1.7-2 us per iteration against ~1 us) and a long
+        // frame it holds ends the batch.  A wave whose last iteration took
+        // more than LDPC_FAIR_CYCLES core clocks issues first for the next
+        // one (same-box A/B on the headline: -2.6 %).  Scheduling only: the
+        // arithmetic is untouched.
+        const uint32_t d = (uint32_t)(now - t_prev);
+        t_prev = now;
+        if (d > LDPC_FAIR_CYCLES)
+          __builtin_amdgcn_s_setprio(3);
+        else
+          __builtin_amdgcn_s_setprio(0);
+      }
+#endif
       wave_lds_sync();  // eb complete
       Real tv[NW][DVN];
 #pragma unroll
