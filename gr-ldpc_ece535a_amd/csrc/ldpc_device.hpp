@@ -13,7 +13,8 @@
 namespace ldpc {
 
 // Arithmetic per precision mode (include/ldpc_hip.h LDPC_PREC_*):
-//   0 F64       double, compact tanh (<= 3 ulp of glibc) and table-driven
+//   0 F64       double, compact two-range tanh (glibc's double near 1, <= 3 ulp
+//               elsewhere) and table-driven
 //               log (<= 1 ulp) of ldpc_math.hpp, reciprocal-based divisions
 //   1 F32       float, ROCm libm
 //   2 F64_LIBM  double, fdlibm tanh bit-identical to glibc's, fdlibm log
@@ -45,7 +46,11 @@ struct Math<0> {
     return fm::log_ratio_fast(T);
   }
 #else
+#ifdef LDPC_TANH_SINGLE_RANGE  // A/B only: loses parity on large-amplitude frames
   static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_fast(m); }
+#else
+  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_acc(m); }
+#endif
   static __device__ __forceinline__ double check_msg(double T, const fm::LogTabEntry *tab) {
     return fm::log_ratio_tab(T, tab);
   }

@@ -52,6 +52,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 #endif
 }
 
+#ifndef LDPC_TANH_SPLIT
+#define LDPC_TANH_SPLIT 16.0  // |m| below which the single-range tanh(m/2) is used
+#endif
 #ifndef LDPC_FAIR_CYCLES
 #define LDPC_FAIR_CYCLES 2200  // ~1.1 us at the ~2 GHz the chip holds under this load
 #endif
@@ -310,6 +313,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       // the next iteration's operands are computed before the exit test (on
       // the last iteration they are dead stores into this wave's tb), so the
       // syndrome's ballot / scalar chain overlaps the tanh arithmetic
+      Real mv[NW][DVN];
 #pragma unroll
       for (int q = 0; q < NW; ++q)
 #pragma unroll
@@ -323,8 +327,35 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
             else
               m = ea[q][k2] != eb_dummy ? m + tv[q][k2] : m;
           }
-          lds_st<Real>(ta[q][k], Math<PREC>::tanh_half(m));  // :509
+          mv[q][k] = m;
         }
+      if constexpr (PREC == 0 && LDPC_TANH_SPLIT > 0) {
+        // tanh(m/2), :509.  While every |m| of the frame is below the split,
+        // the single-range form (no cap, no range selects) is used: its 1-3 ulp
+        // near 1 stay below ~1e-9 in the check messages there.  Otherwise the
+        // two-range form, glibc's double near 1 (Math<0>::tanh_half).
+        bool wide = false;
+#pragma unroll
+        for (int q = 0; q < NW; ++q)
+#pragma unroll
+          for (int k = 0; k < DVN; ++k) wide |= !(__builtin_fabs(mv[q][k]) <= LDPC_TANH_SPLIT);
+        if (__builtin_amdgcn_ballot_w64(wide) == 0) {
+#pragma unroll
+          for (int q = 0; q < NW; ++q)
+#pragma unroll
+            for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], fm::tanh_half_small(mv[q][k]));
+        } else {
+#pragma unroll
+          for (int q = 0; q < NW; ++q)
+#pragma unroll
+            for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], Math<PREC>::tanh_half(mv[q][k]));
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < NW; ++q)
+#pragma unroll
+          for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], Math<PREC>::tanh_half(mv[q][k]));
+      }
 #ifndef LDPC_COLS_LATE_TANH
       weight = syndrome();
       used = h + 1;

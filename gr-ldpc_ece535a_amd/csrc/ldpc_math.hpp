@@ -471,6 +471,32 @@ LDPC_HD double tanh_half_fast(double m) {
   return __builtin_copysign(div_fast(-t, t + 2.0), m);
 }
 
+// tanh_half_fast without its cap: |m| <= 44 (finite) only.
+LDPC_HD double tanh_half_small(double m) {
+  const double t = expm1_mid_f64(-__builtin_fabs(m));
+  return __builtin_copysign(div_fast(-t, t + 2.0), m);
+}
+
+// tanh(m / 2) with fdlibm's two ranges (s_tanh.c) on x = |m| / 2:
+//   |m| <  2: t = expm1(-|m|), tanh = -t / (t + 2)   (as tanh_half_fast)
+//   |m| >= 2: t = expm1( |m|), tanh = 1 - 2 / (t + 2)
+// Near 1 the single-range form's quotient carries 1-3 ulp of 1.0, i.e. a
+// relative error of 1 - tanh, which the check message log((1+T)/(1-T))
+// amplifies (a 30x-amplitude frame moved its posteriors by ~1e-2 and its
+// decisions).  Here the small q = 2 / (t + 2) is formed first and the result
+// is the rounding of 1 - q: q's few-ulp error reaches that rounding only
+// with probability ~ q 2^-50, so the result is glibc's double except near
+// |m| = 2, where 1 - tanh is not small and the error is harmless.  |m| is
+// capped at 44 (tanh = 1 from 38 on); NaN propagates; the sign is copied.
+LDPC_HD double tanh_half_acc(double m) {
+  const double a = __builtin_fabs(m);
+  const bool big = a >= 2.0;
+  const double ac = a > 44.0 ? 44.0 : a;  // NaN stays NaN
+  const double t = expm1_mid_f64(big ? ac : -ac);
+  const double q = div_fast(big ? 2.0 : -t, t + 2.0);
+  return __builtin_copysign(big ? 1.0 - q : q, m);
+}
+
 // log((1+T)/(1-T)), the sum-product check message (:513), for T in [-1, 1]
 // (a product of tanh values) or NaN.  The ratio q is then 0 only for T = -1,
 // +inf only for T = 1 and never subnormal or negative, so log_fast_f64's

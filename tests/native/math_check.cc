@@ -73,7 +73,9 @@ void check_fast(int fn, const double *x, int64_t n, int64_t *out) {
 extern "C" {
 // the check-pass forms vs glibc: fn 0 tanh_half_fast(m) vs tanh(m/2),
 // fn 1 log_ratio_fast(T) vs log((1+T)/(1-T)), fn 2 tanh_half_fast(m) vs
-// tanh_fast_f64(m/2) (must be identical for normal m).
+// tanh_fast_f64(m/2) (must be identical for normal m), fn 3 the two-range
+// tanh_half_acc(m) vs tanh(m/2), fn 4 tanh_half_small vs tanh_half_fast
+// (identical for |m| <= 44).
 // out[0] = mismatches, out[1] = max ulp
 void check_pass(int fn, const double *x, int64_t n, int64_t *out) {
   int64_t mism = 0, maxu = 0;
@@ -81,7 +83,9 @@ void check_pass(int fn, const double *x, int64_t n, int64_t *out) {
     double a, b;
     if (fn == 0) { a = ldpc::fm::tanh_half_fast(x[i]); b = tanh(x[i] / 2.0); }
     else if (fn == 1) { a = ldpc::fm::log_ratio_fast(x[i]); b = log((1.0 + x[i]) / (1.0 - x[i])); }
-    else { a = ldpc::fm::tanh_half_fast(x[i]); b = ldpc::fm::tanh_fast_f64(x[i] / 2.0); }
+    else if (fn == 2) { a = ldpc::fm::tanh_half_fast(x[i]); b = ldpc::fm::tanh_fast_f64(x[i] / 2.0); }
+    else if (fn == 3) { a = ldpc::fm::tanh_half_acc(x[i]); b = tanh(x[i] / 2.0); }
+    else { a = ldpc::fm::tanh_half_small(x[i]); b = ldpc::fm::tanh_half_fast(x[i]); }
     int64_t u = ulps(a, b);
     if (u) ++mism;
     if (u > maxu) maxu = u;

@@ -175,3 +175,27 @@ def test_non_finite_samples(golden, method, prec, graph):
     np.testing.assert_array_equal(out["bits"], ref["bits"])
     np.testing.assert_array_equal(out["iters"], ref["iters"])
     np.testing.assert_array_equal(out["synd"], ref["synd"])
+
+
+@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("prec", [0, 2])
+@pytest.mark.parametrize("method", [0, 1])
+def test_extreme_finite_samples(golden, method, prec, graph):
+    """Finite samples far outside the channel's range: amplitudes up to 1e30
+    (tanh saturates to +-1, so T = +-1 gives +-inf check messages and inf - inf
+    = NaN bit messages inside frames whose samples are all finite -- the
+    select-free sum-product variant), and tiny / subnormal amplitudes.  The
+    decoder must follow the reference's double arithmetic through all of it."""
+    import ldpc_ece535a as L
+    from oracle import oracle as orc
+    fd = golden("frames_default.npz")
+    base = fd["db2_llr"].astype(np.float64)
+    parts = [base[:48] * a for a in (8.0, 30.0, 1e3, 1e10, 1e30, 1e-30, 1e-40)]
+    y = np.concatenate(parts).astype(np.float32)
+    assert np.isfinite(y).all()
+    d = L.Decoder(force_graph=graph)
+    out = d.decode(y, method=method, max_iters=30, precision=prec)
+    ref = orc.decode_batch(method, fd["H_reordered"], y, 30)
+    np.testing.assert_array_equal(out["bits"], ref["bits"])
+    np.testing.assert_array_equal(out["iters"], ref["iters"])
+    np.testing.assert_array_equal(out["synd"], ref["synd"])

@@ -108,6 +108,33 @@ def test_check_pass_forms(mc):
         assert maxulp <= 3
 
 
+def test_two_range_tanh_matches_libm_near_one(mc):
+    """The f64 mode's tanh(m/2) (tanh_half_acc, used whenever some |m| of the
+    frame reaches the split): glibc's exact double for |m| >= 16 and all but
+    ~1e-5 of the values in [8, 16) -- where 1 - tanh is small and
+    log((1+T)/(1-T)) would amplify any last-bit difference --, within 1 ulp
+    for |m| >= 2 (the single-range form is 1-2 ulp off for most of them) and
+    within 3 ulp below (the single-range form there).  The
+    uncapped single-range form of the fast path equals tanh_half_fast
+    wherever it is used (|m| <= 44)."""
+    rng = np.random.default_rng(21)
+    far = np.concatenate([rng.uniform(16, 60, 400_000), -rng.uniform(16, 60, 400_000),
+                          np.array([np.inf, -np.inf, 44.0, 38.0, 100.0, 1e300])])
+    mism, _ = _run(mc, "check_pass", 3, far)
+    assert mism == 0
+    mid = rng.uniform(8, 16, 400_000) * rng.choice([-1.0, 1.0], 400_000)
+    mism, maxulp = _run(mc, "check_pass", 3, mid)
+    assert mism <= 8 and maxulp <= 1
+    for x in _inputs(22):
+        _, maxulp = _run(mc, "check_pass", 3, x)
+        assert maxulp <= 3
+        _, maxulp = _run(mc, "check_pass", 3, x[np.abs(x) >= 2.0])
+        assert maxulp <= 1
+        small = x[np.isfinite(x) & (np.abs(x) <= 44.0)]
+        mism, _ = _run(mc, "check_pass", 4, small)
+        assert mism == 0
+
+
 def test_table_log_within_1ulp(mc):
     """LDPC_PREC_F64's table-driven log((1+T)/(1-T)) (tools/gen_logtab.py):
     within 1 ulp of glibc over T in [-1, 1], near +-1, near 0 and the edges."""
