@@ -450,19 +450,27 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           for (int k = 0; k < DCN; ++k) T = T * nb[s][k];
           eb[lane + 64 * s] = Math<PREC>::check_msg(T, logtab);
         } else {
-          // min-sum horizontal step (:350-376): sign product over the row
-          // times the minimum |L(q)| of the other edges.  Padding neighbours
-          // read DBL_MAX: sign +1, never below the running minimum.
-          const int self = sgn(msg[s]);
-          int prod = self;
+          // min-sum horizontal step (:350-376): L(r) = p * alpha_self * min,
+          // p = prod of every alpha of the row (self included), so
+          // p * alpha_self = alpha_self^2 * prod_{others} alpha: 0 when any
+          // alpha is sign(0) = 0 (NaN too: neither > 0 nor < 0), else the
+          // parity of the others' negative signs -- kept as two masks
+          // instead of integer products.  min: fmin against a running value
+          // that never holds a NaN equals the reference's `beta < min`
+          // (a NaN beta never wins).  Padding neighbours read DBL_MAX: sign
+          // +1, never below the running minimum.  +0.0 for a zero product,
+          // as (double)0 * min.
+          bool zero = !(msg[s] > Real(0)) && !(msg[s] < Real(0));
+          bool neg = false;
           Real lo = Math<PREC>::max_();
 #pragma unroll
           for (int k = 0; k < DCN; ++k) {
-            prod *= sgn(nb[s][k]);
-            const Real beta = Math<PREC>::abs_(nb[s][k]);
-            lo = beta < lo ? beta : lo;
+            const bool pos = nb[s][k] > Real(0), ng = nb[s][k] < Real(0);
+            zero |= !pos && !ng;
+            neg ^= ng;
+            lo = __builtin_fmin(Math<PREC>::abs_(nb[s][k]), lo);
           }
-          lr[s] = (Real)(prod * self) * lo;
+          lr[s] = zero ? Real(0) : (neg ? -lo : lo);
           eb[lane + 64 * s] = lr[s];
         }
       }
