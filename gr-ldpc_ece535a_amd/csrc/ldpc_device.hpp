@@ -35,17 +35,6 @@ __device__ __forceinline__ void stage_logtab(fm::LogTabEntry *lds) {
 template <>
 struct Math<0> {
   typedef double Real;
-#if defined(LDPC_EXP_CHEAP)  // latency experiments only: wrong results
-  static __device__ __forceinline__ double tanh_half(double m) { return m * 0.25; }
-  static __device__ __forceinline__ double check_msg(double T, const fm::LogTabEntry *) {
-    return T * 0.5;
-  }
-#elif defined(LDPC_EXP_POLYLOG)
-  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_fast(m); }
-  static __device__ __forceinline__ double check_msg(double T, const fm::LogTabEntry *) {
-    return fm::log_ratio_fast(T);
-  }
-#else
 #ifdef LDPC_TANH_SINGLE_RANGE  // A/B only: loses parity on large-amplitude frames
   static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_fast(m); }
 #else
@@ -54,7 +43,6 @@ struct Math<0> {
   static __device__ __forceinline__ double check_msg(double T, const fm::LogTabEntry *tab) {
     return fm::log_ratio_tab(T, tab);
   }
-#endif
   static __device__ __forceinline__ double abs_(double x) { return ::fabs(x); }
   static __device__ __forceinline__ double max_() { return DBL_MAX; }
 };
