@@ -304,12 +304,6 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         post[q] = acc;
         hard[q] = __builtin_amdgcn_ballot_w64(acc <= Real(0)) & col_ok[q];
       }
-#ifdef LDPC_COLS_LATE_TANH
-      weight = syndrome();
-      used = h + 1;
-      if (h + 1 == a.max_iters) break;
-      if ((h + 1) % a.et_period == 0 && weight == 0) break;
-#endif
       // the next iteration's operands are computed before the exit test (on
       // the last iteration they are dead stores into this wave's tb), so the
       // syndrome's ballot / scalar chain overlaps the tanh arithmetic
@@ -356,12 +350,10 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
           for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], Math<PREC>::tanh_half(mv[q][k]));
       }
-#ifndef LDPC_COLS_LATE_TANH
       weight = syndrome();
       used = h + 1;
       if (h + 1 == a.max_iters) break;
       if ((h + 1) % a.et_period == 0 && weight == 0) break;
-#endif
     }
   } else if constexpr (METHOD == 1 || METHOD == 0) {
     // the tables were relocated to LDS byte addresses (decode_small_kernel):
