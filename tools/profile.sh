@@ -9,7 +9,7 @@ tag=${1:-run}; shift
 out=gpurun_out/prof/$tag
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-args="--no-cpu-baseline --no-variants --steps 20 --warmup 3 $*"
+args="--no-cpu-baseline --no-variants --steps 100 --warmup 200 $*"
 run() {  # name, rocprof options...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" -d "$out/$name" -o "$name" --output-format csv \
