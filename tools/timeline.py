@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--method", type=int, default=1)
     ap.add_argument("--json", default=None)
     ap.add_argument("--et", type=int, default=1, help="syndrome check period (50: every frame runs 50)")
+    ap.add_argument("--launches", type=int, default=0,
+                    help="instead: run this many launches from a cold process and print the span "
+                         "and median in-kernel clock of selected ones (warmup behaviour)")
     a = ap.parse_args()
     import torch  # first: one HIP runtime
     import bench  # noqa: E402  (sets sys.path from LDPC_PKG_DIR)
@@ -41,12 +44,26 @@ def main():
     dec = L.Decoder()
     y, _ = bench.synth(dec.H, a.batch, a.ebn0, 2024)
     d_in = torch.from_numpy(y).cuda()
-    _, kern_ms, iters, _ = bench.time_decoder(dec, torch, d_in, a.batch, a.method, 50, a.et,
-                                              a.precision, 3, 2)
-    torch.cuda.synchronize()
     B = a.batch
     buf = np.zeros(4 * B, np.uint64)
     lib.ldpc_debug_timeline.restype = ctypes.c_int
+    if a.launches:
+        show = {0, 1, 2, 5, 10, 20, 50, 100, 150, 200, 300, 400, 600, 800}
+        for i in range(a.launches):
+            _, kms, _, _ = bench.time_decoder(dec, torch, d_in, B, a.method, 50, a.et, a.precision, 1, 0)
+            torch.cuda.synchronize()
+            if i in show or i == a.launches - 1:
+                assert lib.ldpc_debug_timeline(buf.ctypes.data_as(ctypes.c_void_p), B) == B
+                t = buf.reshape(B, 4)
+                st = t[:, 0].astype(np.float64)
+                en = t[:, 1].astype(np.float64)
+                dur = np.maximum((en - st) / 100.0, 1e-3)
+                print("launch %4d: kernel %.4f ms, span %.1f us, in-kernel clock median %.3f GHz" %
+                      (i, kms, (en.max() - st.min()) / 100.0, np.median(t[:, 3] / dur / 1e3)), flush=True)
+        return
+    _, kern_ms, iters, _ = bench.time_decoder(dec, torch, d_in, a.batch, a.method, 50, a.et,
+                                              a.precision, 3, 2)
+    torch.cuda.synchronize()
     n = lib.ldpc_debug_timeline(buf.ctypes.data_as(ctypes.c_void_p), B)
     assert n == B, n
     t = buf.reshape(B, 4)
