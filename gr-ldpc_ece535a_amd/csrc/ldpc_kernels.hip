@@ -56,7 +56,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define LDPC_TANH_SPLIT 16.0  // |m| below which the single-range tanh(m/2) is used
 #endif
 #ifndef LDPC_FAIR_CYCLES
-#define LDPC_FAIR_CYCLES 2200  // ~1.1 us at the ~2 GHz the chip holds under this load
+// core clocks (~0.77 us at the warm 2.33 GHz); profiles/round1/ab_fair_threshold_warm.txt:
+// 1800 is the best of 1200..3000 warm and cold, and 1600 or less loses 7 %
+#define LDPC_FAIR_CYCLES 1800
 #endif
 
 template <int NW>
