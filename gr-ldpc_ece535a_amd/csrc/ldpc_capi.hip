@@ -35,8 +35,18 @@ struct ldpc_ctx {
   uint64_t *d_rowmask = nullptr;
   void *d_stage = nullptr;
   size_t stage_bytes = 0;
-  uint32_t *d_tickets = nullptr;  // ring of per-launch frame-queue heads
-  unsigned launch_seq = 0;
+  // small-code frame queues: one monotonic counter per stream that has
+  // launched on this context (ldpc_kernels.hpp DecodeArgs::ticket)
+  uint32_t *d_tickets = nullptr;
+  struct Queue {
+    void *stream;
+    uint32_t base;  // counter value at the start of the next launch
+  };
+  std::vector<Queue> queues;
+  // large-code path: the workspace is shared, so launches on a different
+  // stream than the previous one first wait for it (graph_done)
+  void *graph_stream = nullptr;
+  hipEvent_t graph_done = nullptr;
   int waves_per_cu = 0;           // 0: kernel default
   int schedule = 0;               // 0 auto, 1 wave per frame, 2 workgroup per frame
   // large-code path (ldpc_graph.hip): H as CSR + CSC, messages in a workspace
@@ -54,7 +64,7 @@ struct ldpc_ctx {
   std::string err;
 };
 
-#define LDPC_TICKET_RING 64
+#define LDPC_TICKET_SLOTS 64
 
 namespace {
 
@@ -563,7 +573,7 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     upload(ctx, &ctx->d_ecol, crecs, "upload(ecol)", what, e);
     upload(ctx, &ctx->d_cols, cols, "upload(cols)", what, e);
     upload(ctx, &ctx->d_rowmask, rowmask, "upload(rowmask)", what, e);
-    std::vector<uint32_t> zeros(LDPC_TICKET_RING, 0);
+    std::vector<uint32_t> zeros(LDPC_TICKET_SLOTS, 0);
     upload(ctx, &ctx->d_tickets, zeros, "upload(tickets)", what, e);
   }
   if (what) {
@@ -626,7 +636,11 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
     if (p) (void)hipFree(p);
-  if (ctx->d_work) (void)hipFree(ctx->d_work);
+  if (ctx->d_work) {
+    (void)hipDeviceSynchronize();  // graph decodes may run on caller streams
+    (void)hipFree(ctx->d_work);
+  }
+  if (ctx->graph_done) (void)hipEventDestroy(ctx->graph_done);
   if (ctx->d_encA) (void)hipFree(ctx->d_encA);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -746,15 +760,45 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   void *st = hip_stream ? hip_stream : (void *)ctx->stream;
-  if (ctx->graph) return decode_graph(ctx, a, method, precision, st);
-  a.ticket = ctx->d_tickets + (ctx->launch_seq % LDPC_TICKET_RING);
-  a.ticket_next = ctx->d_tickets + ((ctx->launch_seq + 1) % LDPC_TICKET_RING);
+  if (ctx->graph) {
+    // one workspace per context: order this decode after the previous one
+    // when it was enqueued on another stream
+    if (!ctx->graph_done &&
+        (e = hipEventCreateWithFlags(&ctx->graph_done, hipEventDisableTiming)) != hipSuccess)
+      return hip_err(ctx, e, "hipEventCreate");
+    if (ctx->graph_stream && ctx->graph_stream != st &&
+        (e = hipStreamWaitEvent((hipStream_t)st, ctx->graph_done, 0)) != hipSuccess)
+      return hip_err(ctx, e, "hipStreamWaitEvent");
+    rc = decode_graph(ctx, a, method, precision, st);
+    if (rc != LDPC_OK) return rc;
+    if ((e = hipEventRecord(ctx->graph_done, (hipStream_t)st)) != hipSuccess)
+      return hip_err(ctx, e, "hipEventRecord");
+    ctx->graph_stream = st;
+    return LDPC_OK;
+  }
+  // the stream's own frame-queue counter (ldpc_kernels.hpp DecodeArgs::ticket)
+  size_t q = 0;
+  while (q < ctx->queues.size() && ctx->queues[q].stream != st) ++q;
+  if (q == ctx->queues.size()) {
+    if (q == LDPC_TICKET_SLOTS) {
+      // more streams than counters: drain the device, start every queue over
+      if ((e = hipDeviceSynchronize()) != hipSuccess ||
+          (e = hipMemset(ctx->d_tickets, 0, LDPC_TICKET_SLOTS * sizeof(uint32_t))) != hipSuccess)
+        return hip_err(ctx, e, "ticket reset");
+      ctx->queues.clear();
+      q = 0;
+    }
+    // slots are handed out in order from zeroed memory (creation, reset)
+    ctx->queues.push_back({st, 0u});
+  }
+  a.ticket = ctx->d_tickets + q;
+  a.ticket_base = ctx->queues[q].base;
   a.waves = 0;
   rc = ldpc::launch_decode(code_view(ctx), a, method, precision, ctx->slots, ctx->nw,
                            ctx->waves_per_cu, ctx->schedule, st);
   if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no kernel for this code shape");
   if (rc != 0) return hip_err(ctx, hipGetLastError(), "kernel launch");
-  ++ctx->launch_seq;  // only a launched kernel consumes (and re-arms) a ticket slot
+  ctx->queues[q].base += (uint32_t)B;  // the launch adds exactly B to its counter
   return LDPC_OK;
 }
 

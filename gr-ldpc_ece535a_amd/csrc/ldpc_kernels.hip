@@ -650,7 +650,6 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
   const int wave = threadIdx.x >> 6;
   const int M = code.M;
   const Layout<Real, S, NW> L;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.ticket_next = 0u;  // next launch's queue head
   __shared__ fm::LogTabEntry logtab[1 << fm::kLogTabBits];
   if constexpr (METHOD == 1 && PREC == 0) stage_logtab(logtab);
 
@@ -764,7 +763,7 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
     }
 #endif
     uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(a.ticket, 1u);
+    if (lane == 0) t = atomicAdd(a.ticket, 1u) - a.ticket_base;
     b = (int64_t)a.waves + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
   }
 }
@@ -805,7 +804,6 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
   Real *rb = reinterpret_cast<Real *>(smem + L.waves + (size_t)wave * L.per_wave);
   Real *sb = rb + 64 * NW;
   int *fslot = reinterpret_cast<int *>(smem + L.fslot);
-  if (blockIdx.x == 0 && tid == 0) *a.ticket_next = 0u;  // next launch's queue head
   __shared__ fm::LogTabEntry logtab[1 << fm::kLogTabBits];
   if constexpr (METHOD == 1 && PREC == 0) stage_logtab(logtab);
   if (tid == 0) tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
@@ -969,7 +967,7 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
       }
     }
     wave_lds_sync();  // this wave's rb reads done before the next frame's writes
-    if (tid == 0) *fslot = (int)atomicAdd(a.ticket, 1u);
+    if (tid == 0) *fslot = (int)(atomicAdd(a.ticket, 1u) - a.ticket_base);
     __syncthreads();
     b = (int64_t)a.waves + (int64_t)*fslot;
   }

@@ -65,11 +65,15 @@ struct DecodeArgs {
   int32_t *synd;             // B       (optional)
   float *llr;                // B x N   (optional)
   // persistent scheduling: `waves` resident waves take frames 0..waves-1,
-  // then pull the next frame index from *ticket.  Tickets are a ring owned by
-  // the context: this launch's slot was zeroed by the previous launch on the
-  // stream (or at context creation), and this launch zeroes ticket_next.
+  // then pull the next frame index from *ticket, a monotonic counter owned by
+  // the (context, stream) pair: frame = waves + (atomicAdd(ticket, 1) -
+  // ticket_base).  A launch adds exactly B to its counter (one add per frame
+  // decoded, the last add of each wave being the one past the batch), so the
+  // host advances ticket_base by B per launch and no launch ever zeroes a
+  // counter: launches on different streams use different counters and
+  // cannot disturb each other's queues.
   uint32_t *ticket;
-  uint32_t *ticket_next;
+  uint32_t ticket_base;
   int waves;
 };
 

@@ -30,7 +30,8 @@
  *
  * Conventions: plain pointers and sizes only; errors are negative return
  * codes (LDPC_E*), never exceptions; ldpc_last_error() gives the text.  One
- * context per block instance; a context is not re-entrant.  Host helpers
+ * context per block instance; a context is not re-entrant (one host thread at
+ * a time), though its device decodes may target several streams.  Host helpers
  * (ldpc_reorder_h, ldpc_check_frame, ldpc_encode, ldpc_default_h) need no GPU.
  * Everything that decodes runs on the GPU; there is no CPU fallback.
  */
@@ -165,7 +166,10 @@ int ldpc_decode_strided(ldpc_ctx *ctx, int method, int max_iters,
 
 /* Device-resident buffers (already in HBM); enqueues on `hip_stream`
  * (hipStream_t, NULL = the context's own stream) and returns without
- * synchronising. */
+ * synchronising.  One host thread may enqueue on several streams: small-code
+ * launches on different streams run concurrently (each stream has its own
+ * frame queue), large-code launches share the context's workspace and are
+ * ordered after the previous one when the stream changes. */
 int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
                        int et_period, int precision, const float *d_in,
                        int64_t cw_stride, int elem_stride, float polarity,

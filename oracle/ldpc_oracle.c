@@ -19,6 +19,12 @@
 
 #define AT(A, ncols, r, c) ((A)[(size_t)(r) * (size_t)(ncols) + (size_t)(c)])
 
+/* Early-termination period (not in the reference, which
+ * tests every iteration): the syndrome test that may stop a frame after
+ * iteration `it` (0-based) runs only when (it + 1) % et == 0.  et == 1 is
+ * the reference's rule exactly (:406-408, :470-472, :535-537). */
+#define ET_DUE(it, et) (((it) + 1) % (et) == 0)
+
 /* ------------------------------------------------------------------ */
 /* reorderHMatrix -- lib/ldpc_decoder_cb_impl.cc:255-307                */
 /* ------------------------------------------------------------------ */
@@ -91,8 +97,8 @@ void orc_decode_hard(const double *rx, int N, int *vhat) {
 /* ------------------------------------------------------------------ */
 /* decodeBitFlipping -- :414-476                                        */
 /* ------------------------------------------------------------------ */
-int orc_decode_bitflip(const uint8_t *H, int M, int N, const double *rx,
-                       int iterations, int *vhat) {
+static int bitflip_et(const uint8_t *H, int M, int N, const double *rx,
+                      int iterations, int et, int *vhat) {
   int *y = (int *)malloc(sizeof(int) * N);
   int *E = (int *)calloc((size_t)M * N, sizeof(int));
   for (int i = 0; i < N; i++) y[i] = (rx[i] < 0.0) ? 0 : 1; /* :424-431 */
@@ -116,7 +122,7 @@ int orc_decode_bitflip(const uint8_t *H, int M, int N, const double *rx,
         if (AT(H, N, i, j) != 0 && AT(E, N, i, j) != y[j]) votes++;
       if (votes > half) vhat[j] = (y[j] + 1) % 2;
     }
-    if (it + 1 < iterations && orc_check_frame(H, M, N, vhat, 0) == 0) {
+    if (it + 1 < iterations && ET_DUE(it, et) && orc_check_frame(H, M, N, vhat, 0) == 0) {
       used = it + 1; /* :470-472 */
       break;
     }
@@ -134,8 +140,8 @@ static int orc_sign(double v) { return (v > 0) - (v < 0); }
 /* ------------------------------------------------------------------ */
 /* decodeLogDomainSimple (plain min-sum) -- :309-412                    */
 /* ------------------------------------------------------------------ */
-int orc_decode_minsum(const uint8_t *H, int M, int N, const double *rx,
-                      int iterations, int *vhat, double *post_opt) {
+static int minsum_et(const uint8_t *H, int M, int N, const double *rx,
+                     int iterations, int et, int *vhat, double *post_opt) {
   double *Lci = (double *)malloc(sizeof(double) * N);
   double *Lr = (double *)calloc((size_t)M * N, sizeof(double));
   double *Lq = (double *)malloc(sizeof(double) * (size_t)M * N);
@@ -180,7 +186,7 @@ int orc_decode_minsum(const uint8_t *H, int M, int N, const double *rx,
       vhat[c] = (LQ < 0) ? 1 : 0;
       if (post_opt) post_opt[c] = LQ;
     }
-    if (it + 1 < iterations && orc_check_frame(H, M, N, vhat, 0) == 0) {
+    if (it + 1 < iterations && ET_DUE(it, et) && orc_check_frame(H, M, N, vhat, 0) == 0) {
       used = it + 1; /* :406-408 */
       break;
     }
@@ -196,8 +202,8 @@ int orc_decode_minsum(const uint8_t *H, int M, int N, const double *rx,
 /* ------------------------------------------------------------------ */
 /* decodeSumProductSoft -- :478-557                                     */
 /* ------------------------------------------------------------------ */
-int orc_decode_sumproduct(const uint8_t *H, int M, int N, const double *rx,
-                          int iterations, int *vhat, double *post_opt) {
+static int sumproduct_et(const uint8_t *H, int M, int N, const double *rx,
+                         int iterations, int et, int *vhat, double *post_opt) {
   double *r = (double *)malloc(sizeof(double) * N);
   double *Q = (double *)calloc((size_t)M * N, sizeof(double)); /* M(j,i) */
   double *Ec = (double *)calloc((size_t)M * N, sizeof(double)); /* E(j,i) */
@@ -227,7 +233,7 @@ int orc_decode_sumproduct(const uint8_t *H, int M, int N, const double *rx,
       vhat[i] = (L <= 0) ? 1 : 0;
       if (post_opt) post_opt[i] = L;
     }
-    if (orc_check_frame(H, M, N, vhat, 0) == 0) { /* :535-537 */
+    if (ET_DUE(it, et) && orc_check_frame(H, M, N, vhat, 0) == 0) { /* :535-537 */
       used = it + 1;
       break;
     }
@@ -248,8 +254,27 @@ int orc_decode_sumproduct(const uint8_t *H, int M, int N, const double *rx,
   return used;
 }
 
+int orc_decode_bitflip(const uint8_t *H, int M, int N, const double *rx,
+                       int iterations, int *vhat) {
+  return bitflip_et(H, M, N, rx, iterations, 1, vhat);
+}
+int orc_decode_minsum(const uint8_t *H, int M, int N, const double *rx,
+                      int iterations, int *vhat, double *post_opt) {
+  return minsum_et(H, M, N, rx, iterations, 1, vhat, post_opt);
+}
+int orc_decode_sumproduct(const uint8_t *H, int M, int N, const double *rx,
+                          int iterations, int *vhat, double *post_opt) {
+  return sumproduct_et(H, M, N, rx, iterations, 1, vhat, post_opt);
+}
+
 int orc_decode(int method, const uint8_t *H, int M, int N, const double *rx,
                int iterations, int *vhat, double *post_opt) {
+  return orc_decode_et(method, H, M, N, rx, iterations, 1, vhat, post_opt);
+}
+
+int orc_decode_et(int method, const uint8_t *H, int M, int N, const double *rx,
+                  int iterations, int et_period, int *vhat, double *post_opt) {
+  if (et_period < 1) et_period = 1;
   if (method == 3) {
     orc_decode_hard(rx, N, vhat);
     if (post_opt)
@@ -259,11 +284,11 @@ int orc_decode(int method, const uint8_t *H, int M, int N, const double *rx,
   if (method == 2) {
     if (post_opt) /* llr_out convention of include/ldpc_hip.h: tx */
       for (int i = 0; i < N; i++) post_opt[i] = rx[i];
-    return orc_decode_bitflip(H, M, N, rx, iterations, vhat);
+    return bitflip_et(H, M, N, rx, iterations, et_period, vhat);
   }
   if (method == 1)
-    return orc_decode_sumproduct(H, M, N, rx, iterations, vhat, post_opt);
-  return orc_decode_minsum(H, M, N, rx, iterations, vhat, post_opt);
+    return sumproduct_et(H, M, N, rx, iterations, et_period, vhat, post_opt);
+  return minsum_et(H, M, N, rx, iterations, et_period, vhat, post_opt);
 }
 
 /* ------------------------------------------------------------------ */
@@ -312,7 +337,7 @@ int orc_encode(const uint8_t *Hr, const uint8_t *L, const uint8_t *U, int M,
 /* batched helper                                                      */
 /* ------------------------------------------------------------------ */
 typedef struct {
-  int method, M, N, iterations, B, stride_threads, first;
+  int method, M, N, iterations, et, B, stride_threads, first;
   const uint8_t *H;
   const float *in;
   long cw_stride;
@@ -336,8 +361,8 @@ static void *orc_batch_worker(void *arg) {
       float t = src[(long)i * jb->elem_stride] * jb->polarity;
       rx[i] = (double)t;
     }
-    int used = orc_decode(jb->method, jb->H, M, N, rx, jb->iterations, v,
-                          jb->post ? post : NULL);
+    int used = orc_decode_et(jb->method, jb->H, M, N, rx, jb->iterations, jb->et, v,
+                             jb->post ? post : NULL);
     if (jb->iters) jb->iters[b] = used;
     if (jb->synd) jb->synd[b] = orc_check_frame(jb->H, M, N, v, M);
     if (jb->bits)
@@ -366,16 +391,26 @@ int orc_decode_batch(int method, const uint8_t *H, int M, int N, int iterations,
                      float polarity, int B, uint8_t *bits_opt,
                      uint8_t *packed_opt, int32_t *iters_opt, int32_t *synd_opt,
                      float *post_opt, int nthreads) {
+  return orc_decode_batch_et(method, H, M, N, iterations, 1, in, cw_stride, elem_stride,
+                             polarity, B, bits_opt, packed_opt, iters_opt, synd_opt, post_opt,
+                             nthreads);
+}
+
+int orc_decode_batch_et(int method, const uint8_t *H, int M, int N, int iterations,
+                        int et_period, const float *in, long cw_stride, int elem_stride,
+                        float polarity, int B, uint8_t *bits_opt, uint8_t *packed_opt,
+                        int32_t *iters_opt, int32_t *synd_opt, float *post_opt, int nthreads) {
+  if (et_period < 1) et_period = 1;
   if (nthreads < 1) nthreads = 1;
   if (nthreads > B) nthreads = B > 0 ? B : 1;
   orc_batch_job *jobs =
       (orc_batch_job *)malloc(sizeof(orc_batch_job) * (size_t)nthreads);
   pthread_t *tids = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
   for (int t = 0; t < nthreads; t++) {
-    orc_batch_job j = {method, M,         N,        iterations, B,
-                       nthreads, t,       H,        in,         cw_stride,
-                       elem_stride, polarity, bits_opt, packed_opt, iters_opt,
-                       synd_opt, post_opt};
+    orc_batch_job j = {method,      M,        N,        iterations, et_period,
+                       B,           nthreads, t,        H,          in,
+                       cw_stride,   elem_stride, polarity, bits_opt, packed_opt,
+                       iters_opt,   synd_opt, post_opt};
     jobs[t] = j;
   }
   if (nthreads == 1) {
@@ -440,8 +475,8 @@ int orc_check_frame_sparse(const int32_t *row_ptr, const int32_t *col_idx, int M
 }
 
 /* decodeLogDomainSimple (:309-412) on adjacency lists */
-static int orc_minsum_sparse(const orc_graph *g, const double *rx, int iterations, int *vhat,
-                             double *post_opt) {
+static int orc_minsum_sparse(const orc_graph *g, const double *rx, int iterations, int et,
+                             int *vhat, double *post_opt) {
   const int N = g->N, M = g->M, E = g->E;
   double *Lci = (double *)malloc(sizeof(double) * N);
   double *Lq = (double *)malloc(sizeof(double) * (size_t)(E > 0 ? E : 1));
@@ -472,7 +507,8 @@ static int orc_minsum_sparse(const orc_graph *g, const double *rx, int iteration
       vhat[c] = (LQ < 0) ? 1 : 0;
       if (post_opt) post_opt[c] = LQ;
     }
-    if (it + 1 < iterations && orc_check_frame_sparse(g->rp, g->ci, M, vhat, 0) == 0) {
+    if (it + 1 < iterations && ET_DUE(it, et) &&
+        orc_check_frame_sparse(g->rp, g->ci, M, vhat, 0) == 0) {
       used = it + 1;
       break;
     }
@@ -485,7 +521,7 @@ static int orc_minsum_sparse(const orc_graph *g, const double *rx, int iteration
 
 /* decodeSumProductSoft (:478-557) on adjacency lists */
 static int orc_sumproduct_sparse(const orc_graph *g, const double *rx, int iterations,
-                                 int *vhat, double *post_opt) {
+                                 int et, int *vhat, double *post_opt) {
   const int N = g->N, M = g->M, E = g->E;
   double *r = (double *)malloc(sizeof(double) * N);
   double *Q = (double *)malloc(sizeof(double) * (size_t)(E > 0 ? E : 1));
@@ -508,7 +544,7 @@ static int orc_sumproduct_sparse(const orc_graph *g, const double *rx, int itera
       vhat[i] = (L <= 0) ? 1 : 0;
       if (post_opt) post_opt[i] = L;
     }
-    if (orc_check_frame_sparse(g->rp, g->ci, M, vhat, 0) == 0) {
+    if (ET_DUE(it, et) && orc_check_frame_sparse(g->rp, g->ci, M, vhat, 0) == 0) {
       used = it + 1;
       break;
     }
@@ -528,7 +564,8 @@ static int orc_sumproduct_sparse(const orc_graph *g, const double *rx, int itera
 
 /* decodeBitFlipping (:414-476): E(i,j) for an edge is the parity of the
  * other row members, i.e. row parity ^ ci(j) */
-static int orc_bitflip_sparse(const orc_graph *g, const double *rx, int iterations, int *vhat) {
+static int orc_bitflip_sparse(const orc_graph *g, const double *rx, int iterations, int et,
+                              int *vhat) {
   const int N = g->N, M = g->M;
   int *y = (int *)malloc(sizeof(int) * N);
   int *rowpar = (int *)malloc(sizeof(int) * (M > 0 ? M : 1));
@@ -549,7 +586,8 @@ static int orc_bitflip_sparse(const orc_graph *g, const double *rx, int iteratio
       next[c] = votes > half ? (y[c] + 1) % 2 : vhat[c];
     }
     for (int c = 0; c < N; c++) vhat[c] = next[c];
-    if (it + 1 < iterations && orc_check_frame_sparse(g->rp, g->ci, M, vhat, 0) == 0) {
+    if (it + 1 < iterations && ET_DUE(it, et) &&
+        orc_check_frame_sparse(g->rp, g->ci, M, vhat, 0) == 0) {
       used = it + 1;
       break;
     }
@@ -561,7 +599,7 @@ static int orc_bitflip_sparse(const orc_graph *g, const double *rx, int iteratio
 }
 
 static int orc_decode_graph(int method, const orc_graph *g, const double *rx, int iterations,
-                            int *vhat, double *post_opt) {
+                            int et, int *vhat, double *post_opt) {
   if (method == 3) {
     orc_decode_hard(rx, g->N, vhat);
     if (post_opt)
@@ -571,23 +609,23 @@ static int orc_decode_graph(int method, const orc_graph *g, const double *rx, in
   if (method == 2) {
     if (post_opt)
       for (int i = 0; i < g->N; i++) post_opt[i] = rx[i];
-    return orc_bitflip_sparse(g, rx, iterations, vhat);
+    return orc_bitflip_sparse(g, rx, iterations, et, vhat);
   }
-  if (method == 1) return orc_sumproduct_sparse(g, rx, iterations, vhat, post_opt);
-  return orc_minsum_sparse(g, rx, iterations, vhat, post_opt);
+  if (method == 1) return orc_sumproduct_sparse(g, rx, iterations, et, vhat, post_opt);
+  return orc_minsum_sparse(g, rx, iterations, et, vhat, post_opt);
 }
 
 int orc_decode_sparse(int method, const int32_t *row_ptr, const int32_t *col_idx, int M, int N,
                       const double *rx, int iterations, int *vhat, double *post_opt) {
   orc_graph g;
   orc_graph_build(&g, row_ptr, col_idx, M, N);
-  const int used = orc_decode_graph(method, &g, rx, iterations, vhat, post_opt);
+  const int used = orc_decode_graph(method, &g, rx, iterations, 1, vhat, post_opt);
   orc_graph_free(&g);
   return used;
 }
 
 typedef struct {
-  int method, M, N, iterations, B, stride_threads, first;
+  int method, M, N, iterations, et, B, stride_threads, first;
   const orc_graph *g;
   const float *in;
   long cw_stride;
@@ -605,7 +643,7 @@ static void *orc_sparse_worker(void *arg) {
   for (int b = jb->first; b < jb->B; b += jb->stride_threads) {
     const float *src = jb->in + (long)b * jb->cw_stride;
     for (int i = 0; i < N; i++) rx[i] = (double)(src[(long)i * jb->elem_stride] * jb->polarity);
-    const int used = orc_decode_graph(jb->method, jb->g, rx, jb->iterations, v, NULL);
+    const int used = orc_decode_graph(jb->method, jb->g, rx, jb->iterations, jb->et, v, NULL);
     if (jb->iters) jb->iters[b] = used;
     if (jb->synd) jb->synd[b] = orc_check_frame_sparse(jb->g->rp, jb->g->ci, M, v, M);
     if (jb->bits)
@@ -630,6 +668,17 @@ int orc_decode_batch_sparse(int method, const int32_t *row_ptr, const int32_t *c
                             int elem_stride, float polarity, int B, uint8_t *bits_opt,
                             uint8_t *packed_opt, int32_t *iters_opt, int32_t *synd_opt,
                             int nthreads) {
+  return orc_decode_batch_sparse_et(method, row_ptr, col_idx, M, N, iterations, 1, in, cw_stride,
+                                    elem_stride, polarity, B, bits_opt, packed_opt, iters_opt,
+                                    synd_opt, nthreads);
+}
+
+int orc_decode_batch_sparse_et(int method, const int32_t *row_ptr, const int32_t *col_idx,
+                               int M, int N, int iterations, int et_period, const float *in,
+                               long cw_stride, int elem_stride, float polarity, int B,
+                               uint8_t *bits_opt, uint8_t *packed_opt, int32_t *iters_opt,
+                               int32_t *synd_opt, int nthreads) {
+  if (et_period < 1) et_period = 1;
   orc_graph g;
   orc_graph_build(&g, row_ptr, col_idx, M, N);
   if (nthreads < 1) nthreads = 1;
@@ -637,7 +686,7 @@ int orc_decode_batch_sparse(int method, const int32_t *row_ptr, const int32_t *c
   orc_sparse_job *jobs = (orc_sparse_job *)malloc(sizeof(orc_sparse_job) * (size_t)nthreads);
   pthread_t *tids = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
   for (int t = 0; t < nthreads; t++) {
-    orc_sparse_job j = {method, M, N, iterations, B, nthreads, t, &g, in, cw_stride,
+    orc_sparse_job j = {method, M, N, iterations, et_period, B, nthreads, t, &g, in, cw_stride,
                         elem_stride, polarity, bits_opt, packed_opt, iters_opt, synd_opt};
     jobs[t] = j;
   }

@@ -63,6 +63,13 @@ int orc_decode_sumproduct(const uint8_t *H, int M, int N, const double *rx,
 int orc_decode(int method, const uint8_t *H, int M, int N, const double *rx,
                int iterations, int *vhat, double *post_opt);
 
+/* The same with an early-termination period (an
+ * extension -- the reference tests after every iteration): the syndrome test
+ * that may stop a frame after iteration it (0-based) runs only when
+ * (it + 1) % et_period == 0.  et_period == 1 is orc_decode exactly. */
+int orc_decode_et(int method, const uint8_t *H, int M, int N, const double *rx,
+                  int iterations, int et_period, int *vhat, double *post_opt);
+
 /* makeParityCheck, lib/ldpc_encoder_bc_impl.cc:275-294 (with solve :180-223).
  * data: N-M bits; parity_out: M bits.  Returns 0, or -1 when a triangular
  * factor is singular (the reference's dgesv info>0 path). */
@@ -81,6 +88,11 @@ int orc_decode_batch(int method, const uint8_t *H, int M, int N, int iterations,
                      float polarity, int B, uint8_t *bits_opt,
                      uint8_t *packed_opt, int32_t *iters_opt, int32_t *synd_opt,
                      float *post_opt, int nthreads);
+/* orc_decode_batch with an early-termination period (see orc_decode_et). */
+int orc_decode_batch_et(int method, const uint8_t *H, int M, int N, int iterations,
+                        int et_period, const float *in, long cw_stride, int elem_stride,
+                        float polarity, int B, uint8_t *bits_opt, uint8_t *packed_opt,
+                        int32_t *iters_opt, int32_t *synd_opt, float *post_opt, int nthreads);
 
 /* Sparse (CSR) restatements for codes too large for the reference's dense
  * M x N arrays: the same per-edge arithmetic in the
@@ -97,6 +109,11 @@ int orc_decode_batch_sparse(int method, const int32_t *row_ptr, const int32_t *c
                             int elem_stride, float polarity, int B, uint8_t *bits_opt,
                             uint8_t *packed_opt, int32_t *iters_opt, int32_t *synd_opt,
                             int nthreads);
+int orc_decode_batch_sparse_et(int method, const int32_t *row_ptr, const int32_t *col_idx,
+                               int M, int N, int iterations, int et_period, const float *in,
+                               long cw_stride, int elem_stride, float polarity, int B,
+                               uint8_t *bits_opt, uint8_t *packed_opt, int32_t *iters_opt,
+                               int32_t *synd_opt, int nthreads);
 
 /* general_work restatement, lib/ldpc_decoder_cb_impl.cc:133-234 + forecast
  * :126-130.  `in` is interleaved gr_complex (re, im).  State lives in the

@@ -73,7 +73,7 @@ def decode_hard(rx):
     return [0 if x < 0 else 1 for x in rx], 0
 
 
-def decode_bitflip(H, rx, iterations):
+def decode_bitflip(H, rx, iterations, et_period=1):
     """decodeBitFlipping, :414-476 (E(i,j) for edges = parity of the other
     row members)."""
     g = _Graph(H)
@@ -90,7 +90,7 @@ def decode_bitflip(H, rx, iterations):
             votes = sum(1 for r in g.cols[c] if E[(r, c)] != y[c])
             if votes > half:
                 ci[c] = (y[c] + 1) % 2
-        if it + 1 < iterations and check_frame(H, ci, 0) == 0:
+        if it + 1 < iterations and (it + 1) % et_period == 0 and check_frame(H, ci, 0) == 0:
             used = it + 1
             break
     return ci, used
@@ -100,7 +100,7 @@ def _sign(v):
     return (v > 0) - (v < 0)
 
 
-def decode_minsum(H, rx, iterations):
+def decode_minsum(H, rx, iterations, et_period=1):
     """decodeLogDomainSimple, :309-412."""
     g = _Graph(H)
     Lci = [-x for x in rx]
@@ -126,13 +126,13 @@ def decode_minsum(H, rx, iterations):
             for r in g.cols[c]:
                 Lq[(r, c)] = Lci[c] + s - Lr[(r, c)]
             vhat[c] = 1 if (Lci[c] + s) < 0 else 0
-        if it + 1 < iterations and check_frame(H, vhat, 0) == 0:
+        if it + 1 < iterations and (it + 1) % et_period == 0 and check_frame(H, vhat, 0) == 0:
             used = it + 1
             break
     return vhat, used
 
 
-def decode_sumproduct(H, rx, iterations):
+def decode_sumproduct(H, rx, iterations, et_period=1):
     """decodeSumProductSoft, :478-557."""
     g = _Graph(H)
     r_ = [-x for x in rx]
@@ -166,7 +166,7 @@ def decode_sumproduct(H, rx, iterations):
             for j in g.cols[i]:
                 L += E[(j, i)] + r_[i]
             vhat[i] = 1 if L <= 0 else 0
-        if check_frame(H, vhat, 0) == 0:
+        if (it + 1) % et_period == 0 and check_frame(H, vhat, 0) == 0:
             used = it + 1
             break
         for j in range(g.M):
@@ -179,12 +179,14 @@ def decode_sumproduct(H, rx, iterations):
     return vhat, used
 
 
-def decode(method, H, rx, iterations):
-    """general_work's dispatch, :155-164."""
+def decode(method, H, rx, iterations, et_period=1):
+    """general_work's dispatch, :155-164.  et_period > 1 thins the early-exit
+    test to iterations it with (it + 1) % et_period == 0 (SURVEY 8(d) config 5;
+    1 = the reference)."""
     if method == 3:
         return decode_hard(rx)
     if method == 2:
-        return decode_bitflip(H, rx, iterations)
+        return decode_bitflip(H, rx, iterations, et_period)
     if method == 1:
-        return decode_sumproduct(H, rx, iterations)
-    return decode_minsum(H, rx, iterations)
+        return decode_sumproduct(H, rx, iterations, et_period)
+    return decode_minsum(H, rx, iterations, et_period)

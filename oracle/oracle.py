@@ -43,6 +43,17 @@ def lib():
                                        _f32p, ctypes.c_long, ctypes.c_int, ctypes.c_float,
                                        ctypes.c_int, _u8p, _u8p, _i32p, _i32p, _f32p, ctypes.c_int]
         L.orc_decode_batch.restype = ctypes.c_int
+        L.orc_decode_batch_et.argtypes = [ctypes.c_int, _u8p, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, _f32p, ctypes.c_long,
+                                          ctypes.c_int, ctypes.c_float, ctypes.c_int, _u8p, _u8p,
+                                          _i32p, _i32p, _f32p, ctypes.c_int]
+        L.orc_decode_batch_et.restype = ctypes.c_int
+        L.orc_decode_batch_sparse_et.argtypes = [ctypes.c_int, _i32p, _i32p, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p,
+                                                 ctypes.c_long, ctypes.c_int, ctypes.c_float,
+                                                 ctypes.c_int, _u8p, _u8p, _i32p, _i32p,
+                                                 ctypes.c_int]
+        L.orc_decode_batch_sparse_et.restype = ctypes.c_int
         L.orc_decode_batch_sparse.argtypes = [ctypes.c_int, _i32p, _i32p, ctypes.c_int,
                                               ctypes.c_int, ctypes.c_int, _f32p, ctypes.c_long,
                                               ctypes.c_int, ctypes.c_float, ctypes.c_int, _u8p,
@@ -114,9 +125,10 @@ def decode_one(method, Hr, rx, iterations):
 
 
 def decode_batch(method, Hr, llr, iterations, polarity=1.0, nthreads=1, cw_stride=None,
-                 elem_stride=1, B=None, want_post=False):
+                 elem_stride=1, B=None, want_post=False, et_period=1):
     """Decode B frames of float32 samples.  Returns dict with bits (B,N) u8,
-    packed (B,KB) u8, iters (B,) i32, synd (B,) i32 [, post (B,N) f32]."""
+    packed (B,KB) u8, iters (B,) i32, synd (B,) i32 [, post (B,N) f32].
+    et_period > 1 thins the early-exit test (orc_decode_et; 1 = reference)."""
     Hr = np.ascontiguousarray(Hr, np.uint8)
     M, N = Hr.shape
     llr = np.ascontiguousarray(llr, np.float32)
@@ -130,10 +142,10 @@ def decode_batch(method, Hr, llr, iterations, polarity=1.0, nthreads=1, cw_strid
     iters = np.zeros(B, np.int32)
     synd = np.zeros(B, np.int32)
     post = np.zeros((B, N), np.float32) if want_post else None
-    lib().orc_decode_batch(int(method), _p(Hr, _u8p), M, N, int(iterations),
-                           _p(llr, _f32p), int(cw_stride), int(elem_stride), float(polarity),
-                           int(B), _p(bits, _u8p), _p(packed, _u8p), _p(iters, _i32p),
-                           _p(synd, _i32p), _p(post, _f32p), int(nthreads))
+    lib().orc_decode_batch_et(int(method), _p(Hr, _u8p), M, N, int(iterations), int(et_period),
+                              _p(llr, _f32p), int(cw_stride), int(elem_stride), float(polarity),
+                              int(B), _p(bits, _u8p), _p(packed, _u8p), _p(iters, _i32p),
+                              _p(synd, _i32p), _p(post, _f32p), int(nthreads))
     out = dict(bits=bits, packed=packed, iters=iters, synd=synd)
     if want_post:
         out["post"] = post
@@ -141,7 +153,8 @@ def decode_batch(method, Hr, llr, iterations, polarity=1.0, nthreads=1, cw_strid
 
 
 def decode_batch_sparse(method, row_ptr, col_idx, M, N, llr, iterations, polarity=1.0,
-                        nthreads=1, cw_stride=None, elem_stride=1, B=None, want_bits=True):
+                        nthreads=1, cw_stride=None, elem_stride=1, B=None, want_bits=True,
+                        et_period=1):
     """Sparse (CSR) restatement for large codes; same outputs as decode_batch."""
     rp = np.ascontiguousarray(row_ptr, np.int32)
     ci = np.ascontiguousarray(col_idx, np.int32)
@@ -155,11 +168,11 @@ def decode_batch_sparse(method, row_ptr, col_idx, M, N, llr, iterations, polarit
     packed = np.zeros((B, KB), np.uint8)
     iters = np.zeros(B, np.int32)
     synd = np.zeros(B, np.int32)
-    lib().orc_decode_batch_sparse(int(method), _p(rp, _i32p), _p(ci, _i32p), int(M), int(N),
-                                  int(iterations), _p(llr, _f32p), int(cw_stride),
-                                  int(elem_stride), float(polarity), int(B), _p(bits, _u8p),
-                                  _p(packed, _u8p), _p(iters, _i32p), _p(synd, _i32p),
-                                  int(nthreads))
+    lib().orc_decode_batch_sparse_et(int(method), _p(rp, _i32p), _p(ci, _i32p), int(M), int(N),
+                                     int(iterations), int(et_period), _p(llr, _f32p),
+                                     int(cw_stride), int(elem_stride), float(polarity), int(B),
+                                     _p(bits, _u8p), _p(packed, _u8p), _p(iters, _i32p),
+                                     _p(synd, _i32p), int(nthreads))
     out = dict(packed=packed, iters=iters, synd=synd)
     if want_bits:
         out["bits"] = bits
