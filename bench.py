@@ -7,24 +7,35 @@ already resident in HBM: B = 4096 frames of the reference's default 32x64 H
 the reference's per-frame early exit, Eb/N0 = 2 dB with the reference noise
 convention (sigma = sqrt(10^(-EbN0/10)), apps/ldpc_lapack.cpp:635-642).
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W] [--inflight D] [--strong]
 
-N > 1 runs under torch.distributed.run, one rank per GPU: each rank decodes
-its own batch (weak scaling, independent frames, no collective in the data
-path); after the timed loop RCCL all-gathers the packed outputs and
-all-reduces the counters (the "final throughput gather").  Rank 0 prints ONE
-JSON line.  `value` = info bits of all frames all ranks decoded / the max
-over ranks of the timed wall time.
+Data are made on the GPU before timing: Philox bits (ldpc_random_bits) ->
+systematic GF(2) encode (ldpc_encode_device) -> BPSK + AWGN
+(ldpc_bpsk_awgn); the first frames are cross-checked against the host
+encoder.  D distinct batches are made (D = --inflight, default 2): step k
+decodes batch k mod D on stream k mod D, so D batches are in flight -- the
+next batch's frames fill the SIMDs the previous batch's last long frames
+leave idle (a streaming receiver's steady state).  Every step decodes its
+whole batch; the single-batch latency (D = 1) is reported beside it.
 
-roofline.achieved uses SURVEY.md 8(d)'s algorithmic byte model per launch:
-  sum_b [4N (fp32 Re in) + KB + 8 (packed, iters, syndrome out)
-         + iters_b * (32E + 10N)]  (f64 parity mode; 16E + 6N for f32)
-divided by the kernel's mean duration: one HIP event pair on the launch
-stream around the K timed launches, divided by K.  roofline.traffic is the rocprofv3 PMC measurement
-(profiles/) per launch, when a matching entry exists.  roofline_valu: the
-bound that actually applies to the small-code kernel (messages never leave
-LDS/VGPRs): PMC VALU wave-instructions per launch / kernel time against the
-1024-SIMD issue peak.
+N > 1 runs under torch.distributed.run, one rank per GPU.  Weak scaling
+(default): every rank decodes its own B frames.  --strong: one global batch
+of B frames is split with ldpc_ece535a.dist.shard_range.  No collective runs
+in the data path; after the timed loop ldpc_ece535a.dist.gather_outputs
+all-gathers the packed outputs and all-reduces the counters over RCCL (the
+"final throughput gather"), and the max over ranks of the timed wall time is
+taken.  Rank 0 prints ONE JSON line; `value` = info bits of all frames all
+ranks decoded / that max.
+
+roofline (small-code path): the kernel keeps every edge message in LDS /
+VGPRs, so HBM does not bound it; f64 VALU issue does.  achieved = VALU issue
+cycles per launch (rocprofv3 PMC instruction counts, profiles/, weighted by
+the issue cost measured on gfx950 in profiles/round2/ubench_f64.txt: 4
+cycles per f64 add/mul/fma wave-instruction, 16 per f64 transcendental, 2
+per other VALU instruction) / the per-launch time; peak = 1024 SIMDs x
+2.4 GHz.  The SURVEY 8(d) byte model stays as a labelled secondary figure
+(equivalent streaming bandwidth).  Config 4 (--code dvbs2) is HBM-bound and
+uses the byte model against the 8 TB/s peak.
 cpu_baseline: the C oracle (oracle/, a dense double restatement of the
 reference decoder) decoding the same frames on the host's cores.
 """
@@ -41,22 +52,32 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 # LDPC_PKG_DIR: an alternative build of the package (tools/ab.sh A/B runs)
 sys.path.insert(0, os.environ.get("LDPC_PKG_DIR", os.path.join(REPO, "gr-ldpc_ece535a_amd")))
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SIMDS, CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMDs, max clock
+F64_PEAK_TFLOPS = 78.6         # MI355X FP64 vector spec
+# VALU issue cycles per wave64 instruction on gfx950 (profiles/round2/ubench_f64.txt)
+ISSUE_F64, ISSUE_TRANS64, ISSUE_OTHER = 4.0, 16.0, 2.0
+METRIC = "decoded info Mbit/s @ 50 BP iters, batch=4096; achieved HBM GB/s vs peak"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    # the first ~100-200 launches of a fresh process run ~7 % slower (clock settling,
-    # profiles/round1/warmup_dependence.txt); the default warmup covers them
+    # the first ~100-200 launches of a fresh process run slower while the clock
+    # ramps (profiles/round1/warmup_clock.txt); the default warmup covers them
     ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batches in flight (consecutive steps on alternating streams)")
+    ap.add_argument("--strong", action="store_true",
+                    help="N > 1: split one global batch over the ranks (default: weak scaling)")
     ap.add_argument("--code", choices=["default", "dvbs2"], default="default",
                     help="default: the reference's 32x64 H (config 2); dvbs2: the DVB-S2-size "
                          "code of config 4 (synthetic rate-1/2 address table)")
     ap.add_argument("--batch", type=int, default=None, help="default 4096 (1024 for dvbs2)")
     ap.add_argument("--method", type=int, default=None, help="default 1 (0 for dvbs2)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 variant")
+    ap.add_argument("--no-block", action="store_true", help="skip the block-throughput variant")
     ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--et-period", type=int, default=1)
@@ -66,127 +87,170 @@ def parse():
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--waves-per-cu", type=int, default=0)
-    ap.add_argument("--sweep-wpc", default="", help="comma list; prints a table to stderr")
-    ap.add_argument("--sweep-batch", default="",
-                    help="comma list of B: latency/throughput sweep (config 5) to stderr")
     ap.add_argument("--schedule", type=int, default=0, help="0 auto, 1 wave/frame, 2 workgroup/frame")
-    ap.add_argument("--sweep-schedules", default="0", help="comma list for --sweep-batch")
+    ap.add_argument("--sweep-batch", default="",
+                    help="comma list of B: latency/throughput sweep to stderr")
+    ap.add_argument("--sweep-inflight", default="",
+                    help="comma list of in-flight depths: per-batch time table to stderr")
     ap.add_argument("--sweep-modes", default="1:f64,1:f32,0:f64",
                     help="method:precision list for the sweeps")
     ap.add_argument("--sweep-config5", default="",
                     help="comma list of B: config 5 (syndrome check every 5 iterations, mixed "
                          "Eb/N0 0..4 dB per frame) latency/throughput table to stderr")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_counters.json"))
+    return ap.parse_args(argv)
 
 
-def synth_csr(csr, B, ebn0, seed):
-    """Config 4: PCG64 info bits, IRA encode (ldpc_ece535a.codes), BPSK, AWGN."""
-    from ldpc_ece535a import codes
-    M, N = csr[0], csr[1]
-    rng = np.random.Generator(np.random.PCG64(seed))
-    data = rng.integers(0, 2, size=(B, N - M), dtype=np.uint8)
-    cw = codes.ira_encode(csr, data)
-    sigma = np.sqrt(10.0 ** (-ebn0 / 10.0))
-    y = (2.0 * cw.astype(np.float64) - 1.0 + sigma * rng.standard_normal((B, N)))
-    return y.astype(np.float32), data
+# --------------------------------------------------------------------------
+# synthetic data
+# --------------------------------------------------------------------------
+def sigma_of(ebn0):
+    """The reference's noise convention (apps/ldpc_lapack.cpp:629-636)."""
+    return float(np.sqrt(10.0 ** (-ebn0 / 10.0)))
 
 
-def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
-    """DVB-S2-like N=64800 code, min-sum f64, 1024 frames (config 4) on the
-    large-code path; optional parity of the first frames vs the sparse oracle."""
-    from ldpc_ece535a import codes
-    csr = codes.dvbs2_like(0)
-    dec = L.Decoder(csr=csr, device=dev.index or 0)
-    B = 1024
-    y, data = synth_csr(csr, B, args.ebn0, seed)
-    d_y = torch.from_numpy(y).to(dev)
-    out = {}
-    for name, p in (("f64", 0), ("f32", 1)):
-        w, k, it, o = time_decoder(dec, torch, d_y, B, 0, args.iters, 1, p, steps, warmup)
-        alg = float(B * (4 * dec.N + dec.KB + 8) + it.sum() * bytes_per_iter(dec.E, dec.N, p))
-        pk = o[0].cpu().numpy()
-        out["min-sum " + name] = {
-            "Mbit/s": round(B * dec.K * steps / w / 1e6, 2), "ms_per_decode": round(k, 4),
-            "mean_iters": round(float(it.mean()), 3), "max_iters": int(it.max()),
-            "alg_GB/s": round(alg / (k * 1e-3) / 1e9, 1),
-            "frames_decoded_to_sent_data": int((pk == np.packbits(data, axis=1)).all(axis=1).sum())}
-        if p == 0 and cpu_sample:
-            from oracle import oracle as orc
-            t0 = time.perf_counter()
-            ref = orc.decode_batch_sparse(0, csr[2], csr[3], csr[0], csr[1], y[:cpu_sample],
-                                          args.iters, nthreads=16, want_bits=False)
-            cpu_s = time.perf_counter() - t0
-            out["min-sum f64"]["parity_sample"] = {
-                "frames": cpu_sample,
-                "packed_mismatch_frames": int((ref["packed"] != pk[:cpu_sample]).any(axis=1).sum()),
-                "iters_mismatch_frames": int((ref["iters"] != it[:cpu_sample]).sum()),
-                "checker": "oracle sparse restatement (orc_decode_batch_sparse)",
-                "cpu_Mbit/s_16_threads": round(cpu_sample * dec.K / cpu_s / 1e6, 4)}
-    out["code"] = ("DVB-S2-like N=64800 K=32400 E=226799 (synthetic rate-1/2 address table, "
-                   "ldpc_ece535a.codes.dvbs2_like(0)), B=1024, %d-iteration cap" % args.iters)
-    dec.close()
-    return out
-
-
-def synth(Hr, B, ebn0, seed):
-    """Seeded frames: data ~ Bernoulli(1/2) (PCG64), GF(2) encode through the
-    product's ldpc_encode, BPSK 1->+1, AWGN with the reference sigma."""
-    import ldpc_ece535a as L
-    M, N = Hr.shape
-    rng = np.random.Generator(np.random.PCG64(seed))
-    data = rng.integers(0, 2, size=(B, N - M), dtype=np.uint8)
-    cw = L.encode(Hr, data)
-    sigma = np.sqrt(10.0 ** (-ebn0 / 10.0))
-    y = (2.0 * cw.astype(np.float64) - 1.0 + sigma * rng.standard_normal((B, N)))
-    return y.astype(np.float32), data
+def synth_device(L, torch, dec, B, ebn0, seed, dev, check_frames=64):
+    """Frames made on the GPU: Philox bits -> ldpc_encode_device -> BPSK +
+    AWGN.  ebn0 may be a scalar or a per-frame array (config 5).  Returns
+    (device float32 (B, N), device data bits (B, K)).  The first
+    check_frames codewords are compared with the host encoder."""
+    K, N = dec.K, dec.N
+    # one explicit (non-null) stream for every step: a NULL stream argument
+    # would mean the context's own stream for ldpc_encode_device
+    st = torch.cuda.Stream(dev)
+    sp = ctypes.c_void_p(st.cuda_stream)
+    with torch.cuda.stream(st):
+        d_bits = torch.empty((B, K), dtype=torch.uint8, device=dev)
+        d_cw = torch.empty((B, N), dtype=torch.uint8, device=dev)
+        d_y = torch.empty((B, N), dtype=torch.float32, device=dev)
+        if B == 0:
+            return d_y, d_bits
+        L.random_bits(d_bits.data_ptr(), B * K, seed, sp)
+        dec.encode_device(d_bits.data_ptr(), B, d_cw.data_ptr(), sp)
+        if np.ndim(ebn0) == 0:
+            L.bpsk_awgn(d_cw.data_ptr(), B * N, sigma_of(ebn0), seed * 2 + 1, d_y.data_ptr(), sp)
+        else:  # unit-variance noise, scaled per frame
+            L.bpsk_awgn(d_cw.data_ptr(), B * N, 1.0, seed * 2 + 1, d_y.data_ptr(), sp)
+            x = 2.0 * d_cw.to(torch.float32) - 1.0
+            s = torch.from_numpy(np.sqrt(10.0 ** (-np.asarray(ebn0, np.float64) / 10.0))
+                                 .astype(np.float32)).to(dev)[:, None]
+            d_y = x + (d_y - x) * s
+    st.synchronize()
+    n = min(B, check_frames)
+    if n:
+        bits = d_bits[:n].cpu().numpy()
+        cw = d_cw[:n].cpu().numpy()
+        if dec.N <= 4096:  # small enough for the dense host encoder
+            host = L.encode(dec.H, bits)
+        else:  # large codes: the IRA / DVB-S2 accumulator encoder
+            from ldpc_ece535a import codes
+            host = codes.ira_encode((dec.M, dec.N, dec.row_ptr, dec.col_idx), bits)
+        if not (host == cw).all():
+            raise RuntimeError("device encoder disagrees with the host encoder")
+        if not (cw[:, dec.M:] == bits).all():
+            raise RuntimeError("systematic part of the device codewords is not the data")
+    return d_y, d_bits
 
 
 def bytes_per_iter(E, N, prec):
     return 32 * E + 10 * N if prec == 0 else 16 * E + 6 * N
 
 
-def time_decoder(dec, torch, d_in, B, method, iters, et, prec, steps, warmup, dist=None):
-    """Returns (wall_s, mean_kernel_ms, per-frame iters, outputs).
-
-    One HIP event pair on the launch stream brackets the K timed launches;
-    mean_kernel_ms = that span / K (it includes the short gaps between
-    back-to-back launches, so it is slightly conservative).  Per-launch event
-    records are avoided: they perturb the launches they bracket (measured:
-    +5 % per step)."""
-    dev = d_in.device
-    d_packed = torch.empty((B, dec.KB), dtype=torch.uint8, device=dev)
-    d_iters = torch.empty(B, dtype=torch.int32, device=dev)
-    d_synd = torch.empty(B, dtype=torch.int32, device=dev)
-    # a dedicated (non-null) stream: the kernel and the timing events share it
-    stream = torch.cuda.Stream(dev)
-    sp = ctypes.c_void_p(stream.cuda_stream)
-
-    def step():
-        dec.decode_device(d_in.data_ptr(), B, d_packed.data_ptr(), method=method, max_iters=iters,
-                          et_period=et, precision=prec, d_iters=d_iters.data_ptr(),
-                          d_synd=d_synd.data_ptr(), stream=sp)
-
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+# --------------------------------------------------------------------------
+# timing (shared with tests/test_bench_dist.py, which runs it on the CPU)
+# --------------------------------------------------------------------------
+def timed_steps(step, steps, warmup, sync, dist=None):
+    """W untimed steps, then exactly K timed steps bracketed by a barrier
+    and a device synchronize on both sides.  Returns the wall time (s)."""
+    for k in range(warmup):
+        step(k)
+    sync()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(steps):
-        step()
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
+    for k in range(steps):
+        step(warmup + k)
+    sync()
     if dist is not None:
         dist.barrier()
-    wall = time.perf_counter() - t0
-    kern_ms = e0.elapsed_time(e1) / max(1, steps)
-    return wall, kern_ms, d_iters.cpu().numpy(), (d_packed, d_iters, d_synd)
+    return time.perf_counter() - t0
 
 
+def reduce_results(dist, packed, counters, wall, device=None):
+    """The final throughput gather: all-gather the packed outputs
+    (ldpc_ece535a.dist.gather_outputs), all-reduce the counters, max of the
+    wall times.  Single process: returned as is."""
+    if dist is None:
+        return packed, [float(c) for c in counters], wall
+    import torch
+    from ldpc_ece535a.dist import gather_outputs
+    full, c = gather_outputs(dist, packed, counters, device)
+    dev = packed.device if device is None else device
+    w = torch.tensor([float(wall)], dtype=torch.float64, device=dev)
+    dist.all_reduce(w, op=dist.ReduceOp.MAX)
+    return full, c, float(w.item())
+
+
+def plan_batch(B, world, rank, strong):
+    """Frames this rank decodes: (offset in the global batch, count).  Weak
+    scaling: every rank its own B frames; strong: shard_range of one B."""
+    if not strong or world == 1:
+        return rank * B, B
+    from ldpc_ece535a.dist import shard_range
+    lo, hi = shard_range(B, rank, world)
+    return lo, hi - lo
+
+
+def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, dist=None,
+                 inflight=1):
+    """Decode `steps` batches with `inflight` batches in flight: step k
+    decodes inputs[k % D] on stream k % D into that stream's output buffers.
+    Returns dict(wall, span_ms, per_launch_ms, iters, outs) where span_ms is
+    the device time from the first launch's start (a HIP event on stream 0,
+    which the other streams wait for) to the last launch's end (one event per
+    stream) and per_launch_ms = span_ms / steps.  outs[d] = (packed, iters,
+    synd) of the last decode of batch d."""
+    D = max(1, inflight)
+    dev = inputs[0].device
+    streams = [torch.cuda.Stream(dev) for _ in range(D)]
+    sps = [ctypes.c_void_p(s.cuda_stream) for s in streams]
+    outs = [(torch.empty((B, dec.KB), dtype=torch.uint8, device=dev),
+             torch.empty(B, dtype=torch.int32, device=dev),
+             torch.empty(B, dtype=torch.int32, device=dev)) for _ in range(D)]
+
+    def step(k):
+        d = k % D
+        pk, it, sy = outs[d]
+        dec.decode_device(inputs[d % len(inputs)].data_ptr(), B, pk.data_ptr(), method=method,
+                          max_iters=iters, et_period=et, precision=prec, d_iters=it.data_ptr(),
+                          d_synd=sy.data_ptr(), stream=sps[d])
+
+    e0 = torch.cuda.Event(enable_timing=True)
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(D)]
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    marks = {}
+
+    def timed_step(k):
+        if k == warmup:  # first timed step: start event, every stream waits on it
+            e0.record(streams[0])
+            for s in streams[1:]:
+                s.wait_event(e0)
+        step(k)
+        if k == warmup + steps - 1:
+            for s, e in zip(streams, ends):
+                e.record(s)
+            marks["done"] = True
+
+    wall = timed_steps(timed_step, steps, warmup, sync, dist)
+    span = max(e0.elapsed_time(e) for e in ends) if marks else 0.0
+    return dict(wall=wall, span_ms=span, per_launch_ms=span / max(1, steps),
+                iters=outs[0][1].cpu().numpy(), outs=outs)
+
+
+# --------------------------------------------------------------------------
+# measurement helpers
+# --------------------------------------------------------------------------
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -195,6 +259,151 @@ def cpu_model():
     except OSError:
         pass
     return "unknown CPU"
+
+
+def physical_cores(cpus):
+    """Distinct (package, core) pairs among the given logical CPUs."""
+    seen = set()
+    for c in cpus:
+        base = "/sys/devices/system/cpu/cpu%d/topology/" % c
+        try:
+            seen.add((open(base + "physical_package_id").read().strip(),
+                      open(base + "core_id").read().strip()))
+        except OSError:
+            return None
+    return len(seen)
+
+
+def cpu_share():
+    """(threads to use, logical CPUs visible).  The GPU box grants each GPU a
+    CPU share and exports it as OMP_NUM_THREADS (16 per GPU) while
+    sched_getaffinity shows the whole machine; the share is used."""
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except AttributeError:
+        visible = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    n = int(share) if share and share.isdigit() and int(share) > 0 else visible
+    return max(1, min(n, visible)), visible
+
+
+def load_pmc(path, key):
+    try:
+        return json.load(open(path)).get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def valu_roofline(pmc, per_launch_ms):
+    """VALU issue-cycle roofline from PMC instruction counts per launch."""
+    f64 = sum(pmc.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                         "SQ_INSTS_VALU_FMA_F64"))
+    trans = pmc.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+    other = max(0.0, pmc["SQ_INSTS_VALU"] - f64 - trans)
+    cycles = ISSUE_F64 * f64 + ISSUE_TRANS64 * trans + ISSUE_OTHER * other
+    peak = SIMDS * CLOCK_HZ / 1e9
+    ach = cycles / (per_launch_ms * 1e-3) / 1e9
+    flop = 64.0 * (2.0 * pmc.get("SQ_INSTS_VALU_FMA_F64", 0.0) +
+                   pmc.get("SQ_INSTS_VALU_ADD_F64", 0.0) + pmc.get("SQ_INSTS_VALU_MUL_F64", 0.0))
+    return {"bound": "valu", "achieved": round(ach, 1), "peak": peak,
+            "unit": "G SIMD-cycles/s of VALU issue (f64-weighted)", "frac": round(ach / peak, 4),
+            "issue_cycles_per_launch": round(cycles),
+            "f64_tflops": round(flop / (per_launch_ms * 1e-3) / 1e12, 2),
+            "f64_tflops_frac": round(flop / (per_launch_ms * 1e-3) / 1e12 / F64_PEAK_TFLOPS, 4),
+            "weights": "issue cycles per wave64 instruction: f64 add/mul/fma %g, f64 "
+                       "transcendental %g, other VALU %g (profiles/round2/ubench_f64.txt)"
+                       % (ISSUE_F64, ISSUE_TRANS64, ISSUE_OTHER)}
+
+
+class _quiet_stdout:
+    """The block prints the reference's sync messages on stdout
+    (lib/ldpc_decoder_cb_impl.cc:171-200); keep them out of the JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        null = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(null, 1)
+        os.close(null)
+
+    def __exit__(self, *exc):
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
+def block_variant(L, torch, blocks, dev, args, d_y, B):
+    """The drop-in block's own throughput: ldpc_decoder_cb (method 1, 50
+    iterations, f64) general_work over a stream of gr_complex frames in host
+    memory, as a GNU Radio scheduler drives it (lib/ldpc_decoder_cb_impl.cc:
+    133-234): one call per B-frame chunk, input consumed, packed bytes out."""
+    out = {}
+    for name, ebn0 in (("in-sync stream (4 dB)", 4.0), ("2 dB stream (sync losses)", 2.0)):
+        dec = L.Decoder(device=dev.index or 0)
+        y, _ = synth_device(L, torch, dec, B, ebn0, args.seed + 77, dev, check_frames=0)
+        dec.close()
+        stream = np.zeros(2 * y.numel(), np.float32)
+        stream[0::2] = y.cpu().numpy().ravel()
+        cx = stream.view(np.complex64)
+        blk = blocks.ldpc_decoder_cb(1, iterations=args.iters, precision=0, device=dev.index or 0)
+        reps = 4
+        pos, made, calls = 0, 0, 0
+        blk.general_work(B * 4, cx[:64 * 8])  # acquire sync on the first frames
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            pos = 0
+            while pos + 64 <= cx.size:
+                o, used = blk.general_work(B * 4, cx[pos:])
+                pos += used
+                made += o.size
+                calls += 1
+                if used == 0:
+                    break
+        dt = time.perf_counter() - t0
+        out[name] = {"Mbit/s": round(made * 8 / dt / 1e6, 2), "calls": calls,
+                     "ms_per_call": round(dt / max(1, calls) * 1e3, 4),
+                     "frames_decoded": int(blk.frames_decoded), "bytes_out": int(made)}
+    return out
+
+
+def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
+    """DVB-S2-like N=64800 code, min-sum, 1024 frames (config 4) on the
+    large-code path; optional parity of the first frames vs the sparse oracle."""
+    from ldpc_ece535a import codes
+    csr = codes.dvbs2_like(0)
+    dec = L.Decoder(csr=csr, device=dev.index or 0)
+    B = 1024
+    d_y, d_bits = synth_device(L, torch, dec, B, args.ebn0, seed, dev)
+    data = d_bits.cpu().numpy()
+    out = {}
+    for name, p in (("f64", 0), ("f32", 1)):
+        r = time_decoder(dec, torch, [d_y], B, 0, args.iters, 1, p, steps, warmup)
+        it = r["iters"]
+        k = r["per_launch_ms"]
+        alg = float(B * (4 * dec.N + dec.KB + 8) + it.sum() * bytes_per_iter(dec.E, dec.N, p))
+        pk = r["outs"][0][0].cpu().numpy()
+        out["min-sum " + name] = {
+            "Mbit/s": round(B * dec.K * steps / r["wall"] / 1e6, 2), "ms_per_decode": round(k, 4),
+            "mean_iters": round(float(it.mean()), 3), "max_iters": int(it.max()),
+            "alg_GB/s": round(alg / (k * 1e-3) / 1e9, 1),
+            "frames_decoded_to_sent_data": int((pk == np.packbits(data, axis=1)).all(axis=1).sum())}
+        if p == 0 and cpu_sample:
+            from oracle import oracle as orc
+            y = d_y[:cpu_sample].cpu().numpy()
+            threads, _ = cpu_share()
+            t0 = time.perf_counter()
+            ref = orc.decode_batch_sparse(0, csr[2], csr[3], csr[0], csr[1], y, args.iters,
+                                          nthreads=threads, want_bits=False)
+            cpu_s = time.perf_counter() - t0
+            out["min-sum f64"]["parity_sample"] = {
+                "frames": cpu_sample,
+                "packed_mismatch_frames": int((ref["packed"] != pk[:cpu_sample]).any(axis=1).sum()),
+                "iters_mismatch_frames": int((ref["iters"] != it[:cpu_sample]).sum()),
+                "checker": "oracle sparse restatement (orc_decode_batch_sparse)",
+                "cpu_Mbit/s": round(cpu_sample * dec.K / cpu_s / 1e6, 4), "cpu_threads": threads}
+    out["code"] = ("DVB-S2-like N=64800 K=32400 E=226799 (synthetic rate-1/2 address table, "
+                   "ldpc_ece535a.codes.dvbs2_like(0)), B=1024, %d-iteration cap" % args.iters)
+    dec.close()
+    return out
 
 
 def relaunch_distributed(args):
@@ -211,6 +420,47 @@ def relaunch_distributed(args):
     return subprocess.call(cmd)
 
 
+def sweeps(L, torch, dec, args, dev):
+    modes = [(int(m.split(":")[0]), 0 if m.split(":")[1] == "f64" else 1)
+             for m in args.sweep_modes.split(",")]
+    if args.sweep_batch:
+        for Bs in [int(x) for x in args.sweep_batch.split(",")]:
+            d_y, _ = synth_device(L, torch, dec, Bs, args.ebn0, args.seed + 17, dev)
+            for m, p in modes:
+                r = time_decoder(dec, torch, [d_y], Bs, m, args.iters, args.et_period, p,
+                                 args.steps, args.warmup)
+                k0, it0 = r["per_launch_ms"], r["iters"]
+                print("sweepB method=%d prec=%d B=%6d ebn0=%g mean_it=%6.2f max_it=%2d "
+                      "kernel_ms=%8.4f Mbit/s=%9.2f" %
+                      (m, p, Bs, args.ebn0, it0.mean(), it0.max(), k0,
+                       Bs * dec.K / (k0 * 1e-3) / 1e6), file=sys.stderr, flush=True)
+    if args.sweep_inflight:
+        B = args.batch
+        ins = [synth_device(L, torch, dec, B, args.ebn0, args.seed + 300 + j, dev)[0]
+               for j in range(8)]
+        for m, p in modes:
+            for D in [int(x) for x in args.sweep_inflight.split(",")]:
+                r = time_decoder(dec, torch, ins, B, m, args.iters, args.et_period, p,
+                                 args.steps, args.warmup, inflight=D)
+                print("inflight method=%d prec=%d D=%d ms_per_batch=%8.4f Mbit/s=%9.2f" %
+                      (m, p, D, r["wall"] / args.steps * 1e3,
+                       B * dec.K * args.steps / r["wall"] / 1e6), file=sys.stderr, flush=True)
+    if args.sweep_config5:
+        # config 5: et_period 5, each frame at its own Eb/N0 drawn from {0,1,2,3,4} dB
+        for Bs in [int(x) for x in args.sweep_config5.split(",")]:
+            rng = np.random.Generator(np.random.PCG64(args.seed + 5))
+            dbs = rng.integers(0, 5, size=Bs).astype(np.float64)
+            d_y, _ = synth_device(L, torch, dec, Bs, dbs, args.seed + 100, dev)
+            for m, p in ((1, 0), (1, 1), (0, 0)):
+                r = time_decoder(dec, torch, [d_y], Bs, m, args.iters, 5, p, args.steps,
+                                 args.warmup)
+                k0, it0 = r["per_launch_ms"], r["iters"]
+                print("config5 method=%d prec=%d B=%7d et=5 mean_it=%6.2f max_it=%2d "
+                      "latency_ms=%8.4f Mbit/s=%9.2f" % (m, p, Bs, it0.mean(), it0.max(), k0,
+                                                          Bs * dec.K / (k0 * 1e-3) / 1e6),
+                      file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -222,13 +472,11 @@ def main():
     import ldpc_ece535a as L
 
     dist = None
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         dist = tdist
-    else:
-        torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     prec = 0 if args.precision == "f64" else 1
     dvb = args.code == "dvbs2"
@@ -236,6 +484,7 @@ def main():
         args.method = 0 if dvb else 1
     if args.batch is None:
         args.batch = 1024 if dvb else 4096
+    D = max(1, args.inflight)
 
     csr = None
     if dvb:
@@ -248,103 +497,40 @@ def main():
         dec.set_waves_per_cu(args.waves_per_cu)
         dec.set_schedule(args.schedule)
         Hr = dec.H
-    B = args.batch
-    if dvb:
-        llr, data = synth_csr(csr, B, args.ebn0, args.seed + 7919 * rank)
-    else:
-        llr, data = synth(Hr, B, args.ebn0, args.seed + 7919 * rank)
-    d_in = torch.from_numpy(llr).to(dev)  # resident in HBM before timing
+    offset, B = plan_batch(args.batch, world, rank, args.strong)
+    # D distinct batches per rank, made on the GPU, resident in HBM before timing
+    inputs = [synth_device(L, torch, dec, B, args.ebn0, args.seed + 7919 * rank + 104729 * j,
+                           dev)[0] for j in range(D)]
+    torch.cuda.synchronize(dev)
+    sweeps(L, torch, dec, args, dev)
 
-    if args.sweep_batch:
-        modes = [(int(m.split(":")[0]), 0 if m.split(":")[1] == "f64" else 1)
-                 for m in args.sweep_modes.split(",")]
-        for Bs in [int(x) for x in args.sweep_batch.split(",")]:
-            y, _ = synth(Hr, Bs, args.ebn0, args.seed + 17)
-            d_y = torch.from_numpy(y).to(dev)
-            for sched in [int(x) for x in args.sweep_schedules.split(",")]:
-                dec.set_schedule(sched)
-                for m, p in modes:
-                    w0, k0, it0, _ = time_decoder(dec, torch, d_y, Bs, m, args.iters,
-                                                  args.et_period, p, args.steps, args.warmup)
-                    print("sweepB sched=%d method=%d prec=%d B=%6d ebn0=%g mean_it=%6.2f "
-                          "max_it=%2d kernel_ms=%8.4f Mbit/s=%9.2f us/iter(max-frame)=%7.3f" %
-                          (sched, m, p, Bs, args.ebn0, it0.mean(), it0.max(), k0,
-                           Bs * dec.K / (k0 * 1e-3) / 1e6, k0 * 1e3 / max(1, it0.max())),
-                          file=sys.stderr, flush=True)
-            dec.set_schedule(args.schedule)
-
-    if args.sweep_config5:
-        # config 5: et_period 5, each frame at its own Eb/N0 drawn from {0,1,2,3,4} dB
-        for Bs in [int(x) for x in args.sweep_config5.split(",")]:
-            rng = np.random.Generator(np.random.PCG64(args.seed + 5))
-            dbs = rng.integers(0, 5, size=Bs)
-            parts = []
-            for db in range(5):
-                n = int((dbs == db).sum())
-                parts.append(synth(Hr, n, float(db), args.seed + 100 + db)[0] if n else
-                             np.zeros((0, Hr.shape[1]), np.float32))
-            y = np.zeros((Bs, Hr.shape[1]), np.float32)
-            for db in range(5):
-                y[dbs == db] = parts[db]
-            d_y = torch.from_numpy(y).to(dev)
-            for m, p in ((1, 0), (1, 1), (0, 0)):
-                w0, k0, it0, _ = time_decoder(dec, torch, d_y, Bs, m, args.iters, 5, p,
-                                              args.steps, args.warmup)
-                print("config5 method=%d prec=%d B=%7d et=5 mean_it=%6.2f max_it=%2d "
-                      "latency_ms=%8.4f Mbit/s=%9.2f" % (m, p, Bs, it0.mean(), it0.max(), k0,
-                                                          Bs * dec.K / (k0 * 1e-3) / 1e6),
-                      file=sys.stderr, flush=True)
-
-    if args.sweep_wpc:
-        for m, p in ((args.method, prec), (1, 1), (0, 0)):
-            for wpc in [int(x) for x in args.sweep_wpc.split(",")]:
-                dec.set_waves_per_cu(wpc)
-                w0, k0, it0, _ = time_decoder(dec, torch, d_in, B, m, args.iters,
-                                              args.et_period, p, args.steps, args.warmup)
-                print("sweep method=%d prec=%d wpc=%2d kernel_ms=%.4f wall_ms/step=%.4f" %
-                      (m, p, wpc, k0, w0 / args.steps * 1e3), file=sys.stderr, flush=True)
-        dec.set_waves_per_cu(args.waves_per_cu)
-
-    wall, kern_ms, iters_b, outs = time_decoder(dec, torch, d_in, B, args.method, args.iters,
-                                                args.et_period, prec, args.steps, args.warmup,
-                                                dist)
-    packed = outs[0].cpu().numpy()
-    synd = outs[2].cpu().numpy()
-
-    # ---- final gather (RCCL): outputs to every rank + counters ------------
-    totals = np.array([B, B * dec.K, int(iters_b.sum()), int((synd > 0).sum())], np.float64)
-    wall_max = wall
-    if dist is not None:
-        g = [torch.empty_like(outs[0]) for _ in range(world)]
-        dist.all_gather(g, outs[0])
-        t = torch.tensor(totals, device=dev)
-        dist.all_reduce(t)
-        totals = t.cpu().numpy()
-        w = torch.tensor([wall], device=dev, dtype=torch.float64)
-        dist.all_reduce(w, op=dist.ReduceOp.MAX)
-        wall_max = float(w.item())
+    r = time_decoder(dec, torch, inputs, B, args.method, args.iters, args.et_period, prec,
+                     args.steps, args.warmup, dist, inflight=D)
+    wall = r["wall"]
+    iters_b = [o[1].cpu().numpy() for o in r["outs"]]
+    synd_b = [o[2].cpu().numpy() for o in r["outs"]]
+    # per step: batch k % D; counters over the K timed steps
+    steps_of = [len(range(j, args.steps, D)) for j in range(D)]
+    counters = [sum(steps_of[j] * B for j in range(D)),
+                sum(steps_of[j] * B * dec.K for j in range(D)),
+                sum(steps_of[j] * int(iters_b[j].sum()) for j in range(D)),
+                sum(steps_of[j] * int((synd_b[j] > 0).sum()) for j in range(D))]
+    full, totals, wall_max = reduce_results(dist, r["outs"][0][0], counters, wall, dev)
 
     if rank != 0:
         dist.destroy_process_group()
         return
 
-    frames_all = totals[0] * args.steps
-    info_bits = totals[1] * args.steps
+    frames_all, info_bits = totals[0], totals[1]
     value = info_bits / wall_max / 1e6
+    per_launch_ms = wall_max / args.steps * 1e3
+    mean_it = totals[2] / max(1.0, frames_all)
     E, N = dec.E, dec.N
-    alg_bytes = float(B * (4 * N + dec.KB + 8) + iters_b.sum() * bytes_per_iter(E, N, prec))
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = None
-    workload_key = "%s%d_%s_b%d_i%d_db%g" % ("dvb" if dvb else "sp", args.method, args.precision, B,
-                                            args.iters, args.ebn0)
-    try:
-        tj = json.load(open(args.traffic_json))
-        if workload_key in tj:
-            traffic = tj[workload_key]["hbm_bytes_per_launch"]
-            pmc = tj[workload_key].get("pmc")
-    except (OSError, ValueError, KeyError):
-        pass
+    alg_bytes = float(B * (4 * N + dec.KB + 8) + mean_it * B * bytes_per_iter(E, N, prec))
+    workload_key = "%s%d_%s_b%d_i%d_db%g" % ("dvb" if dvb else "sp", args.method, args.precision,
+                                            args.batch, args.iters, args.ebn0)
+    pmc = load_pmc(args.pmc_json, workload_key)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
 
     mname = {0: "min-sum", 1: "sum-product", 2: "bit-flip", 3: "hard"}[args.method]
     if dvb:
@@ -353,58 +539,74 @@ def main():
                     "method %d (%s), %d-iteration cap with per-frame early exit, Eb/N0 %g dB"
                     % (B, args.method, mname, args.iters, args.ebn0))
     else:
-        workload = ("config2: reference default 32x64 H (reordered), B=%d frames/GPU, "
-                    "method %d (%s), %d-iteration cap with per-frame early exit, "
-                    "Eb/N0 %g dB" % (B, args.method, mname, args.iters, args.ebn0))
+        workload = ("config2: reference default 32x64 H (reordered), B=%d frames%s, method %d "
+                    "(%s), %d-iteration cap with per-frame early exit, Eb/N0 %g dB"
+                    % (args.batch, " split over the ranks" if args.strong and world > 1
+                       else "/GPU", args.method, mname, args.iters, args.ebn0))
     line = {
-        "metric": "decoded info Mbit/s @ 50 BP iters, batch=4096; achieved HBM GB/s vs peak",
+        "metric": METRIC,
         "value": round(value, 3),
         "unit": "Mbit/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+        "ms_per_step": round(per_launch_ms, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong and world > 1 else "weak",
         "vs_baseline": None,
         "dtype": args.precision,
-        "data": "synthetic (PCG64 bits, GF(2) encode, BPSK, AWGN sigma=sqrt(10^(-EbN0/10)))",
+        "data": "synthetic, made on the GPU: Philox bits, GF(2) systematic encode "
+                "(ldpc_encode_device), BPSK, AWGN sigma=sqrt(10^(-EbN0/10))",
         "config": {
             "workload": workload,
-            "global_batch": int(totals[0]),
+            "global_batch": args.batch * (1 if args.strong else world),
             "frames_per_gpu": B,
+            "batches_in_flight": D,
             "parallelism": "dp%d (independent frames)" % world,
-            "mean_iters": round(float(iters_b.mean()), 3),
-            "syndrome_fail_frac": round(float((synd > 0).mean()), 4),
+            "mean_iters": round(mean_it, 3),
+            "syndrome_fail_frac": round(totals[3] / max(1.0, frames_all), 4),
             "et_period": args.et_period,
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "kernel_ms": round(kern_ms, 5),
-            "model": "SURVEY 8(d) algorithmic bytes per launch = %d" % int(alg_bytes),
-            "label": ("equivalent streaming bandwidth: the small-code kernel keeps every message "
-                      "in LDS/VGPRs (traffic = measured HBM bytes per launch); roofline_valu is "
-                      "the bound that applies") if not dvb else "HBM-resident messages",
-        },
     }
-    if pmc and "SQ_INSTS_VALU" in pmc and not dvb:
-        # The small-code kernel keeps every message in LDS / VGPRs (traffic is
-        # ~0.2 % of the byte model), so HBM does not bound it: VALU issue does.
-        # achieved = PMC VALU wave-instructions per launch (profiles/) / the
-        # live kernel time; peak = 1024 SIMDs x 2.4 GHz / 4 cycles per wave64
-        # VALU instruction (f64 FMA is full rate on gfx950).
-        valu_peak = 256 * 4 * 2.4e9 / 4 / 1e9
-        valu_ach = pmc["SQ_INSTS_VALU"] / (kern_ms * 1e-3) / 1e9
-        line["roofline_valu"] = {
-            "bound": "valu", "achieved": round(valu_ach, 1), "peak": valu_peak,
-            "unit": "G wave-instr/s", "frac": round(valu_ach / valu_peak, 4),
-            "f64_fma_per_launch": pmc.get("SQ_INSTS_VALU_FMA_F64"),
-            "source": "SQ_INSTS_VALU per launch from the rocprofv3 PMC pass (profiles/pmc_traffic.json)"}
+    hbm_model = {
+        "achieved_equiv_GB/s": round(alg_bytes / (per_launch_ms * 1e-3) / 1e9, 1),
+        "model_bytes_per_launch": int(alg_bytes),
+        "model": "SURVEY 8(d) algorithmic bytes: sum_b [4N + KB + 8 + iters_b (32E + 10N)] "
+                 "(f64; 16E + 6N f32)",
+        "traffic": traffic,
+    }
+    if dvb:
+        achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
+        line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                            "traffic": traffic, "model": hbm_model["model"]}
+    elif pmc and "SQ_INSTS_VALU" in pmc:
+        line["roofline"] = valu_roofline(pmc, per_launch_ms)
+        line["roofline"]["traffic"] = traffic
+        line["roofline"]["pmc_source"] = pmc.get("source")
+        hbm_model["label"] = ("equivalent streaming bandwidth of a decoder that streams its edge "
+                              "messages through HBM; this kernel keeps them on chip (traffic = "
+                              "measured HBM bytes per launch), so no HBM fraction applies")
+        line["hbm_byte_model"] = hbm_model
+    else:
+        line["roofline"] = {"bound": "valu", "achieved": None, "peak": SIMDS * CLOCK_HZ / 1e9,
+                            "unit": "G SIMD-cycles/s of VALU issue (f64-weighted)", "frac": None,
+                            "traffic": traffic,
+                            "note": "no PMC instruction counts for %s in %s" % (workload_key,
+                                                                              args.pmc_json)}
+        line["hbm_byte_model"] = hbm_model
+    line["timing"] = {"device_span_ms_per_launch": round(r["per_launch_ms"], 5),
+                      "wall_ms_per_step": round(per_launch_ms, 5),
+                      "note": "span = HIP events: start on stream 0 (other streams wait on it) "
+                              "to the last stream's end, / K"}
+
+    # ---- single batch in flight (latency per batch), same process ----------
+    if D > 1 and not args.no_variants:
+        r1 = time_decoder(dec, torch, inputs[:1], B, args.method, args.iters, args.et_period,
+                          prec, max(10, args.steps // 2), 5, inflight=1)
+        line["serial_1_batch_in_flight"] = {
+            "Mbit/s": round(B * dec.K * max(10, args.steps // 2) / r1["wall"] / 1e6, 2),
+            "latency_ms_per_batch": round(r1["per_launch_ms"], 5)}
 
     # ---- variants measured in the same process (not the headline) ----------
     variant_outs = {}
@@ -415,24 +617,28 @@ def main():
             if (m, p) == (args.method, prec):
                 continue
             st = max(5, args.steps // 2)
-            w2, k2, it2, o2 = time_decoder(dec, torch, d_in, B, m, args.iters, args.et_period, p,
-                                           st, 2)
-            alg2 = float(B * (4 * dec.N + dec.KB + 8) + it2.sum() * bytes_per_iter(dec.E, dec.N, p))
-            var[name] = {"Mbit/s": round(B * dec.K * st / w2 / 1e6, 2),
-                         "kernel_ms": round(k2, 5), "mean_iters": round(float(it2.mean()), 3),
-                         "alg_GB/s": round(alg2 / (k2 * 1e-3) / 1e9, 1)}
-            variant_outs[name] = (m, o2[0].cpu().numpy(), it2)
+            r2 = time_decoder(dec, torch, inputs, B, m, args.iters, args.et_period, p, st, 4,
+                              inflight=D)
+            it2 = r2["iters"]
+            var[name] = {"Mbit/s": round(B * dec.K * st / r2["wall"] / 1e6, 2),
+                         "ms_per_batch": round(r2["wall"] / st * 1e3, 5),
+                         "mean_iters": round(float(it2.mean()), 3)}
+            variant_outs[name] = (m, r2["outs"][0][0].cpu().numpy(), it2)
         line["variants_1gpu"] = var
+        if not args.no_block and world == 1:
+            from ldpc_ece535a import blocks
+            with _quiet_stdout():
+                var["block general_work (host buffers)"] = block_variant(L, torch, blocks, dev,
+                                                                         args, inputs[0], B)
 
     # ---- CPU baseline + parity (the oracle as checker) ----------------------
     if not args.no_cpu_baseline:
         sys.path.insert(0, REPO)
         from oracle import oracle as orc
-        try:
-            ncpu = len(os.sched_getaffinity(0))
-        except AttributeError:
-            ncpu = os.cpu_count() or 1
-        threads = args.cpu_threads or max(1, min(16, ncpu))
+        threads, visible = cpu_share()
+        threads = args.cpu_threads or threads
+        llr = inputs[0].cpu().numpy()
+        packed = r["outs"][0][0].cpu().numpy()
         if dvb:  # bounded sample: the sparse restatement on the first 128 frames
             nb = min(B, 128)
             t0 = time.perf_counter()
@@ -446,38 +652,45 @@ def main():
                           % (nb, B, threads, cpu_model())}
             line["parity"] = {"frames": nb,
                               "packed_mismatch_frames": int((ref["packed"] != packed[:nb]).any(axis=1).sum()),
-                              "iters_mismatch_frames": int((ref["iters"] != iters_b[:nb]).sum()),
+                              "iters_mismatch_frames": int((ref["iters"] != iters_b[0][:nb]).sum()),
                               "checker": "oracle sparse restatement (orc_decode_batch_sparse)"}
-            print(json.dumps(line), flush=True)
-            if dist is not None:
-                dist.destroy_process_group()
-            return
-        t0 = time.perf_counter()
-        ref = orc.decode_batch(args.method, Hr, llr, args.iters, nthreads=threads)
-        cpu_s = time.perf_counter() - t0
-        nsample = min(B, 128)
-        t1 = time.perf_counter()
-        orc.decode_batch(args.method, Hr, llr[:nsample], args.iters, nthreads=1)
-        cpu1_s = time.perf_counter() - t1
-        mism = int((ref["packed"] != packed).any(axis=1).sum()) if rank == 0 else None
-        line["cpu_baseline"] = {
-            "value": round(B * dec.K / cpu_s / 1e6, 5),
-            "unit": "Mbit/s",
-            "cores": threads,
-            "kind": "port",
-            "sample": "the same %d frames (rank 0's batch), %d threads on %s; 1-core: %.5f "
-                      "Mbit/s on the first %d frames" % (B, threads, cpu_model(),
-                                                          nsample * dec.K / cpu1_s / 1e6, nsample),
-        }
-        line["parity"] = {"frames": B, "packed_mismatch_frames": mism,
-                          "iters_mismatch_frames": int((ref["iters"] != iters_b).sum()),
-                          "checker": "oracle/ (C restatement of the reference decoder)"}
-        refs = {args.method: ref}
-        for name, (m, pk, it2) in variant_outs.items():
-            if m not in refs:
-                refs[m] = orc.decode_batch(m, Hr, llr, args.iters, nthreads=threads)
-            line["variants_1gpu"][name]["packed_mismatch_frames"] = int(
-                (refs[m]["packed"] != pk).any(axis=1).sum())
+        else:
+            t0 = time.perf_counter()
+            ref = orc.decode_batch(args.method, Hr, llr, args.iters, nthreads=threads,
+                                   et_period=args.et_period)
+            cpu_s = time.perf_counter() - t0
+            nsample = min(B, 256)
+            t1 = time.perf_counter()
+            orc.decode_batch(args.method, Hr, llr[:nsample], args.iters, nthreads=1,
+                             et_period=args.et_period)
+            cpu1 = nsample * dec.K / (time.perf_counter() - t1) / 1e6
+            phys = physical_cores(sorted(os.sched_getaffinity(0))) if hasattr(
+                os, "sched_getaffinity") else None
+            line["cpu_baseline"] = {
+                "value": round(B * dec.K / cpu_s / 1e6, 5),
+                "unit": "Mbit/s",
+                "cores": threads,
+                "kind": "port",
+                "sample": "the same %d frames (rank 0's first batch), %d threads (the GPU box's "
+                          "CPU share per GPU) on %s; 1 core: %.5f Mbit/s on the first %d frames; "
+                          "host: %d logical CPUs visible, %s physical cores" % (
+                              B, threads, cpu_model(), cpu1, nsample, visible, phys),
+                "one_core_Mbit/s": round(cpu1, 5),
+                "all_physical_cores_Mbit/s_linear_extrapolation":
+                    round(cpu1 * phys, 4) if phys else None,
+            }
+            line["parity"] = {"frames": B,
+                              "packed_mismatch_frames": int((ref["packed"] != packed).any(axis=1).sum()),
+                              "iters_mismatch_frames": int((ref["iters"] != iters_b[0]).sum()),
+                              "synd_mismatch_frames": int((ref["synd"] != synd_b[0]).sum()),
+                              "checker": "oracle/ (C restatement of the reference decoder)"}
+            refs = {args.method: ref}
+            for name, (m, pk, it2) in variant_outs.items():
+                if m not in refs:
+                    refs[m] = orc.decode_batch(m, Hr, llr, args.iters, nthreads=threads,
+                                               et_period=args.et_period)
+                line["variants_1gpu"][name]["packed_mismatch_frames"] = int(
+                    (refs[m]["packed"] != pk).any(axis=1).sum())
     if not args.no_variants and not dvb and not args.no_config4:
         line.setdefault("variants_1gpu", {})["config4"] = config4_variant(
             L, torch, dev, args, args.seed + 31, cpu_sample=0 if args.no_cpu_baseline else 64)

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--kernel", default="decode_small_kernel")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--steps", type=int, default=0, help="timed launches at the end of the run")
+    ap.add_argument("--source", default=None, help="recorded in the json entry")
     ap.add_argument("--key", default=None)
     ap.add_argument("--per-decode", default=None,
                     help="large-code path: sum the traffic of every kernel whose name contains "
@@ -39,6 +41,16 @@ def main():
     for r in kt:
         durs[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     print("== kernel trace (ns) ==")
+    if a.steps:
+        # the last K dispatches of the kernel are the timed steps: their span
+        # (first start to last end) / K is the per-launch time bench.py reports
+        # (with D batches in flight a launch's own start-to-end is longer)
+        mine = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in kt
+                      if a.kernel in r["Kernel_Name"])[-a.steps:]
+        if mine:
+            res["span_ns_per_launch"] = (max(e for _, e in mine) - mine[0][0]) / len(mine)
+            print("timed launches: %d, span per launch %.1f ns" % (len(mine),
+                                                                   res["span_ns_per_launch"]))
     for k, v in sorted(durs.items(), key=lambda kv: -sum(kv[1])):
         print("%-90s n=%4d mean=%10.1f median=%10.1f" % (k[:90], len(v), statistics.mean(v),
                                                           statistics.median(v)))
@@ -53,7 +65,7 @@ def main():
             print("stats:", {k: r[k] for k in r if k in ("Name", "Calls", "AverageNs", "TotalDurationNs",
                                                            "Percentage")})
     counters = collections.defaultdict(list)
-    for p in ("pmc1", "pmc2", "pmc3", "pmc4"):
+    for p in ("pmc1", "pmc2", "pmc3", "pmc4", "pmc5"):
         for r in rows(os.path.join(a.dir, p, "**", "*counter_collection.csv")):
             if a.kernel in r["Kernel_Name"]:
                 counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -92,6 +104,8 @@ def main():
             allj = json.load(open(a.json))
         except (OSError, ValueError):
             allj = {}
+        if a.source:
+            res["source"] = a.source
         allj[a.key] = res
         json.dump(allj, open(a.json, "w"), indent=1, sort_keys=True)
 

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Collects the rocprofv3 evidence for the bench workload on the GPU box:
 #   1. --kernel-trace --stats (kernel durations)
-#   2. separate --pmc passes (SQ counters; FETCH_SIZE; WRITE_SIZE)
+#   2. separate --pmc passes (SQ instruction mix, LDS conflicts, waits;
+#      FETCH_SIZE; WRITE_SIZE), each within the per-block counter limits
 # Run from the repo root, via gpurun.  Output: gpurun_out/prof/<tag>/...
 # usage: tools/profile.sh <tag> [bench args...]
 set -o pipefail
@@ -19,7 +20,7 @@ run() {  # name, rocprof options...
   return $rc
 }
 run kt --kernel-trace --stats &&
-run pmc1 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE &&
-run pmc2 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_BRANCH &&
+run pmc1 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT &&
+run pmc2 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU GRBM_GUI_ACTIVE &&
 run pmc3 --kernel-trace --pmc FETCH_SIZE &&
 run pmc4 --kernel-trace --pmc WRITE_SIZE
