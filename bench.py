@@ -152,6 +152,19 @@ def synth_device(L, torch, dec, B, ebn0, seed, dev, check_frames=64):
     return d_y, d_bits
 
 
+def synth(Hr, B, ebn0, seed):
+    """Host-made frames (tests and tools): data ~ Bernoulli(1/2) (PCG64),
+    GF(2) encode through the product's ldpc_encode, BPSK 1->+1, AWGN with the
+    reference sigma.  Returns (float32 (B, N), data bits (B, K))."""
+    import ldpc_ece535a as L
+    M, N = Hr.shape
+    rng = np.random.Generator(np.random.PCG64(seed))
+    data = rng.integers(0, 2, size=(B, N - M), dtype=np.uint8)
+    cw = L.encode(Hr, data)
+    y = (2.0 * cw.astype(np.float64) - 1.0 + sigma_of(ebn0) * rng.standard_normal((B, N)))
+    return y.astype(np.float32), data
+
+
 def bytes_per_iter(E, N, prec):
     return 32 * E + 10 * N if prec == 0 else 16 * E + 6 * N
 

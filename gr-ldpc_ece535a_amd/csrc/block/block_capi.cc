@@ -2,6 +2,7 @@
 #include <ldpc_block.h>
 
 #include <exception>
+#include <stdexcept>
 #include <string>
 
 #include "ldpc_decoder_cb_impl.h"
@@ -43,6 +44,58 @@ ldpc_block *ldpc_decoder_cb_make(int method, int iterations, int precision, int 
     return nullptr;
   }
   return b;
+}
+
+ldpc_block *ldpc_decoder_cb_make_h(int method, int iterations, int precision, int device,
+                                   const uint8_t *H, int M, int N, int flags) {
+  ldpc_block *b = new ldpc_block();
+  if (guarded([&] {
+        if (!H) throw std::invalid_argument("ldpc_decoder_cb_make_h: null H");
+        b->dec = new ldpc_decoder_cb_impl(method, iterations, precision, device, H, M, N, flags);
+        return 0;
+      }) != 0) {
+    delete b;
+    return nullptr;
+  }
+  return b;
+}
+
+ldpc_block *ldpc_decoder_cb_make_csr(int method, int iterations, int precision, int device, int M,
+                                     int N, const int32_t *row_ptr, const int32_t *col_idx,
+                                     int flags) {
+  ldpc_block *b = new ldpc_block();
+  if (guarded([&] {
+        b->dec = new ldpc_decoder_cb_impl(method, iterations, precision, device, M, N, row_ptr,
+                                          col_idx, flags);
+        return 0;
+      }) != 0) {
+    delete b;
+    return nullptr;
+  }
+  return b;
+}
+
+ldpc_block *ldpc_decoder_cb_make_alist(int method, int iterations, int precision, int device,
+                                       const char *alist_path) {
+  ldpc_block *b = new ldpc_block();
+  if (guarded([&] {
+        if (!alist_path) throw std::invalid_argument("ldpc_decoder_cb_make_alist: null path");
+        b->dec = new ldpc_decoder_cb_impl(method, iterations, precision, device,
+                                          std::string(alist_path));
+        return 0;
+      }) != 0) {
+    delete b;
+    return nullptr;
+  }
+  return b;
+}
+
+int ldpc_decoder_cb_frame_shape(const ldpc_block *blk, int *M, int *N, int *bytes_per_frame) {
+  if (!blk || !blk->dec) return -1;
+  if (M) *M = blk->dec->frame_checks();
+  if (N) *N = (int)blk->dec->frame_samples();
+  if (bytes_per_frame) *bytes_per_frame = blk->dec->frame_bytes();
+  return 0;
 }
 
 ldpc_block *ldpc_decoder_cb_make_with_backend(int method, int iterations,

@@ -35,6 +35,8 @@ struct ldpc_ctx {
   uint64_t *d_rowmask = nullptr;
   void *d_stage = nullptr;
   size_t stage_bytes = 0;
+  float *h_stage = nullptr;  // pinned host staging of host-buffer decodes
+  size_t h_stage_bytes = 0;
   // small-code frame queues: one monotonic counter per stream that has
   // launched on this context (ldpc_kernels.hpp DecodeArgs::ticket)
   uint32_t *d_tickets = nullptr;
@@ -227,6 +229,21 @@ int ensure_stage(ldpc_ctx *ctx, size_t bytes) {
   hipError_t e = hipMalloc(&ctx->d_stage, want);
   if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(staging)");
   ctx->stage_bytes = want;
+  return LDPC_OK;
+}
+
+int ensure_host_stage(ldpc_ctx *ctx, size_t bytes) {
+  if (bytes <= ctx->h_stage_bytes) return LDPC_OK;
+  if (ctx->h_stage) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipHostFree(ctx->h_stage);
+    ctx->h_stage = nullptr;
+    ctx->h_stage_bytes = 0;
+  }
+  size_t want = std::max(bytes, (size_t)1 << 20);
+  hipError_t e = hipHostMalloc((void **)&ctx->h_stage, want, hipHostMallocDefault);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipHostMalloc(staging)");
+  ctx->h_stage_bytes = want;
   return LDPC_OK;
 }
 
@@ -450,6 +467,99 @@ int ldpc_default_h(uint8_t *H_out) {
   return LDPC_OK;
 }
 
+// MacKay's alist format: "N M", "max_col_deg max_row_deg", the N column
+// degrees, the M row degrees, then per column its rows and per row its
+// columns (1-based), each list zero-padded to the maximum degree or not
+// padded at all (both forms are in use).  The row lists must agree with the
+// column lists.
+int ldpc_alist_read(const char *path, int *M_out, int *N_out, int32_t *row_ptr_opt,
+                    int32_t *col_idx_opt, int64_t col_idx_cap) {
+  if (!path || !M_out || !N_out) return set_err(nullptr, LDPC_EINVAL, "null argument");
+  FILE *f = fopen(path, "r");
+  if (!f) return set_err(nullptr, LDPC_EINVAL, std::string("cannot open ") + path);
+  std::vector<long> v;
+  long x;
+  while (fscanf(f, "%ld", &x) == 1) v.push_back(x);
+  const bool clean_eof = feof(f) != 0;
+  fclose(f);
+  if (!clean_eof) return set_err(nullptr, LDPC_EINVAL, "alist: non-numeric content");
+  if (v.size() < 4) return set_err(nullptr, LDPC_EINVAL, "alist: truncated header");
+  const long N = v[0], M = v[1], dvm = v[2], dcm = v[3];
+  if (N <= 0 || M <= 0 || M >= N || N > (1L << 24) || dvm <= 0 || dcm <= 0 ||
+      v.size() < (size_t)(4 + N + M))
+    return set_err(nullptr, LDPC_EINVAL, "alist: bad header (need 0 < M < N)");
+  long sum_c = 0, sum_r = 0;
+  for (long i = 0; i < N; ++i) {
+    const long d = v[4 + i];
+    if (d < 0 || d > dvm) return set_err(nullptr, LDPC_EINVAL, "alist: bad column degree");
+    sum_c += d;
+  }
+  for (long j = 0; j < M; ++j) {
+    const long d = v[4 + N + j];
+    if (d < 0 || d > dcm) return set_err(nullptr, LDPC_EINVAL, "alist: bad row degree");
+    sum_r += d;
+  }
+  if (sum_c != sum_r) return set_err(nullptr, LDPC_EINVAL, "alist: degree sums differ");
+  const size_t head = 4 + N + M;
+  bool padded;
+  if (v.size() == head + (size_t)(N * dvm + M * dcm))
+    padded = true;
+  else if (v.size() == head + (size_t)(sum_c + sum_r))
+    padded = false;
+  else
+    return set_err(nullptr, LDPC_EINVAL, "alist: list length matches neither padded nor unpadded");
+  // column lists -> (row, col) pairs; row lists checked against them
+  std::vector<std::vector<int32_t>> rows(M);
+  size_t at = head;
+  for (long i = 0; i < N; ++i) {
+    const long d = v[4 + i], width = padded ? dvm : d;
+    for (long k = 0; k < width; ++k) {
+      const long r = v[at++];
+      if (k >= d) {
+        if (r != 0) return set_err(nullptr, LDPC_EINVAL, "alist: non-zero padding");
+        continue;
+      }
+      if (r < 1 || r > M) return set_err(nullptr, LDPC_EINVAL, "alist: row index out of range");
+      rows[r - 1].push_back((int32_t)i);
+    }
+  }
+  int64_t E = 0;
+  for (long j = 0; j < M; ++j) {
+    std::vector<int32_t> &c = rows[j];
+    std::sort(c.begin(), c.end());
+    if (std::adjacent_find(c.begin(), c.end()) != c.end())
+      return set_err(nullptr, LDPC_EINVAL, "alist: repeated entry");
+    const long d = v[4 + N + j], width = padded ? dcm : d;
+    if ((long)c.size() != d) return set_err(nullptr, LDPC_EINVAL, "alist: row degree mismatch");
+    std::vector<int32_t> listed;
+    for (long k = 0; k < width; ++k) {
+      const long cc = v[at++];
+      if (k >= d) {
+        if (cc != 0) return set_err(nullptr, LDPC_EINVAL, "alist: non-zero padding");
+        continue;
+      }
+      if (cc < 1 || cc > N) return set_err(nullptr, LDPC_EINVAL, "alist: column index out of range");
+      listed.push_back((int32_t)(cc - 1));
+    }
+    std::sort(listed.begin(), listed.end());
+    if (listed != c) return set_err(nullptr, LDPC_EINVAL, "alist: row and column lists disagree");
+    E += d;
+  }
+  *M_out = (int)M;
+  *N_out = (int)N;
+  if (row_ptr_opt) {
+    row_ptr_opt[0] = 0;
+    for (long j = 0; j < M; ++j) row_ptr_opt[j + 1] = row_ptr_opt[j] + (int32_t)rows[j].size();
+  }
+  if (col_idx_opt) {
+    if (col_idx_cap < E) return set_err(nullptr, LDPC_EINVAL, "alist: col_idx buffer too small");
+    int64_t o = 0;
+    for (long j = 0; j < M; ++j)
+      for (int32_t c : rows[j]) col_idx_opt[o++] = c;
+  }
+  return (int)E;
+}
+
 int ldpc_reorder_h(uint8_t *H, int M, int N, int32_t *chosen_opt) {
   if (!valid_h(H, M, N)) return LDPC_EINVAL;
   reorder_columns(H, M, N, chosen_opt, nullptr, nullptr);
@@ -633,6 +743,7 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->d_cols) (void)hipFree(ctx->d_cols);
   if (ctx->d_rowmask) (void)hipFree(ctx->d_rowmask);
   if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
     if (p) (void)hipFree(p);
@@ -734,9 +845,16 @@ int ldpc_set_work_limit(ldpc_ctx *ctx, int64_t bytes) {
   return LDPC_OK;
 }
 
-int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+}  // extern "C"
+
+namespace {
+
+// Enqueues one decode of device-resident frames.  pm_half > 0: B = 2 pm_half
+// and frames pm_half.. re-decode windows 0..pm_half-1 with -polarity
+// (DecodeArgs::pm_half), in the same launch on the small-code path.
+int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
                        const float *d_in, int64_t cw_stride, int elem_stride, float polarity,
-                       int B, uint8_t *d_out_packed, uint8_t *d_out_bits_opt,
+                       int B, int pm_half, uint8_t *d_out_packed, uint8_t *d_out_bits_opt,
                        int32_t *d_iters_used_opt, int32_t *d_syn_weight_opt,
                        float *d_llr_out_opt, void *hip_stream) {
   int rc = check_decode_args(ctx, method, max_iters, et_period, precision, B, elem_stride,
@@ -750,6 +868,7 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   a.elem_stride = elem_stride;
   a.polarity = polarity;
   a.B = B;
+  a.pm_half = 0;
   a.max_iters = max_iters;
   a.et_period = et_period;
   a.packed = d_out_packed;
@@ -769,13 +888,27 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
     if (ctx->graph_stream && ctx->graph_stream != st &&
         (e = hipStreamWaitEvent((hipStream_t)st, ctx->graph_done, 0)) != hipSuccess)
       return hip_err(ctx, e, "hipStreamWaitEvent");
-    rc = decode_graph(ctx, a, method, precision, st);
+    if (pm_half > 0) {  // the large-code passes run per polarity
+      ldpc::DecodeArgs n = a;
+      a.B = n.B = pm_half;
+      n.polarity = -polarity;
+      n.packed += (int64_t)pm_half * ctx->KB;
+      if (n.bits) n.bits += (int64_t)pm_half * ctx->N;
+      if (n.iters) n.iters += pm_half;
+      if (n.synd) n.synd += pm_half;
+      if (n.llr) n.llr += (int64_t)pm_half * ctx->N;
+      rc = decode_graph(ctx, a, method, precision, st);
+      if (rc == LDPC_OK) rc = decode_graph(ctx, n, method, precision, st);
+    } else {
+      rc = decode_graph(ctx, a, method, precision, st);
+    }
     if (rc != LDPC_OK) return rc;
     if ((e = hipEventRecord(ctx->graph_done, (hipStream_t)st)) != hipSuccess)
       return hip_err(ctx, e, "hipEventRecord");
     ctx->graph_stream = st;
     return LDPC_OK;
   }
+  a.pm_half = pm_half;
   // the stream's own frame-queue counter (ldpc_kernels.hpp DecodeArgs::ticket)
   size_t q = 0;
   while (q < ctx->queues.size() && ctx->queues[q].stream != st) ++q;
@@ -802,10 +935,14 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   return LDPC_OK;
 }
 
-int ldpc_decode_strided(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
-                        const float *in, int64_t n_in_floats, int64_t cw_stride, int elem_stride,
-                        float polarity, int B, uint8_t *out_packed, uint8_t *out_bits_opt,
-                        int32_t *iters_used_opt, int32_t *syn_weight_opt, float *llr_out_opt) {
+// Host-buffer decode (synchronous).  B_out = B (pm_half 0) or 2B (both
+// polarities).  The frames' samples are staged through a pinned buffer; for
+// an interleaved gr_complex stream (elem_stride 2, even cw_stride) only the
+// real parts are gathered and copied, and the kernel reads them densely.
+int decode_host_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+                     const float *in, int64_t n_in_floats, int64_t cw_stride, int elem_stride,
+                     float polarity, int B, bool both, uint8_t *out_packed, uint8_t *out_bits_opt,
+                     int32_t *iters_used_opt, int32_t *syn_weight_opt, float *llr_out_opt) {
   int rc = check_decode_args(ctx, method, max_iters, et_period, precision, B, elem_stride,
                              cw_stride);
   if (rc != LDPC_OK) return rc;
@@ -813,15 +950,22 @@ int ldpc_decode_strided(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   if (!in || !out_packed) return set_err(ctx, LDPC_EINVAL, "null buffer");
   const int64_t span = (int64_t)(B - 1) * cw_stride + (int64_t)(ctx->N - 1) * elem_stride + 1;
   if (span > n_in_floats) return set_err(ctx, LDPC_EINVAL, "input shorter than the frames read");
+  const bool re_only = elem_stride == 2 && cw_stride % 2 == 0;
+  const int64_t n_stage = re_only ? (span + 1) / 2 : span;
+  const int64_t cw = re_only ? cw_stride / 2 : cw_stride;
+  const int es = re_only ? 1 : elem_stride;
+  const int BO = both ? 2 * B : B;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t b_in = al((size_t)span * 4), b_pk = al((size_t)B * ctx->KB),
-               b_bits = out_bits_opt ? al((size_t)B * ctx->N) : 0,
-               b_it = iters_used_opt ? al((size_t)B * 4) : 0,
-               b_sy = syn_weight_opt ? al((size_t)B * 4) : 0,
-               b_llr = llr_out_opt ? al((size_t)B * ctx->N * 4) : 0;
+  const size_t b_in = al((size_t)n_stage * 4), b_pk = al((size_t)BO * ctx->KB),
+               b_bits = out_bits_opt ? al((size_t)BO * ctx->N) : 0,
+               b_it = iters_used_opt ? al((size_t)BO * 4) : 0,
+               b_sy = syn_weight_opt ? al((size_t)BO * 4) : 0,
+               b_llr = llr_out_opt ? al((size_t)BO * ctx->N * 4) : 0;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   rc = ensure_stage(ctx, b_in + b_pk + b_bits + b_it + b_sy + b_llr);
+  if (rc != LDPC_OK) return rc;
+  rc = ensure_host_stage(ctx, (size_t)n_stage * 4);
   if (rc != LDPC_OK) return rc;
   char *base = (char *)ctx->d_stage;
   float *d_in = (float *)base;
@@ -830,21 +974,26 @@ int ldpc_decode_strided(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   int32_t *d_it = iters_used_opt ? (int32_t *)(base + b_in + b_pk + b_bits) : nullptr;
   int32_t *d_sy = syn_weight_opt ? (int32_t *)(base + b_in + b_pk + b_bits + b_it) : nullptr;
   float *d_llr = llr_out_opt ? (float *)(base + b_in + b_pk + b_bits + b_it + b_sy) : nullptr;
-  if ((e = hipMemcpyAsync(d_in, in, (size_t)span * 4, hipMemcpyHostToDevice, ctx->stream)) !=
+  float *h = ctx->h_stage;
+  if (re_only)
+    for (int64_t i = 0; i < n_stage; ++i) h[i] = in[2 * i];
+  else
+    memcpy(h, in, (size_t)span * 4);
+  if ((e = hipMemcpyAsync(d_in, h, (size_t)n_stage * 4, hipMemcpyHostToDevice, ctx->stream)) !=
       hipSuccess)
     return hip_err(ctx, e, "hipMemcpyAsync(in)");
-  rc = ldpc_decode_device(ctx, method, max_iters, et_period, precision, d_in, cw_stride,
-                          elem_stride, polarity, B, d_pk, d_bits, d_it, d_sy, d_llr, ctx->stream);
+  rc = decode_device_impl(ctx, method, max_iters, et_period, precision, d_in, cw, es, polarity,
+                          BO, both ? B : 0, d_pk, d_bits, d_it, d_sy, d_llr, ctx->stream);
   if (rc != LDPC_OK) return rc;
   struct {
     void *dst;
     const void *src;
     size_t n;
-  } back[] = {{out_packed, d_pk, (size_t)B * ctx->KB},
-              {out_bits_opt, d_bits, (size_t)B * ctx->N},
-              {iters_used_opt, d_it, (size_t)B * 4},
-              {syn_weight_opt, d_sy, (size_t)B * 4},
-              {llr_out_opt, d_llr, (size_t)B * ctx->N * 4}};
+  } back[] = {{out_packed, d_pk, (size_t)BO * ctx->KB},
+              {out_bits_opt, d_bits, (size_t)BO * ctx->N},
+              {iters_used_opt, d_it, (size_t)BO * 4},
+              {syn_weight_opt, d_sy, (size_t)BO * 4},
+              {llr_out_opt, d_llr, (size_t)BO * ctx->N * 4}};
   for (auto &c : back)
     if (c.dst && (e = hipMemcpyAsync(c.dst, c.src, c.n, hipMemcpyDeviceToHost, ctx->stream)) !=
                      hipSuccess)
@@ -852,6 +1001,38 @@ int ldpc_decode_strided(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
     return hip_err(ctx, e, "hipStreamSynchronize");
   return LDPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+                       const float *d_in, int64_t cw_stride, int elem_stride, float polarity,
+                       int B, uint8_t *d_out_packed, uint8_t *d_out_bits_opt,
+                       int32_t *d_iters_used_opt, int32_t *d_syn_weight_opt,
+                       float *d_llr_out_opt, void *hip_stream) {
+  return decode_device_impl(ctx, method, max_iters, et_period, precision, d_in, cw_stride,
+                            elem_stride, polarity, B, 0, d_out_packed, d_out_bits_opt,
+                            d_iters_used_opt, d_syn_weight_opt, d_llr_out_opt, hip_stream);
+}
+
+int ldpc_decode_strided(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+                        const float *in, int64_t n_in_floats, int64_t cw_stride, int elem_stride,
+                        float polarity, int B, uint8_t *out_packed, uint8_t *out_bits_opt,
+                        int32_t *iters_used_opt, int32_t *syn_weight_opt, float *llr_out_opt) {
+  return decode_host_impl(ctx, method, max_iters, et_period, precision, in, n_in_floats,
+                          cw_stride, elem_stride, polarity, B, false, out_packed, out_bits_opt,
+                          iters_used_opt, syn_weight_opt, llr_out_opt);
+}
+
+int ldpc_decode_strided_both(ldpc_ctx *ctx, int method, int max_iters, int et_period,
+                             int precision, const float *in, int64_t n_in_floats,
+                             int64_t cw_stride, int elem_stride, float polarity, int B,
+                             uint8_t *out_packed, int32_t *syn_weight_opt) {
+  return decode_host_impl(ctx, method, max_iters, et_period, precision, in, n_in_floats,
+                          cw_stride, elem_stride, polarity, B, true, out_packed, nullptr,
+                          nullptr, syn_weight_opt, nullptr);
 }
 
 int ldpc_decode(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,

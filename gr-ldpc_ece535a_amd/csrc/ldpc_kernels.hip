@@ -627,6 +627,17 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
   wave_lds_sync();
 }
 
+// Frame b's first sample and polarity (DecodeArgs::pm_half: the second half
+// of a both-polarities launch re-reads the first half's windows negated).
+__device__ __forceinline__ const float *frame_src(const DecodeArgs &a, int64_t b, float &pol) {
+  pol = a.polarity;
+  if (a.pm_half > 0 && b >= a.pm_half) {
+    b -= a.pm_half;
+    pol = -pol;
+  }
+  return a.in + b * a.cw_stride;
+}
+
 // Persistent launch: `a.waves` waves; wave w decodes frame w, then frames
 // a.waves + ticket++ until the batch is exhausted.  Frames stop after 1..cap
 // iterations, so pulling work keeps every SIMD busy to the end instead of
@@ -709,7 +720,9 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
   float pf[NW];
   {
     const int64_t pb = (int64_t)a.waves + b;
-    const float *ps = a.in + (pb < a.B ? pb : b) * a.cw_stride;
+    float ppol;
+    const float *ps = frame_src(a, pb < a.B ? pb : b, ppol);
+    (void)ppol;  // the prefetch only pulls the samples into L2
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
       const int c = lane + 64 * q;
@@ -725,12 +738,12 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
 #endif
     // the frame's channel samples, one load per lane and 64-column slot
     // (coalesced); the samples past N are 0
-    float xin[NW];
-    const float *src = a.in + b * a.cw_stride;
+    float xin[NW], pol;
+    const float *src = frame_src(a, b, pol);
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
       const int c = lane + 64 * q;
-      xin[q] = c < code.N ? src[(int64_t)c * a.elem_stride] * a.polarity : 0.0f;
+      xin[q] = c < code.N ? src[(int64_t)c * a.elem_stride] * pol : 0.0f;
     }
     if constexpr (METHOD == 1) {
       bool bad = false;
@@ -833,13 +846,14 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
   int64_t b = blockIdx.x;
   while (b < a.B) {
     // channel samples, one private copy per wave (:149-153, :486)
-    const float *src = a.in + b * a.cw_stride;
+    float pol;
+    const float *src = frame_src(a, b, pol);
     Real post[NW];
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
       const int c = lane + 64 * q;
       float x = 0.0f;
-      if (c < N) x = src[(int64_t)c * a.elem_stride] * a.polarity;
+      if (c < N) x = src[(int64_t)c * a.elem_stride] * pol;
       rb[c] = -(Real)x;
       post[q] = (Real)x;
     }

@@ -57,6 +57,10 @@ struct DecodeArgs {
   int elem_stride;
   float polarity;
   int B;
+  // both polarities in one launch (the block's OUT_OF_SYNC search, :178-198):
+  // when pm_half > 0, frames b >= pm_half decode window b - pm_half with
+  // -polarity (B = 2 * pm_half)
+  int pm_half;
   int max_iters;
   int et_period;
   uint8_t *packed;           // B x KB

@@ -15,6 +15,9 @@
 #include <gnuradio/block.h>
 #include <ldpc_ece535a/api.h>
 
+#include <string>
+#include <vector>
+
 namespace gr {
 namespace ldpc_ece535a {
 
@@ -33,8 +36,23 @@ class LDPC_ECE535A_API ldpc_decoder_cb : virtual public gr::block {
   static sptr make(const int method);
 
   /*! Additive overload: iteration cap (the reference hard-codes 5) and
-   *  arithmetic precision (0 = f64 parity mode, 1 = f32). */
+   *  arithmetic precision (0 = f64 parity mode, 1 = f32, 2 = f64 with
+   *  glibc-identical tanh). */
   static sptr make(const int method, const int iterations, const int precision = 0);
+
+  /*! Additive overload: a runtime H in place of the compiled-in matrix
+   *  (lib/ldpc_decoder_cb_impl.cc:60-102).  H is M x N, row-major, one byte
+   *  per entry; reorderHMatrix is applied as the reference's constructor does
+   *  (:104-106).  Per frame N samples in, M/8 bytes (bits M.. of the decision)
+   *  out, frame-error threshold M/8 (:141-142); needs N - M >= 8 (M/8). */
+  static sptr make(const int method, const int iterations, const int precision,
+                   const std::vector<unsigned char> &H, const int M, const int N);
+
+  /*! Additive overload: H from a MacKay alist file.  Codes small enough for a
+   *  dense matrix (M N <= 2^22) are reordered like the reference's H; larger
+   *  ones are used as given (put the information columns last). */
+  static sptr make(const int method, const int iterations, const int precision,
+                   const std::string &alist_path);
 };
 
 }  // namespace ldpc_ece535a

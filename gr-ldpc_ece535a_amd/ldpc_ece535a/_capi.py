@@ -53,6 +53,9 @@ SIGNATURES = {
                                  _u8p, _u8p, _i32p, _i32p, _f32p]),
     "ldpc_decode_device": (_i, [_vp, _i, _i, _i, _i, _vp, _i64, _i, ctypes.c_float, _i,
                                 _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ldpc_decode_strided_both": (_i, [_vp, _i, _i, _i, _i, _f32p, _i64, _i64, _i,
+                                     ctypes.c_float, _i, _u8p, _i32p]),
+    "ldpc_alist_read": (_i, [ctypes.c_char_p, _i32p, _i32p, _i32p, _i32p, _i64]),
     "ldpc_set_waves_per_cu": (_i, [_vp, _i]),
     "ldpc_set_schedule": (_i, [_vp, _i]),
     "ldpc_synchronize": (_i, [_vp]),
@@ -213,6 +216,25 @@ class Decoder:
             out["llr"] = post
         return out
 
+    def decode_both(self, llr, method=METHOD_SUMPRODUCT, max_iters=50, et_period=1,
+                    precision=PREC_F64, polarity=1.0, cw_stride=None, elem_stride=1, B=None):
+        """ldpc_decode_strided_both: the B windows decoded at +polarity (rows
+        0..B-1) and -polarity (rows B..2B-1) in one launch.  Returns dict with
+        packed (2B,KB) and synd (2B,)."""
+        x = np.ascontiguousarray(llr, np.float32).reshape(-1)
+        if cw_stride is None:
+            cw_stride = self.N * elem_stride
+        if B is None:
+            B = x.size // cw_stride if cw_stride else 0
+        packed = np.zeros((2 * B, self.KB), np.uint8)
+        synd = np.zeros(2 * B, np.int32)
+        _check(lib().ldpc_decode_strided_both(self._ctx, int(method), int(max_iters),
+                                              int(et_period), int(precision), _p(x, _f32p),
+                                              x.size, int(cw_stride), int(elem_stride),
+                                              float(polarity), int(B), _p(packed, _u8p),
+                                              _p(synd, _i32p)), self._ctx)
+        return dict(packed=packed, synd=synd)
+
     def decode_device(self, d_in, B, d_packed, method=METHOD_SUMPRODUCT, max_iters=50,
                       et_period=1, precision=PREC_F64, polarity=1.0, cw_stride=None,
                       elem_stride=1, d_bits=None, d_iters=None, d_synd=None, d_llr=None,
@@ -244,6 +266,20 @@ class Decoder:
 
     def synchronize(self):
         _check(lib().ldpc_synchronize(self._ctx), self._ctx)
+
+
+def alist_read(path):
+    """ldpc_alist_read: a MacKay alist file as (M, N, row_ptr, col_idx)."""
+    M, N = ctypes.c_int32(0), ctypes.c_int32(0)
+    bpath = os.fsencode(path)
+    E = lib().ldpc_alist_read(bpath, ctypes.byref(M), ctypes.byref(N), None, None, 0)
+    if E < 0:
+        raise LdpcError("ldpc_alist_read(%s): %s" % (path, lib().ldpc_last_error(None).decode()))
+    rp = np.zeros(M.value + 1, np.int32)
+    ci = np.zeros(max(E, 1), np.int32)
+    _check(lib().ldpc_alist_read(bpath, ctypes.byref(M), ctypes.byref(N), _p(rp, _i32p),
+                                 _p(ci, _i32p), int(E)))
+    return M.value, N.value, rp, ci[:E]
 
 
 def random_bits(d_out, n, seed, stream=None):

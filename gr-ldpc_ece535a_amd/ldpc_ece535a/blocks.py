@@ -37,6 +37,10 @@ SIGNATURES = {
     "ldpc_decoder_cb_frames_decoded": (ctypes.c_int64, [_vp]),
     "ldpc_decoder_cb_destroy": (None, [_vp]),
     "ldpc_decoder_cb_make_with_backend": (_vp, [_i, _i, BACKEND_FN, _vp]),
+    "ldpc_decoder_cb_make_h": (_vp, [_i, _i, _i, _i, _u8p, _i, _i, _i]),
+    "ldpc_decoder_cb_make_csr": (_vp, [_i, _i, _i, _i, _i, _i, _i32p, _i32p, _i]),
+    "ldpc_decoder_cb_make_alist": (_vp, [_i, _i, _i, _i, ctypes.c_char_p]),
+    "ldpc_decoder_cb_frame_shape": (_i, [_vp, _i32p, _i32p, _i32p]),
     "ldpc_encoder_bc_make": (_vp, []),
     "ldpc_encoder_bc_forecast": (None, [_vp, _i, _i32p]),
     "ldpc_encoder_bc_general_work": (_i, [_vp, _i, _i, _u8p, _f32p, _i32p]),
@@ -70,14 +74,35 @@ class ldpc_decoder_cb:
     """LDPC decoder block: gr_complex in, packed bytes out.
 
     ldpc_decoder_cb(method) is the reference's make(method) (5 iterations,
-    f64 parity arithmetic); iterations/precision are additive options.
+    f64 parity arithmetic, the default 32x64 H); iterations / precision are
+    additive options, as is a runtime H: `H` (dense M x N, reorderHMatrix
+    applied as the reference's constructor does, unless reorder=False), `csr`
+    = (M, N, row_ptr, col_idx) used as given, or `alist` = a MacKay alist path.
     """
     in_itemsize = 8   # sizeof(gr_complex)
     out_itemsize = 1
 
-    def __init__(self, method=0, iterations=5, precision=0, device=0, _backend=None):
+    def __init__(self, method=0, iterations=5, precision=0, device=0, H=None, csr=None,
+                 alist=None, reorder=True, _backend=None):
         self._backend = None
-        if _backend is not None:
+        if H is not None:
+            H = np.ascontiguousarray(H, np.uint8)
+            self._h = lib().ldpc_decoder_cb_make_h(int(method), int(iterations), int(precision),
+                                                   int(device), H.ctypes.data_as(_u8p),
+                                                   H.shape[0], H.shape[1], 0 if reorder else 1)
+        elif csr is not None:
+            M, N, rp, ci = csr
+            rp = np.ascontiguousarray(rp, np.int32)
+            ci = np.ascontiguousarray(ci, np.int32)
+            self._h = lib().ldpc_decoder_cb_make_csr(int(method), int(iterations), int(precision),
+                                                     int(device), int(M), int(N),
+                                                     rp.ctypes.data_as(_i32p),
+                                                     ci.ctypes.data_as(_i32p), 0)
+        elif alist is not None:
+            self._h = lib().ldpc_decoder_cb_make_alist(int(method), int(iterations),
+                                                       int(precision), int(device),
+                                                       os.fsencode(alist))
+        elif _backend is not None:
             # TEST SEAM: host-logic tests only (see include/ldpc_block.h)
             self._backend = BACKEND_FN(_backend)
             self._h = lib().ldpc_decoder_cb_make_with_backend(int(method), int(iterations),
@@ -88,6 +113,10 @@ class ldpc_decoder_cb:
         if not self._h:
             raise LdpcError("ldpc_decoder_cb: %s" % _err())
         self.method = method
+        m, n, k = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        lib().ldpc_decoder_cb_frame_shape(self._h, ctypes.byref(m), ctypes.byref(n),
+                                          ctypes.byref(k))
+        self.M, self.N, self.frame_bytes = m.value, n.value, k.value
 
     def __del__(self):
         h = getattr(self, "_h", None)

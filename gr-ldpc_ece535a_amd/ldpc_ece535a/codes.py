@@ -113,3 +113,48 @@ def syndrome_weight(csr, bits):
         par = np.bincount(row_of, weights=bits[b, col_idx], minlength=M).astype(np.int64) & 1
         out[b] = par.sum()
     return out
+
+
+def alist_text(H=None, csr=None, padded=True):
+    """MacKay alist text of a dense H (M, N) or a CSR (M, N, row_ptr, col_idx):
+    "N M", the maximum column / row degrees, the degrees, then each column's
+    rows and each row's columns (1-based; zero-padded to the maximum degree
+    when `padded`)."""
+    if H is not None:
+        H = np.asarray(H, np.uint8)
+        M, N = H.shape
+        rows = [np.nonzero(H[j])[0] for j in range(M)]
+    else:
+        M, N, rp, ci = csr
+        rp = np.asarray(rp, np.int64)
+        ci = np.asarray(ci, np.int64)
+        rows = [np.sort(ci[rp[j]:rp[j + 1]]) for j in range(M)]
+    cols = [[] for _ in range(N)]
+    for j, r in enumerate(rows):
+        for c in r:
+            cols[int(c)].append(j)
+    dv = [len(c) for c in cols]
+    dc = [len(r) for r in rows]
+    dvm, dcm = max(dv), max(dc)
+
+    def line(v, width):
+        v = [int(x) + 1 for x in v]
+        if padded:
+            v += [0] * (width - len(v))
+        return " ".join(str(x) for x in v)
+    out = ["%d %d" % (N, M), "%d %d" % (dvm, dcm), " ".join(map(str, dv)), " ".join(map(str, dc))]
+    out += [line(c, dvm) for c in cols]
+    out += [line(r, dcm) for r in rows]
+    return "\n".join(out) + "\n"
+
+
+def write_alist(path, H=None, csr=None, padded=True):
+    with open(path, "w") as f:
+        f.write(alist_text(H=H, csr=csr, padded=padded))
+
+
+def read_alist(path):
+    """(M, N, row_ptr, col_idx) of a MacKay alist file, read by the C ABI's
+    ldpc_alist_read (include/ldpc_hip.h)."""
+    from ._capi import alist_read
+    return alist_read(path)

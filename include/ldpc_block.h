@@ -28,6 +28,27 @@ typedef struct ldpc_block ldpc_block;
 /* ldpc_decoder_cb::make(method) is ldpc_decoder_cb_make(method, 5, 0, 0). */
 ldpc_block *ldpc_decoder_cb_make(int method, int iterations, int precision, int device);
 
+/* Additive constructors with a runtime H (the reference compiles its H in,
+ * lib/ldpc_decoder_cb_impl.cc:60-102):
+ *   _make_h      dense M x N H (row-major bytes), reorderHMatrix applied as
+ *                the reference's constructor does (:104-106) unless flags has
+ *                LDPC_FLAG_NO_REORDER;
+ *   _make_csr    CSR H, used as given;
+ *   _make_alist  MacKay alist file (dense + reordered when M N <= 2^22, else
+ *                CSR as given).
+ * Per frame the block consumes N samples and emits M/8 bytes (bits M.. of the
+ * decision, :141, :209-219) with frame-error threshold M/8 (:142); an H with
+ * N - M < 8 (M/8) is rejected.  NULL on failure (ldpc_block_last_error()). */
+ldpc_block *ldpc_decoder_cb_make_h(int method, int iterations, int precision, int device,
+                                   const uint8_t *H, int M, int N, int flags);
+ldpc_block *ldpc_decoder_cb_make_csr(int method, int iterations, int precision, int device,
+                                     int M, int N, const int32_t *row_ptr,
+                                     const int32_t *col_idx, int flags);
+ldpc_block *ldpc_decoder_cb_make_alist(int method, int iterations, int precision, int device,
+                                       const char *alist_path);
+/* The block's code shape: M checks, N samples per frame, bytes out per frame. */
+int ldpc_decoder_cb_frame_shape(const ldpc_block *blk, int *M, int *N, int *bytes_per_frame);
+
 /* forecast: ninput_items_required[0] = noutput_items * N (:126-130). */
 void ldpc_decoder_cb_forecast(ldpc_block *blk, int noutput_items, int *ninput_items_required);
 

@@ -12,7 +12,7 @@
  *       lib/ldpc_decoder_cb_impl.cc:35-117 (H setup + reorderHMatrix :104-106);
  *       ldpc_create_csr takes H as a sparse row list, for codes whose dense
  *       M x N matrix the reference could not hold
- *   ldpc_decode, ldpc_decode_strided, ldpc_decode_device
+ *   ldpc_decode, ldpc_decode_strided, ldpc_decode_strided_both, ldpc_decode_device
  *       decodeLogDomainSimple :309-412, decodeSumProductSoft :478-557,
  *       decodeBitFlipping :414-476, decodeHard :559-572 and the early-exit
  *       checkFrame(vhat, 0) they call, dispatched as general_work :155-164;
@@ -22,6 +22,8 @@
  *   ldpc_check_frame        checkFrame :236-253
  *   ldpc_encode             makeParityCheck, lib/ldpc_encoder_bc_impl.cc:275-294
  *   ldpc_default_h          the hard-coded 32x64 H, lib/ldpc_decoder_cb_impl.cc:60-96
+ *   ldpc_alist_read         a runtime H source in place of the compiled-in matrices
+ *                           (lib/ldpc_decoder_cb_impl.cc:60-102, apps/test_data.h)
  *   ldpc_encode_device      makeParityCheck on the GPU (lib/ldpc_encoder_bc_impl.cc:275-294;
  *                           IRA accumulator codes for SURVEY config 4)
  *   ldpc_random_bits, ldpc_bpsk_awgn, ldpc_count_bit_errors
@@ -96,6 +98,16 @@ int ldpc_check_frame(const uint8_t *H, int M, int N, const uint8_t *bits,
 int ldpc_encode(const uint8_t *H_reordered, int M, int N,
                 const uint8_t *data_bits, int B, uint8_t *codewords_out);
 
+/* Reads a parity-check matrix in MacKay's alist format (column lists
+ * zero-padded to the maximum degree, or unpadded) as CSR: returns E (the
+ * number of ones) and M, N; row_ptr_opt (M+1) and col_idx_opt (E, capacity
+ * col_idx_cap) are filled when given -- call once with NULLs to size them.
+ * Negative return on a malformed file (ldpc_last_error(NULL) says why).
+ * Replaces the reference's compiled-in matrices (lib/ldpc_decoder_cb_impl.cc:
+ * 60-102, apps/test_data.h) as a runtime H source. */
+int ldpc_alist_read(const char *path, int *M_out, int *N_out, int32_t *row_ptr_opt,
+                    int32_t *col_idx_opt, int64_t col_idx_cap);
+
 /* ---- device context ----------------------------------------------- */
 
 /* Builds the decoder's view of H (reorderHMatrix unless
@@ -155,7 +167,9 @@ int ldpc_decode(ldpc_ctx *ctx, int method, int max_iters, int et_period,
                 int32_t *syn_weight_opt);
 
 /* Host buffers with the strided frame descriptor above; n_in_floats bounds
- * the input read.  Synchronous. */
+ * the input read.  Synchronous.  The samples go through a pinned staging
+ * buffer; for an interleaved gr_complex stream (elem_stride 2, even
+ * cw_stride) only the real parts are copied to the device. */
 int ldpc_decode_strided(ldpc_ctx *ctx, int method, int max_iters,
                         int et_period, int precision, const float *in,
                         int64_t n_in_floats, int64_t cw_stride,
@@ -163,6 +177,16 @@ int ldpc_decode_strided(ldpc_ctx *ctx, int method, int max_iters,
                         uint8_t *out_packed, uint8_t *out_bits_opt,
                         int32_t *iters_used_opt, int32_t *syn_weight_opt,
                         float *llr_out_opt);
+
+/* Both polarities in one launch (the block's OUT_OF_SYNC search, reference
+ * general_work :178-198): the B windows of the strided descriptor are decoded
+ * with tx = in * polarity into rows 0..B-1 and with tx = -in * polarity into
+ * rows B..2B-1 of out_packed (2B x KB) and syn_weight_opt (2B).  Synchronous. */
+int ldpc_decode_strided_both(ldpc_ctx *ctx, int method, int max_iters,
+                             int et_period, int precision, const float *in,
+                             int64_t n_in_floats, int64_t cw_stride,
+                             int elem_stride, float polarity, int B,
+                             uint8_t *out_packed, int32_t *syn_weight_opt);
 
 /* Device-resident buffers (already in HBM); enqueues on `hip_stream`
  * (hipStream_t, NULL = the context's own stream) and returns without

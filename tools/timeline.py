@@ -50,7 +50,8 @@ def main():
     if a.launches:
         show = {0, 1, 2, 5, 10, 20, 50, 100, 150, 200, 300, 400, 600, 800}
         for i in range(a.launches):
-            _, kms, _, _ = bench.time_decoder(dec, torch, d_in, B, a.method, 50, a.et, a.precision, 1, 0)
+            kms = bench.time_decoder(dec, torch, [d_in], B, a.method, 50, a.et, a.precision, 1,
+                                     0)["per_launch_ms"]
             torch.cuda.synchronize()
             if i in show or i == a.launches - 1:
                 assert lib.ldpc_debug_timeline(buf.ctypes.data_as(ctypes.c_void_p), B) == B
@@ -61,8 +62,8 @@ def main():
                 print("launch %4d: kernel %.4f ms, span %.1f us, in-kernel clock median %.3f GHz" %
                       (i, kms, (en.max() - st.min()) / 100.0, np.median(t[:, 3] / dur / 1e3)), flush=True)
         return
-    _, kern_ms, iters, _ = bench.time_decoder(dec, torch, d_in, a.batch, a.method, 50, a.et,
-                                              a.precision, 3, 2)
+    r = bench.time_decoder(dec, torch, [d_in], a.batch, a.method, 50, a.et, a.precision, 3, 2)
+    kern_ms, iters = r["per_launch_ms"], r["iters"]
     torch.cuda.synchronize()
     n = lib.ldpc_debug_timeline(buf.ctypes.data_as(ctypes.c_void_p), B)
     assert n == B, n
