@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -37,6 +38,8 @@ struct ldpc_ctx {
   size_t stage_bytes = 0;
   float *h_stage = nullptr;  // pinned host staging of host-buffer decodes
   size_t h_stage_bytes = 0;
+  int32_t *h_ctrl = nullptr;  // pinned progress words of the min-sum pipeline
+  bool ms_pipeline = true;    // large-code min-sum: compressed messages + pipeline
   // small-code frame queues: one monotonic counter per stream that has
   // launched on this context (ldpc_kernels.hpp DecodeArgs::ticket)
   uint32_t *d_tickets = nullptr;
@@ -359,6 +362,32 @@ ldpc::CodeView code_view(const ldpc_ctx *ctx) {
 int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int precision, void *st) {
   const ldpc::GraphView g = graph_view(ctx);
   const bool want_post = a.llr != nullptr;
+  if (method == 0 && ctx->ms_pipeline) {
+    // min-sum: compressed check messages, frames pipelined through S slots
+    const int S = std::min(ldpc::ms_default_slots(), (a.B + 63) / 64 * 64);
+    const size_t need = ldpc::ms_work_bytes(g, S, precision, want_post);
+    if (need > ctx->work_bytes) {
+      if (ctx->d_work) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ctx->d_work);
+        ctx->d_work = nullptr;
+        ctx->work_bytes = 0;
+      }
+      hipError_t e = hipMalloc(&ctx->d_work, need);
+      if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(graph workspace)");
+      ctx->work_bytes = need;
+    }
+    if (!ctx->h_ctrl) {
+      hipError_t e = hipHostMalloc((void **)&ctx->h_ctrl, 64, hipHostMallocDefault);
+      if (e != hipSuccess) return hip_err(ctx, e, "hipHostMalloc(ctrl)");
+    }
+    ldpc::MsWork w;
+    ldpc::ms_work_carve(w, ctx->d_work, g, S, precision, want_post);
+    const int rc = ldpc::launch_graph_decode_ms(g, w, a, precision, ctx->h_ctrl, st);
+    if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "code degrees outside the large-code kernels");
+    if (rc != 0) return hip_err(ctx, hipGetLastError(), "graph kernel launch");
+    return LDPC_OK;
+  }
   const size_t per64 = ldpc::graph_work_bytes(g, 64, precision, method, want_post);
   int group = (int)std::min<size_t>((size_t)1 << 30, std::max<size_t>(1, ctx->work_limit / per64) * 64);
   group = std::min(group, (a.B + 63) / 64 * 64);
@@ -668,6 +697,10 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     return nullptr;
   }
   ctx->device = device;
+  {  // A/B knob: LDPC_MS_PIPELINE=0 keeps large-code min-sum on the edge-message passes
+    const char *v = getenv("LDPC_MS_PIPELINE");
+    ctx->ms_pipeline = !(v && v[0] == '0');
+  }
   const char *what = nullptr;
   if ((e = hipSetDevice(device)) != hipSuccess) what = "hipSetDevice";
   if (!what && (e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
@@ -744,6 +777,7 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->d_rowmask) (void)hipFree(ctx->d_rowmask);
   if (ctx->d_stage) (void)hipFree(ctx->d_stage);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
     if (p) (void)hipFree(p);

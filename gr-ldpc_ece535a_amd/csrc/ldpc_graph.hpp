@@ -80,4 +80,32 @@ void graph_work_carve(GraphWork &w, void *base, const GraphView &g, int Bp, int 
 int launch_graph_decode(const GraphView &g, const GraphWork &w, const DecodeArgs &args,
                         int method, int prec, void *stream);
 
+// ---- min-sum with compressed check messages and a frame pipeline
+// (ldpc_graph_ms.hip) ------------------------------------------------------
+struct MsWork {
+  int S, chunks, check_waves;  // S slots (frames in flight), multiple of 64
+  float *L;          // N x S: Lci = -tx of the slot's frame
+  void *LQ;          // N x S Real: Lci + sum of the column's L(r)
+  void *m1, *m2;     // M x S Real: smallest / second smallest |L(q)| of the row
+  uint8_t *meta;     // M x S: (P + 1) << 6 | (i1 + 1)
+  uint64_t *alpha;   // (E x chunks) x 2: slots with L(q) < 0, slots with sign 0
+  uint64_t *hard;    // N x chunks: decisions, bit = slot
+  float *post;       // N x S: L(Q) (only with an llr output)
+  uint64_t *odd;     // check waves x chunks: rows seen unsatisfied
+  int32_t *it;       // S: iterations the slot's frame has executed
+  int32_t *frame;    // S: the slot's frame (-1: empty)
+  int32_t *nxt;      // S: frame after this pass's refill
+  int32_t *used;     // S: iterations of a frame that stopped this pass
+  uint64_t *live_w, *run_w, *stop_w, *fill_w, *cap_w;  // per-chunk lane masks
+  int32_t *ctrl;     // [0] next frame of the batch, [1] frames finished
+};
+
+int ms_default_slots();
+size_t ms_work_bytes(const GraphView &g, int S, int prec, bool want_post);
+void ms_work_carve(MsWork &w, void *base, const GraphView &g, int S, int prec, bool want_post);
+// Min-sum decode of args.B frames through S slots; waits on the device between
+// rounds of passes (h_ctrl: 4 ints of pinned host memory).  0, -2 or -1.
+int launch_graph_decode_ms(const GraphView &g, const MsWork &w, const DecodeArgs &args, int prec,
+                           int32_t *h_ctrl, void *stream);
+
 }  // namespace ldpc

@@ -1,0 +1,489 @@
+// ldpc_graph_ms.hip -- min-sum on large codes with
+// compressed check messages and a frame pipeline.
+//
+// The reference's horizontal step (lib/ldpc_decoder_cb_impl.cc:350-376) gives
+// every edge of row j the message
+//     L(r_ji) = (double)(P_j * alpha_ji) * (i == i1_j ? m2_j : m1_j)
+// where alpha = sign(L(q)) (sign(0) = sign(NaN) = 0), P_j = prod of the
+// row's alphas, m1 / m2 = the smallest / second smallest |L(q)| of the row
+// (strict <, first occurrence, DBL_MAX seeds, NaN never taken) and i1 the
+// position of m1.  So a row's messages are exactly recoverable from
+// {m1, m2, i1, P} plus one 2-bit alpha per edge, and the vertical step's
+// L(q_ij) = (Lci + s) - L(r_ji) (:387-392) is LQ_i - L(r_ji) with
+// LQ_i = Lci + s (:395).  This path stores per 64-frame chunk
+//   LQ (N) and Lci (N, float: -tx is a float),
+//   m1, m2 (M), meta (M bytes: P+1 in bits 6-7, i1+1 in bits 0-5),
+//   alpha (2 words per edge: lanes with L(q) < 0, lanes with sign 0),
+// instead of the edge messages L(q) and L(r) (2 E values), and recomputes
+// L(q) in the check pass and L(r) in the variable pass, operation for
+// operation as the reference.  Per frame-iteration that is ~17 M + 12 N
+// bytes plus 2 bits per edge of state instead of 16 E -- small enough that a
+// few chunks' state stays in the 256 MiB Infinity Cache between the passes.
+//
+// Frame pipeline: S slots (a few 64-frame chunks) are in flight; every pass
+// advances each running slot by one iteration; a slot whose frame stops
+// (early exit under the reference's rule, or the cap) writes that frame's
+// outputs and loads the next frame of the batch.  Per pass:
+//   ms_check   one wave = 4 rows x 64 slots: syndrome parities of the last
+//              decisions, L(q) = LQ - L(r_old), the row state of the new L(r)
+//   ms_decide  one block per chunk: stop / run / refill per slot
+//   ms_flush   packed bytes, iterations (+ bits / posteriors) of stopped frames
+//   ms_synd    syndrome weight of frames stopped at the cap (uncapped checkFrame)
+//   ms_var     one wave = 4 columns x 64 slots: L(r) from the row states,
+//              s = sum L(r) ascending rows, LQ = Lci + s, vhat = LQ < 0
+//   ms_refill  channel values of the frames the freed slots take
+// A slot refilled in pass p runs its first horizontal step in pass p+1.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include <stdlib.h>
+
+#include "ldpc_device.hpp"
+#include "ldpc_graph.hpp"
+
+namespace ldpc {
+namespace {
+
+constexpr int kMsRows = 4;  // check rows per wave
+constexpr int kMsCols = 4;  // columns per wave
+
+__device__ __forceinline__ int wave_id() {
+  return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+__device__ __forceinline__ uint64_t lane_bit(uint64_t w, int lane) { return (w >> lane) & 1ull; }
+__device__ __forceinline__ int64_t at(int64_t x, int k, int64_t n, int lane) {
+  return ((int64_t)k * n + x) * 64 + lane;
+}
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// alpha of an edge for this lane from its two words
+__device__ __forceinline__ int alpha_of(uint64_t neg, uint64_t zero, int lane) {
+  return lane_bit(zero, lane) ? 0 : (lane_bit(neg, lane) ? -1 : 1);
+}
+
+// ---------------------------------------------------------------------------
+template <int PREC, int DC>
+__global__ void __launch_bounds__(256) ms_check(GraphView g, MsWork w) {
+  typedef typename Math<PREC>::Real Real;
+  const int k = blockIdx.y;
+  if (!w.live_w[k]) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t chunks = w.chunks;
+  const bool fresh = w.it[k * 64 + lane] == 0;  // first horizontal step: L(q) = Lci
+  const Real *LQ = (const Real *)w.LQ;
+  Real *m1 = (Real *)w.m1, *m2 = (Real *)w.m2;
+  const int wg = blockIdx.x * 4 + wave_id();
+  const int j0 = wg * kMsRows;
+  const int j1 = min(j0 + kMsRows, g.M);
+  uint64_t odd = 0;  // checkFrame (:236-253) of the last decisions, 64 slots per word
+  for (int j = j0; j < j1; ++j) {
+    uint64_t par = 0;
+    const int e1 = g.rp[j + 1];
+    for (int e = g.rp[j]; e < e1; ++e) par ^= w.hard[(int64_t)g.ci[e] * chunks + k];
+    odd |= par;
+  }
+  for (int j = j0; j < j1; ++j) {
+    const int e0 = g.rp[j], d = g.rp[j + 1] - e0;
+    const int64_t ro = at(j, k, g.M, lane);
+    const Real om1 = m1[ro], om2 = m2[ro];
+    const int omt = w.meta[ro];
+    const int oP = (omt >> 6) - 1, oi1 = (omt & 63) - 1;
+    Real q[DC];
+#pragma unroll
+    for (int t = 0; t < DC; ++t) {
+      if (t < d) {
+        const Real lq = LQ[at(g.ci[e0 + t], k, g.N, lane)];
+        const uint64_t *aw = w.alpha + ((int64_t)(e0 + t) * chunks + k) * 2;
+        const int al = alpha_of(aw[0], aw[1], lane);
+        // the previous L(r) of the edge (:376), then L(q) = LQ - L(r) (:387-392)
+        const Real r = fresh ? Real(0) : (Real)(oP * al) * (t == oi1 ? om2 : om1);
+        q[t] = lq - r;
+      } else {
+        q[t] = Real(0);
+      }
+    }
+    // horizontal step (:340-376): sign product, smallest and second smallest
+    // |L(q)| with the reference's strict < (NaN never passes)
+    int P = 1, i1 = -1;
+    Real a1 = Math<PREC>::max_(), a2 = Math<PREC>::max_();
+#pragma unroll
+    for (int t = 0; t < DC; ++t)
+      if (t < d) {
+        P *= sgn(q[t]);
+        const Real a = Math<PREC>::abs_(q[t]);
+        if (a < a1) {
+          a2 = a1;
+          a1 = a;
+          i1 = t;
+        } else if (a < a2) {
+          a2 = a;
+        }
+      }
+    m1[ro] = a1;
+    m2[ro] = a2;
+    w.meta[ro] = (uint8_t)(((P + 1) << 6) | (i1 + 1));
+#pragma unroll
+    for (int t = 0; t < DC; ++t)
+      if (t < d) {
+        const uint64_t neg = __ballot(q[t] < Real(0));
+        const uint64_t zero = __ballot(!(q[t] > Real(0)) && !(q[t] < Real(0)));
+        if (lane == 0) {
+          uint64_t *aw = w.alpha + ((int64_t)(e0 + t) * chunks + k) * 2;
+          aw[0] = neg;
+          aw[1] = zero;
+        }
+      }
+  }
+  if (lane == 0) w.odd[(int64_t)wg * chunks + k] = odd;
+}
+
+// One 256-thread block per chunk.  A running slot that has executed `it`
+// iterations stops at the cap, or -- min-sum's rule (:406-408) -- when
+// it < cap, it % et_period == 0 and its decision satisfies every check.
+// Freed (and empty) slots take the next frames of the batch in lane order.
+__global__ void __launch_bounds__(256) ms_decide(MsWork w, int max_iters, int et_period, int B) {
+  __shared__ uint64_t part[4];
+  const int k = blockIdx.x, lane = threadIdx.x & 63;
+  const int64_t chunks = w.chunks;
+  uint64_t odd = 0;
+  if (w.live_w[k])
+    for (int i = threadIdx.x; i < w.check_waves; i += 256) odd |= w.odd[(int64_t)i * chunks + k];
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)odd, off), hi = __shfl_xor((uint32_t)(odd >> 32), off);
+    odd |= ((uint64_t)hi << 32) | lo;
+  }
+  if (lane == 0) part[threadIdx.x >> 6] = odd;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  odd = part[0] | part[1] | part[2] | part[3];
+  const int slot = k * 64 + lane;
+  const int it = w.it[slot], f = w.frame[slot];
+  const bool running = f >= 0;
+  const bool unsat = lane_bit(odd, lane) != 0;
+  const bool stop = running && it >= 1 &&
+                    (it >= max_iters || (it % et_period == 0 && !unsat));
+  const bool want = stop || !running;
+  const uint64_t wm = __ballot(want);
+  int base = 0;
+  if (lane == 0 && wm) base = atomicAdd(&w.ctrl[0], __popcll(wm));
+  base = __shfl(base, 0);
+  const int rank = __popcll(wm & ((1ull << lane) - 1ull));
+  const int nf = want && base + rank < B ? base + rank : -1;
+  const bool fill = nf >= 0;
+  const bool run = running && !stop;
+  if (stop) w.used[slot] = it;
+  w.nxt[slot] = want ? nf : f;
+  w.it[slot] = run ? it + 1 : 0;
+  const uint64_t sw = __ballot(stop), rw = __ballot(run), fw = __ballot(fill);
+  const uint64_t cw = __ballot(stop && unsat);
+  if (lane == 0) {
+    w.stop_w[k] = sw;
+    w.run_w[k] = rw;
+    w.fill_w[k] = fw;
+    w.cap_w[k] = cw;
+    w.live_w[k] = rw | fw;
+    if (sw) atomicAdd(&w.ctrl[1], __popcll(sw));
+  }
+}
+
+// Outputs of the frames that stopped in this pass: packed info bits (bits
+// M.., MSB first, :207-219) through an LDS transpose, iterations, syndrome 0
+// (ms_synd adds the weight of frames stopped at the cap).
+__global__ void __launch_bounds__(256) ms_flush_packed(GraphView g, MsWork w, DecodeArgs a) {
+  const int k = blockIdx.y;
+  const uint64_t sel = w.stop_w[k];
+  if (!sel) return;
+  __shared__ uint8_t tile[64][65];
+  const int q0 = blockIdx.x * 64, lane = threadIdx.x & 63, wv = wave_id();
+  const int64_t chunks = w.chunks;
+  for (int qq = wv; qq < 64; qq += 4) {
+    const int q = q0 + qq;
+    unsigned o = 0;
+    if (q < g.KB)
+      for (int j = 0; j < 8; ++j) {
+        const int c = g.M + q * 8 + j;
+        if (c < g.N) o |= (unsigned)lane_bit(w.hard[(int64_t)c * chunks + k], lane) << (7 - j);
+      }
+    tile[lane][qq] = (uint8_t)o;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int f = i >> 6, qq = i & 63, q = q0 + qq;
+    if (lane_bit(sel, f) && q < g.KB) a.packed[(int64_t)w.frame[k * 64 + f] * g.KB + q] = tile[f][qq];
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 64 && lane_bit(sel, threadIdx.x)) {
+    const int slot = k * 64 + threadIdx.x, fr = w.frame[slot];
+    if (a.iters) a.iters[fr] = w.used[slot];
+    if (a.synd) a.synd[fr] = 0;
+  }
+}
+
+// Full hard decisions (B x N bytes) and posteriors (B x N floats) of the
+// frames that stopped.
+__global__ void __launch_bounds__(256) ms_flush_cols(GraphView g, MsWork w, uint8_t *bits,
+                                                     float *llr) {
+  const int k = blockIdx.y;
+  const uint64_t sel = w.stop_w[k];
+  if (!sel) return;
+  __shared__ float tile[64][65];
+  __shared__ uint8_t btile[64][65];
+  const int c0 = blockIdx.x * 64, lane = threadIdx.x & 63, wv = wave_id();
+  for (int cc = wv; cc < 64; cc += 4) {
+    const int c = c0 + cc;
+    btile[lane][cc] = c < g.N ? (uint8_t)lane_bit(w.hard[(int64_t)c * w.chunks + k], lane) : 0;
+    if (llr) tile[lane][cc] = c < g.N ? w.post[at(c, k, g.N, lane)] : 0.0f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int f = i >> 6, cc = i & 63, c = c0 + cc;
+    if (!lane_bit(sel, f) || c >= g.N) continue;
+    const int64_t fr = w.frame[k * 64 + f];
+    if (bits) bits[fr * g.N + c] = btile[f][cc];
+    if (llr) llr[fr * g.N + c] = tile[f][cc];
+  }
+}
+
+// Uncapped syndrome weight of the frames that stopped at the cap with
+// unsatisfied checks (added to the zero ms_flush_packed wrote).
+__global__ void __launch_bounds__(256) ms_synd(GraphView g, MsWork w, int32_t *synd) {
+  const int k = blockIdx.y;
+  const uint64_t sel = w.cap_w[k];
+  if (!sel || !synd) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t chunks = w.chunks;
+  const int j0 = (blockIdx.x * 4 + wave_id()) * kMsRows;
+  int cnt = 0;
+  for (int j = j0; j < min(j0 + kMsRows, g.M); ++j) {
+    uint64_t par = 0;
+    const int e1 = g.rp[j + 1];
+    for (int e = g.rp[j]; e < e1; ++e) par ^= w.hard[(int64_t)g.ci[e] * chunks + k];
+    cnt += (int)lane_bit(par, lane);
+  }
+  if (cnt && lane_bit(sel, lane)) atomicAdd(&synd[w.frame[k * 64 + lane]], cnt);
+}
+
+// Vertical step (:379-403) for the running slots: L(r_ji) of every edge of
+// the column from its row's state, s = sum_j L(r_ji) in ascending j,
+// LQ = Lci + s, vhat = LQ < 0.
+template <typename Real, int DV>
+__global__ void __launch_bounds__(256) ms_var(GraphView g, MsWork w) {
+  const int k = blockIdx.y;
+  if (!w.run_w[k]) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t chunks = w.chunks;
+  const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
+  Real *LQ = (Real *)w.LQ;
+  const int c0 = (blockIdx.x * 4 + wave_id()) * kMsCols;
+  for (int cc = 0; cc < kMsCols; ++cc) {
+    const int c = c0 + cc;
+    if (c >= g.N) break;
+    const int k0 = g.cp[c], d = g.cp[c + 1] - k0;
+    const Real lci = (Real)w.L[at(c, k, g.N, lane)];
+    Real r[DV];
+#pragma unroll
+    for (int t = 0; t < DV; ++t) {
+      r[t] = Real(0);
+      if (t < d) {
+        const int e = g.ce[k0 + t], j = g.cr[k0 + t];
+        const int pos = e - g.rp[j];  // the edge's place in its row
+        const int64_t ro = at(j, k, g.M, lane);
+        const int mt = w.meta[ro];
+        const uint64_t *aw = w.alpha + ((int64_t)e * chunks + k) * 2;
+        const int al = alpha_of(aw[0], aw[1], lane);
+        r[t] = (Real)(((mt >> 6) - 1) * al) * (pos == (mt & 63) - 1 ? m2[ro] : m1[ro]);
+      }
+    }
+    Real s = Real(0);
+#pragma unroll
+    for (int t = 0; t < DV; ++t)
+      if (t < d) s = s + r[t];
+    const Real lq = lci + s;
+    LQ[at(c, k, g.N, lane)] = lq;
+    const uint64_t bw = __ballot(lq < Real(0));
+    if (lane == 0) w.hard[(int64_t)c * chunks + k] = bw;
+    if (w.post) w.post[at(c, k, g.N, lane)] = (float)lq;
+  }
+}
+
+// Channel values of the frames the freed slots take: Lci = -tx (:318-321)
+// as float (exact) and LQ = Lci, through an LDS transpose (the block reads
+// each new frame's 64 samples along the frame).  Block 0 of each chunk also
+// moves the slots' frame indices forward.
+template <typename Real>
+__global__ void __launch_bounds__(256) ms_refill(GraphView g, MsWork w, DecodeArgs a) {
+  const int k = blockIdx.y;
+  const uint64_t fill = w.fill_w[k];
+  const int lane = threadIdx.x & 63, wv = wave_id();
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    const int slot = k * 64 + threadIdx.x;
+    if (lane_bit(w.stop_w[k] | fill, threadIdx.x)) w.frame[slot] = w.nxt[slot];
+  }
+  if (!fill) return;
+  __shared__ float tile[64][65];
+  const int c0 = blockIdx.x * 64;
+  for (int f = wv; f < 64; f += 4) {
+    float x = 0.0f;
+    const int c = c0 + lane;
+    if (lane_bit(fill, f) && c < g.N) {
+      const int64_t fr = w.nxt[k * 64 + f];
+      x = a.in[fr * a.cw_stride + (int64_t)c * a.elem_stride] * a.polarity;
+    }
+    tile[f][lane] = x;
+  }
+  __syncthreads();
+  if (!lane_bit(fill, lane)) return;
+  Real *LQ = (Real *)w.LQ;
+  for (int cc = wv; cc < 64; cc += 4) {
+    const int c = c0 + cc;
+    if (c >= g.N) break;
+    const float x = tile[lane][cc];
+    w.L[at(c, k, g.N, lane)] = -x;
+    LQ[at(c, k, g.N, lane)] = -(Real)x;
+  }
+}
+
+__global__ void ms_init(MsWork w) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < w.S; i += gridDim.x * blockDim.x) {
+    w.frame[i] = -1;
+    w.it[i] = 0;
+  }
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < w.chunks; k += gridDim.x * blockDim.x) {
+    w.live_w[k] = 0;
+    w.run_w[k] = w.stop_w[k] = w.fill_w[k] = w.cap_w[k] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.ctrl[0] = 0;
+    w.ctrl[1] = 0;
+  }
+}
+
+int ms_check_waves(const GraphView &g) { return 4 * ((g.M + 4 * kMsRows - 1) / (4 * kMsRows)); }
+
+template <int PREC>
+void ms_pass(const GraphView &g, const MsWork &w, const DecodeArgs &a, int method_iters,
+             hipStream_t st) {
+  typedef typename Math<PREC>::Real Real;
+  const dim3 rgrid(w.check_waves / 4, w.chunks);
+  const dim3 cgrid((g.N + 4 * kMsCols - 1) / (4 * kMsCols), w.chunks);
+  const dim3 tgrid((g.N + 63) / 64, w.chunks);
+  if (g.dc_max <= 8)
+    ms_check<PREC, 8><<<rgrid, 256, 0, st>>>(g, w);
+  else if (g.dc_max <= 16)
+    ms_check<PREC, 16><<<rgrid, 256, 0, st>>>(g, w);
+  else
+    ms_check<PREC, 32><<<rgrid, 256, 0, st>>>(g, w);
+  ms_decide<<<w.chunks, 256, 0, st>>>(w, method_iters, a.et_period, a.B);
+  ms_flush_packed<<<dim3((g.KB + 63) / 64, w.chunks), 256, 0, st>>>(g, w, a);
+  if (a.bits || (a.llr && w.post)) ms_flush_cols<<<tgrid, 256, 0, st>>>(g, w, a.bits, a.llr);
+  ms_synd<<<rgrid, 256, 0, st>>>(g, w, a.synd);
+  if (g.dv_max <= 4)
+    ms_var<Real, 4><<<cgrid, 256, 0, st>>>(g, w);
+  else if (g.dv_max <= 8)
+    ms_var<Real, 8><<<cgrid, 256, 0, st>>>(g, w);
+  else
+    ms_var<Real, 16><<<cgrid, 256, 0, st>>>(g, w);
+  ms_refill<Real><<<tgrid, 256, 0, st>>>(g, w, a);
+}
+
+}  // namespace
+
+int ms_default_slots() {
+  const char *e = getenv("LDPC_MS_SLOTS");  // A/B knob
+  const int v = e ? atoi(e) : 0;
+  return v >= 64 ? v / 64 * 64 : 128;
+}
+
+size_t ms_work_bytes(const GraphView &g, int S, int prec, bool want_post) {
+  const size_t real = prec == 1 ? 4 : 8;
+  const size_t chunks = (size_t)S / 64;
+  size_t n = al256((size_t)g.N * S * 4) + al256((size_t)g.N * S * real);  // L, LQ
+  n += 2 * al256((size_t)g.M * S * real) + al256((size_t)g.M * S);        // m1, m2, meta
+  n += al256((size_t)g.E * chunks * 16);                                  // alpha
+  n += al256((size_t)g.N * chunks * 8);                                   // hard
+  if (want_post) n += al256((size_t)g.N * S * 4);
+  n += al256((size_t)ms_check_waves(g) * chunks * 8);                     // odd
+  n += 4 * al256((size_t)S * 4);                                          // it, frame, nxt, used
+  n += 6 * al256(chunks * 8) + al256(64);                                 // masks, ctrl
+  return n;
+}
+
+void ms_work_carve(MsWork &w, void *base, const GraphView &g, int S, int prec, bool want_post) {
+  const size_t real = prec == 1 ? 4 : 8;
+  const size_t chunks = (size_t)S / 64;
+  char *p = (char *)base;
+  auto take = [&](size_t bytes) {
+    char *r = p;
+    p += al256(bytes);
+    return (void *)r;
+  };
+  w = MsWork{};
+  w.S = S;
+  w.chunks = (int)chunks;
+  w.check_waves = ms_check_waves(g);
+  w.L = (float *)take((size_t)g.N * S * 4);
+  w.LQ = take((size_t)g.N * S * real);
+  w.m1 = take((size_t)g.M * S * real);
+  w.m2 = take((size_t)g.M * S * real);
+  w.meta = (uint8_t *)take((size_t)g.M * S);
+  w.alpha = (uint64_t *)take((size_t)g.E * chunks * 16);
+  w.hard = (uint64_t *)take((size_t)g.N * chunks * 8);
+  w.post = want_post ? (float *)take((size_t)g.N * S * 4) : nullptr;
+  w.odd = (uint64_t *)take((size_t)w.check_waves * chunks * 8);
+  w.it = (int32_t *)take((size_t)S * 4);
+  w.frame = (int32_t *)take((size_t)S * 4);
+  w.nxt = (int32_t *)take((size_t)S * 4);
+  w.used = (int32_t *)take((size_t)S * 4);
+  w.live_w = (uint64_t *)take(chunks * 8);
+  w.run_w = (uint64_t *)take(chunks * 8);
+  w.stop_w = (uint64_t *)take(chunks * 8);
+  w.fill_w = (uint64_t *)take(chunks * 8);
+  w.cap_w = (uint64_t *)take(chunks * 8);
+  take(chunks * 8);
+  w.ctrl = (int32_t *)take(64);
+}
+
+int launch_graph_decode_ms(const GraphView &g, const MsWork &w, const DecodeArgs &a, int prec,
+                           int32_t *h_ctrl, void *stream) {
+  if (g.dc_max > kGraphDcMax || g.dv_max > kGraphDvMax) return -2;
+  if (a.B <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  ms_init<<<std::max(1, std::min(64, (w.S + 255) / 256)), 256, 0, st>>>(w);
+  // a slot finishes a frame at least every max_iters + 1 passes, so the pool
+  // drains within ceil(B/S) (max+1) passes and the last frames finish
+  // within max+1 more; passes past the end return at once (empty chunks)
+  const int64_t bound = ((int64_t)(a.B + w.S - 1) / w.S + 1) * (a.max_iters + 1) + 2;
+  const int kRound = 8;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  for (int i = 0; i < 2; ++i)
+    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return -1;
+  int rc = 0;
+  int64_t pass = 0;
+  for (int round = 0; pass < bound; ++round) {
+    for (int i = 0; i < kRound && pass < bound; ++i, ++pass) {
+      if (prec == 1)
+        ms_pass<1>(g, w, a, a.max_iters, st);
+      else
+        ms_pass<0>(g, w, a, a.max_iters, st);
+    }
+    // progress of this round, read back when the next round is queued
+    if (hipMemcpyAsync(h_ctrl + 2 * (round & 1), w.ctrl, 8, hipMemcpyDeviceToHost, st) !=
+            hipSuccess ||
+        hipEventRecord(ev[round & 1], st) != hipSuccess) {
+      rc = -1;
+      break;
+    }
+    if (round > 0) {
+      if (hipEventSynchronize(ev[(round - 1) & 1]) != hipSuccess) {
+        rc = -1;
+        break;
+      }
+      if (h_ctrl[2 * ((round - 1) & 1) + 1] >= a.B) break;  // all frames finished
+    }
+  }
+  for (int i = 0; i < 2; ++i) (void)hipEventDestroy(ev[i]);
+  if (rc == 0 && hipGetLastError() != hipSuccess) rc = -1;
+  return rc;
+}
+
+}  // namespace ldpc

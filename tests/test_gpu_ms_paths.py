@@ -1,0 +1,92 @@
+"""Large-code min-sum has two implementations (ldpc_capi.hip decode_graph):
+the frame pipeline with compressed check messages (ldpc_graph_ms.hip, the
+default) and the edge-message passes (ldpc_graph.hip, LDPC_MS_PIPELINE=0 at
+context creation).  Both must reproduce the oracle exactly: the reference's
+fixtures on its own H forced onto the large-code path (hard decisions, packed
+bytes, iterations, syndromes, posteriors), the DVB-S2-like code against the
+sparse restatement, non-finite samples, et_period 5, and batches far larger
+than the pipeline's slots (every slot recycled many times)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _decoder(pipeline, **kw):
+    import ldpc_ece535a as L
+    old = os.environ.get("LDPC_MS_PIPELINE")
+    os.environ["LDPC_MS_PIPELINE"] = "1" if pipeline else "0"
+    try:
+        return L.Decoder(**kw)
+    finally:
+        if old is None:
+            del os.environ["LDPC_MS_PIPELINE"]
+        else:
+            os.environ["LDPC_MS_PIPELINE"] = old
+
+
+@pytest.fixture(scope="module", params=[True, False], ids=["pipeline", "edge"])
+def gdec(request):
+    return _decoder(request.param, force_graph=True)
+
+
+@pytest.mark.parametrize("db", [0, 2, 4])
+@pytest.mark.parametrize("iters", [5, 50])
+def test_fixtures(gdec, golden, db, iters):
+    fd = golden("frames_default.npz")
+    out = gdec.decode(fd["db%d_llr" % db], method=0, max_iters=iters, want_llr=True)
+    key = "db%d_m0_i%d" % (db, iters)
+    for k in ("bits", "packed", "iters", "synd"):
+        np.testing.assert_array_equal(out[k], fd[key + "_" + k], err_msg=k)
+    np.testing.assert_array_equal(out["llr"], fd[key + "_post"])
+
+
+@pytest.mark.parametrize("B", [1, 63, 65, 300, 5000])
+def test_batches_and_et_period(gdec, B):
+    from oracle import oracle as orc
+    rng = np.random.default_rng(B)
+    Hr = gdec.H
+    x = 2.0 * __import__("ldpc_ece535a").encode(
+        Hr, rng.integers(0, 2, size=(B, 32), dtype=np.uint8)) - 1.0
+    db = rng.integers(0, 5, size=B)
+    y = (x + np.sqrt(10.0 ** (-db / 10.0))[:, None] * rng.standard_normal(x.shape)).astype(
+        np.float32)
+    for et in (1, 5):
+        out = gdec.decode(y, method=0, max_iters=50, et_period=et)
+        ref = orc.decode_batch(0, Hr, y, 50, nthreads=16, et_period=et)
+        for k in ("bits", "packed", "iters", "synd"):
+            np.testing.assert_array_equal(out[k], ref[k], err_msg="%s et=%d" % (k, et))
+
+
+def test_non_finite(gdec):
+    from oracle import oracle as orc
+    rng = np.random.default_rng(3)
+    y = rng.standard_normal((200, 64)).astype(np.float32)
+    y[::7, 3] = np.inf
+    y[1::5, 10] = -np.inf
+    y[2::9, 20] = np.nan
+    y[3::4, 30:34] = 0.0
+    out = gdec.decode(y, method=0, max_iters=20, want_llr=True)
+    ref = orc.decode_batch(0, gdec.H, y, 20, want_post=True)
+    for k in ("bits", "iters", "synd"):
+        np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
+    np.testing.assert_array_equal(out["llr"], ref["post"])
+
+
+@pytest.mark.parametrize("pipeline", [True, False])
+def test_dvbs2_like_vs_sparse_oracle(pipeline):
+    from ldpc_ece535a import codes
+    from oracle import oracle as orc
+    csr = codes.dvbs2_like(0)
+    d = _decoder(pipeline, csr=csr)
+    M, N, rp, ci = csr
+    rng = np.random.Generator(np.random.PCG64(77))
+    info = rng.integers(0, 2, size=(160, N - M), dtype=np.uint8)
+    x = 2.0 * codes.ira_encode(csr, info) - 1.0
+    y = (x + np.sqrt(10 ** (-1.0 / 10)) * rng.standard_normal(x.shape)).astype(np.float32)
+    out = d.decode(y, method=0, max_iters=50)
+    ref = orc.decode_batch_sparse(0, rp, ci, M, N, y, 50, nthreads=16)
+    for k in ("bits", "packed", "iters", "synd"):
+        np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
