@@ -453,6 +453,7 @@ def sweeps(L, torch, dec, args, dev):
                for j in range(8)]
         for m, p in modes:
             for D in [int(x) for x in args.sweep_inflight.split(",")]:
+                dec.set_launch_mode(1 if D > 1 else 0)
                 r = time_decoder(dec, torch, ins, B, m, args.iters, args.et_period, p,
                                  args.steps, args.warmup, inflight=D)
                 print("inflight method=%d prec=%d D=%d ms_per_batch=%8.4f Mbit/s=%9.2f" %
@@ -507,7 +508,6 @@ def main():
         Hr = None
     else:
         dec = L.Decoder(device=local)  # default H, reorderHMatrix applied
-        dec.set_waves_per_cu(args.waves_per_cu)
         dec.set_schedule(args.schedule)
         Hr = dec.H
     offset, B = plan_batch(args.batch, world, rank, args.strong)
@@ -517,6 +517,12 @@ def main():
     torch.cuda.synchronize(dev)
     sweeps(L, torch, dec, args, dev)
 
+    # several batches in flight: the throughput launch mode (10 waves per CU,
+    # no issue-priority management; include/ldpc_hip.h ldpc_set_launch_mode)
+    if not dvb:
+        dec.set_launch_mode(1 if D > 1 else 0)
+        if args.waves_per_cu:
+            dec.set_waves_per_cu(args.waves_per_cu)
     r = time_decoder(dec, torch, inputs, B, args.method, args.iters, args.et_period, prec,
                      args.steps, args.warmup, dist, inflight=D)
     wall = r["wall"]
@@ -542,8 +548,9 @@ def main():
     alg_bytes = float(B * (4 * N + dec.KB + 8) + mean_it * B * bytes_per_iter(E, N, prec))
     workload_key = "%s%d_%s_b%d_i%d_db%g" % ("dvb" if dvb else "sp", args.method, args.precision,
                                             args.batch, args.iters, args.ebn0)
-    pmc = load_pmc(args.pmc_json, workload_key)
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    entry = load_pmc(args.pmc_json, workload_key) or {}
+    pmc = entry.get("pmc")
+    traffic = entry.get("hbm_bytes_per_launch")
 
     mname = {0: "min-sum", 1: "sum-product", 2: "bit-flip", 3: "hard"}[args.method]
     if dvb:
@@ -596,7 +603,7 @@ def main():
     elif pmc and "SQ_INSTS_VALU" in pmc:
         line["roofline"] = valu_roofline(pmc, per_launch_ms)
         line["roofline"]["traffic"] = traffic
-        line["roofline"]["pmc_source"] = pmc.get("source")
+        line["roofline"]["pmc_source"] = entry.get("source")
         hbm_model["label"] = ("equivalent streaming bandwidth of a decoder that streams its edge "
                               "messages through HBM; this kernel keeps them on chip (traffic = "
                               "measured HBM bytes per launch), so no HBM fraction applies")
@@ -615,8 +622,12 @@ def main():
 
     # ---- single batch in flight (latency per batch), same process ----------
     if D > 1 and not args.no_variants:
+        if not dvb:
+            dec.set_launch_mode(0)  # one launch at a time: the latency mode
         r1 = time_decoder(dec, torch, inputs[:1], B, args.method, args.iters, args.et_period,
                           prec, max(10, args.steps // 2), 5, inflight=1)
+        if not dvb:
+            dec.set_launch_mode(1)
         line["serial_1_batch_in_flight"] = {
             "Mbit/s": round(B * dec.K * max(10, args.steps // 2) / r1["wall"] / 1e6, 2),
             "latency_ms_per_batch": round(r1["per_launch_ms"], 5)}

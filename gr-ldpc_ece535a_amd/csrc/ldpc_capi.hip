@@ -53,6 +53,10 @@ struct ldpc_ctx {
   void *graph_stream = nullptr;
   hipEvent_t graph_done = nullptr;
   int waves_per_cu = 0;           // 0: kernel default
+  // launch mode (ldpc_set_launch_mode): issue-priority threshold of the
+  // small-code kernel, core clocks (profiles/round1/ab_fair_threshold_warm.txt:
+  // 1800 is the best of 1200..3000 for one launch at a time); 0 = off
+  uint32_t fair_cycles = 1800;
   int schedule = 0;               // 0 auto, 1 wave per frame, 2 workgroup per frame
   // large-code path (ldpc_graph.hip): H as CSR + CSC, messages in a workspace
   bool graph = false;
@@ -961,6 +965,7 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   a.ticket = ctx->d_tickets + q;
   a.ticket_base = ctx->queues[q].base;
   a.waves = 0;
+  a.fair_cycles = ctx->fair_cycles;
   rc = ldpc::launch_decode(code_view(ctx), a, method, precision, ctx->slots, ctx->nw,
                            ctx->waves_per_cu, ctx->schedule, st);
   if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no kernel for this code shape");
@@ -1082,6 +1087,17 @@ int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu) {
   if (!ctx || waves_per_cu < 0 || waves_per_cu > 32)
     return set_err(ctx, LDPC_EINVAL, "waves_per_cu must be in [0, 32]");
   ctx->waves_per_cu = waves_per_cu;
+  return LDPC_OK;
+}
+
+int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode) {
+  if (!ctx || (mode != LDPC_MODE_LATENCY && mode != LDPC_MODE_THROUGHPUT))
+    return set_err(ctx, LDPC_EINVAL, "mode must be LDPC_MODE_LATENCY or LDPC_MODE_THROUGHPUT");
+  // measured on the config-2 batch (profiles/round2/ab_launch_mode.txt):
+  // one launch at a time: 12 waves per CU, priority for starved waves;
+  // overlapping launches: 10 waves per CU, no priority games
+  ctx->waves_per_cu = mode == LDPC_MODE_THROUGHPUT ? 10 : 0;
+  ctx->fair_cycles = mode == LDPC_MODE_THROUGHPUT ? 0 : 1800;
   return LDPC_OK;
 }
 

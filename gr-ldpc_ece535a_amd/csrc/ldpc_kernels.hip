@@ -55,11 +55,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef LDPC_TANH_SPLIT
 #define LDPC_TANH_SPLIT 16.0  // |m| below which the single-range tanh(m/2) is used
 #endif
-#ifndef LDPC_FAIR_CYCLES
-// core clocks (~0.77 us at the warm 2.33 GHz); profiles/round1/ab_fair_threshold_warm.txt:
-// 1800 is the best of 1200..3000 warm and cold, and 1600 or less loses 7 %
-#define LDPC_FAIR_CYCLES 1800
-#endif
 
 template <int NW>
 __device__ __forceinline__ uint64_t word_at(const uint64_t (&w)[NW], int idx) {
@@ -231,25 +226,27 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         ea[q][k] = (FIN && e == eb_dummy) ? lds_addr(nr + lane + 64 * q) : e;
       }
     Real rc[NW];
+    // every check operand in tb is a tanh(m/2) with |m| <= LDPC_TANH_SPLIT
+    // (so |T| < 1 and finite): the check messages need no saturation select
+    bool open = FIN && PREC == 0 && LDPC_TANH_SPLIT > 0;
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
       rc[q] = rb[lane + 64 * q];  // written by this lane above
       if constexpr (FIN) nr[lane + 64 * q] = -rc[q];
       // initial bit messages M(j,i) = r(i) (:489-496)
       const Real t0 = Math<PREC>::tanh_half(rc[q]);
+      open = open && __builtin_amdgcn_ballot_w64(!(__builtin_fabs((double)rc[q]) <=
+                                                    LDPC_TANH_SPLIT)) == 0;
 #pragma unroll
       for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], t0);
     }
-#ifndef LDPC_NO_FAIR
-    uint64_t t_prev = __builtin_amdgcn_s_memtime();
-#endif
+    const uint32_t fair = a.fair_cycles;  // 0: no issue-priority management
+    uint64_t t_prev = fair ? __builtin_amdgcn_s_memtime() : 0;
     for (int h = 0; h < a.max_iters; ++h) {
-#ifndef LDPC_NO_FAIR
       // read here, used once the row gathers below have been waited for (an
       // SMEM result needs lgkmcnt(0), which would otherwise also drain the
       // previous iteration's LDS scatters before any gather could issue)
-      const uint64_t now = __builtin_amdgcn_s_memtime();
-#endif
+      const uint64_t now = fair ? __builtin_amdgcn_s_memtime() : 0;
       wave_lds_sync();  // tb complete
       Real nb[S][DCN];
 #pragma unroll
@@ -260,32 +257,46 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       for (int s = 0; s < S; ++s)
 #pragma unroll
         for (int k = 0; k < DCN; ++k) asm volatile("" ::"v"(nb[s][k]));
+      // T = prod_{k != i} tanh(M(j,k)/2), ascending k; E = log((1+T)/(1-T))
+      // (:506-513).  Padding neighbours read the 1.0 dummy: exact no-op.
+      Real Ts[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        // T = prod_{k != i} tanh(M(j,k)/2), ascending k; E = log((1+T)/(1-T))
-        // (:506-513).  Padding neighbours read the 1.0 dummy: exact no-op.
         Real T = Real(1);
 #pragma unroll
         for (int k = 0; k < DCN; ++k) T = T * nb[s][k];
-        eb[lane + 64 * s] = Math<PREC>::check_msg(T, logtab);
+        Ts[s] = T;
       }
-#ifndef LDPC_NO_FAIR
-      {
-        // Issue priority for starved waves.  A SIMD's waves issue oldest
-        // first, and two waves already keep its VALU busy, so the third wave
-        // of a SIMD crawls (1.7-2 us per iteration against ~1 us) and a long
-        // frame it holds ends the batch.  A wave whose last iteration took
-        // more than LDPC_FAIR_CYCLES core clocks issues first for the next
-        // one (same-box A/B on the headline: -2.6 %).  Scheduling only: the
+      if constexpr (FIN && PREC == 0 && LDPC_TANH_SPLIT > 0) {
+        if (open) {
+#pragma unroll
+          for (int s = 0; s < S; ++s) eb[lane + 64 * s] = fm::log_ratio_tab_open(Ts[s], logtab);
+        } else {
+#pragma unroll
+          for (int s = 0; s < S; ++s) eb[lane + 64 * s] = Math<PREC>::check_msg(Ts[s], logtab);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) eb[lane + 64 * s] = Math<PREC>::check_msg(Ts[s], logtab);
+      }
+      if (fair) {
+        // Issue priority for starved waves (latency mode, one launch at a
+        // time).  A SIMD's waves issue oldest first, and two waves already
+        // keep its VALU busy, so the third wave of a SIMD crawls (1.7-2 us
+        // per iteration against ~1 us) and a long frame it holds ends the
+        // batch.  A wave whose last iteration took more than `fair` core
+        // clocks issues first for the next one (-2.6 % per launch).  With
+        // launches overlapping (throughput mode) the next batch fills those
+        // SIMDs instead, and the priority games cost 2.5 % (same-box A/B,
+        // profiles/round2/ab_launch_mode.txt).  Scheduling only: the
         // arithmetic is untouched.
         const uint32_t d = (uint32_t)(now - t_prev);
         t_prev = now;
-        if (d > LDPC_FAIR_CYCLES)
+        if (d > fair)
           __builtin_amdgcn_s_setprio(3);
         else
           __builtin_amdgcn_s_setprio(0);
       }
-#endif
       wave_lds_sync();  // eb complete
       Real tv[NW][DVN];
 #pragma unroll
@@ -340,11 +351,13 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           for (int q = 0; q < NW; ++q)
 #pragma unroll
             for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], fm::tanh_half_small(mv[q][k]));
+          open = FIN;
         } else {
 #pragma unroll
           for (int q = 0; q < NW; ++q)
 #pragma unroll
             for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], Math<PREC>::tanh_half(mv[q][k]));
+          open = false;
         }
       } else {
 #pragma unroll

@@ -79,6 +79,9 @@ struct DecodeArgs {
   uint32_t *ticket;
   uint32_t ticket_base;
   int waves;
+  // issue-priority threshold in core clocks for waves whose last iteration
+  // was slow (0: off); see decode_frame
+  uint32_t fair_cycles;
 };
 
 // Launch one decode (host side, implemented in ldpc_kernels.hip).

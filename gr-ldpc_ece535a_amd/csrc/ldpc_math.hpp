@@ -531,6 +531,12 @@ LDPC_HD double log_ratio_fast(double T) {
   return __builtin_fabs(T) == 1.0 ? __builtin_copysign(__builtin_inf(), T) : r;
 }
 
+// log((1+T)/(1-T)) for |T| < 1 (no NaN): log_ratio_tab without its final
+// select.  The decode kernels use it for iterations whose check operands are
+// all tanh values of |m| <= LDPC_TANH_SPLIT (< 1 - 2e-7 in magnitude), so no
+// product can reach 1.
+LDPC_HD double log_ratio_tab_open(double T, const LogTabEntry *tab);
+
 // log((1+T)/(1-T)) with a table-driven log (tools/gen_logtab.py): the same
 // ratio q as log_ratio_fast, then q = 2^k z, z in [0.6875, 1.375), bucket i
 // from the top 9 bits, r = z invc_i - 1 (|r| < 1/512), log(q) = k ln2 +
@@ -572,6 +578,35 @@ LDPC_HD double log_ratio_tab(double T, const LogTabEntry *tab) {
   const double y = fma_(r2, p, lo) + hi;
   // |T| == 1 -> T * inf = +-inf; NaN -> NaN
   return __builtin_fabs(T) < 1.0 ? y : T * __builtin_inf();
+}
+
+LDPC_HD double log_ratio_tab_open(double T, const LogTabEntry *tab) {
+  const double ln2_hi = 6.93147180369123816490e-01;
+  const double ln2_lo = 1.90821492927058770002e-10;
+  const double q = div_fast(1.0 + T, 1.0 - T);
+  uint64_t ix;
+  __builtin_memcpy(&ix, &q, 8);
+  const uint32_t hx = (uint32_t)(ix >> 32);
+  const uint32_t th = hx - 0x3FE60000u;
+  const uint32_t off = (th >> (20 - kLogTabBits - 4)) & (((1u << kLogTabBits) - 1) << 4);
+  const int k = (int)th >> 20;
+  const uint64_t iz = ((uint64_t)(hx - (th & 0xFFF00000u)) << 32) | (ix & 0xFFFFFFFFull);
+  double z;
+  __builtin_memcpy(&z, &iz, 8);
+  const LogTabEntry e = *reinterpret_cast<const LogTabEntry *>(
+      reinterpret_cast<const char *>(tab) + off);
+  const double r = fma_(z, e.invc, -1.0);
+  const double kd = (double)k;
+  const double w = fma_(kd, ln2_hi, e.logc);
+  const double hi = w + r;
+  const double lo = fma_(kd, ln2_lo, w - hi + r);
+  const double r2 = r * r;
+  double p = -1.0 / 6.0;
+  p = fma_(p, r, 1.0 / 5.0);
+  p = fma_(p, r, -1.0 / 4.0);
+  p = fma_(p, r, 1.0 / 3.0);
+  p = fma_(p, r, -0.5);
+  return fma_(r2, p, lo) + hi;
 }
 
 }  // namespace fm

@@ -19,6 +19,7 @@ PREC_F64, PREC_F32, PREC_F64_LIBM = 0, 1, 2
 FLAG_NO_REORDER = 1
 FLAG_GRAPH = 2
 PATH_SMALL, PATH_GRAPH = 0, 1
+MODE_LATENCY, MODE_THROUGHPUT = 0, 1
 ERRORS = {0: "LDPC_OK", -1: "LDPC_EINVAL", -2: "LDPC_EUNSUPPORTED", -3: "LDPC_EDEVICE",
           -4: "LDPC_ESINGULAR", -5: "LDPC_ENOMEM"}
 
@@ -57,6 +58,7 @@ SIGNATURES = {
                                      ctypes.c_float, _i, _u8p, _i32p]),
     "ldpc_alist_read": (_i, [ctypes.c_char_p, _i32p, _i32p, _i32p, _i32p, _i64]),
     "ldpc_set_waves_per_cu": (_i, [_vp, _i]),
+    "ldpc_set_launch_mode": (_i, [_vp, _i]),
     "ldpc_set_schedule": (_i, [_vp, _i]),
     "ldpc_synchronize": (_i, [_vp]),
 }
@@ -246,6 +248,11 @@ class Decoder:
                                         int(precision), d_in, int(cw_stride), int(elem_stride),
                                         float(polarity), int(B), d_packed, d_bits, d_iters,
                                         d_synd, d_llr, stream), self._ctx)
+
+    def set_launch_mode(self, mode):
+        """MODE_LATENCY (default: one decode at a time) or MODE_THROUGHPUT
+        (several decodes in flight on different streams)."""
+        _check(lib().ldpc_set_launch_mode(self._ctx, int(mode)), self._ctx)
 
     def set_waves_per_cu(self, n):
         _check(lib().ldpc_set_waves_per_cu(self._ctx, int(n)), self._ctx)

@@ -205,6 +205,18 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
  * Frames are pulled from a per-launch queue by that many resident waves. */
 int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu);
 
+/* Tuning: launch mode of the small-code kernel (results are identical).
+ * LDPC_MODE_LATENCY (default): for one decode at a time (the block's
+ * general_work): 12 persistent waves per CU, and a wave whose last iteration
+ * was slow gets issue priority, so the frames that end a batch are not
+ * starved.  LDPC_MODE_THROUGHPUT: for callers that keep several decodes in
+ * flight on different streams: 10 waves per CU, no priority management (the
+ * next batch fills the SIMDs a batch's last frames leave idle).  Overrides an
+ * earlier ldpc_set_waves_per_cu. */
+#define LDPC_MODE_LATENCY 0
+#define LDPC_MODE_THROUGHPUT 1
+int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode);
+
 /* Tuning: kernel schedule.  0 (default) = 1: one frame per wave; 2: one
  * frame per workgroup of ceil(E/64) waves, one edge per lane (kept for
  * latency experiments; measured no faster at any batch size on MI355X).

@@ -35,7 +35,7 @@ for r in 1 2; do
     d=\${d%/}
     v=\$(basename \$d)
     LDPC_PKG_DIR=\$PWD/\$d timeout -k 10 200 python bench.py $args > ab/out/\$v.\$r.json 2> gpurun_out/ab_\$v.\$r.err || { tail -5 gpurun_out/ab_\$v.\$r.err; exit 1; }
-    python3 -c "import json;d=json.load(open('ab/out/\$v.\$r.json'));print('\$v', \$r, d['value'], d['roofline']['kernel_ms'])"
+    python3 -c "import json;d=json.load(open('ab/out/\$v.\$r.json'));print('\$v', \$r, d['value'], d['timing']['device_span_ms_per_launch'])"
   done
 done
 EOS
