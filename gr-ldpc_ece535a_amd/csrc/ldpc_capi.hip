@@ -18,6 +18,7 @@
 #include "ldpc_aux.hpp"
 #include "ldpc_graph.hpp"
 #include "ldpc_kernels.hpp"
+#include "ldpc_layout.hpp"
 
 using ldpc::ColRec;
 using ldpc::EdgeColRec;
@@ -34,6 +35,10 @@ struct ldpc_ctx {
   EdgeColRec *d_ecol = nullptr;
   ColRec *d_cols = nullptr;
   uint64_t *d_rowmask = nullptr;
+  uint16_t *d_lane_col = nullptr;  // small-code LDS layout (ldpc_layout.hpp)
+  uint8_t *d_col_lane = nullptr;
+  uint64_t dpos[2] = {0, 0};
+  int layout_model[5] = {0, 0, 0, 0, 0};  // searched?, modelled cc / ec, plain cc / ec
   void *d_stage = nullptr;
   size_t stage_bytes = 0;
   float *h_stage = nullptr;  // pinned host staging of host-buffer decodes
@@ -150,9 +155,23 @@ bool valid_h(const uint8_t *H, int M, int N) {
   return true;
 }
 
-// Edge / column / row tables of the decoder's H (see ldpc_kernels.hpp).
+// The loop lengths the small-code kernel is built with for this code
+// (ldpc_kernels.hip launch_slots), and whether sum-product runs its
+// column-centric form (cols_kernel).
+void kernel_shape(int nw, int slots, int dc_max, int dv_max, int &dcn, int &dvn, bool &cols) {
+  const bool low = nw == 1 && dc_max <= 6 && dv_max <= 3 && slots <= 4;
+  dcn = low ? 5 : ldpc::kDcMax - 1;
+  dvn = low ? 3 : ldpc::kDvMax;
+  cols = nw == 1 && dvn <= slots;
+}
+
+// Edge / column / row tables of the decoder's H (see ldpc_kernels.hpp), at
+// the cells and positions plan_layout chooses (LDPC_LAYOUT=0: the plain CSR
+// layout, for A/B runs).
 int build_tables(ldpc_ctx *ctx, std::vector<EdgeRowRec> &erecs, std::vector<EdgeColRec> &crecs,
-                 std::vector<ColRec> &cols, std::vector<uint64_t> &rowmask) {
+                 std::vector<ColRec> &cols, std::vector<uint64_t> &rowmask,
+                 std::vector<uint16_t> &lane_col, std::vector<uint8_t> &col_lane,
+                 bool search, std::vector<int> *cell_out = nullptr) {
   const int M = ctx->M, N = ctx->N;
   const uint8_t *H = ctx->H.data();
   std::vector<std::vector<int>> row_edges(M), col_edges(N);
@@ -188,6 +207,23 @@ int build_tables(ldpc_ctx *ctx, std::vector<EdgeRowRec> &erecs, std::vector<Edge
   ctx->K = N - M;
   ctx->KB = (ctx->K + 7) / 8;
 
+  int dcn, dvn;
+  bool cols_k;
+  kernel_shape(ctx->nw, ctx->slots, ctx->dc_max, ctx->dv_max, dcn, dvn, cols_k);
+  const char *lv = getenv("LDPC_LAYOUT");
+  const ldpc::EdgeLayout lay = ldpc::plan_layout(M, N, erow, ecol, ctx->slots, ctx->nw, dcn, dvn,
+                                                 cols_k, search && !(lv && lv[0] == '0'));
+  const std::vector<int> &cell = lay.slot, &pos = lay.pos;
+  if (cell_out) *cell_out = cell;
+  ctx->layout_model[0] = lay.searched ? 1 : 0;
+  ctx->layout_model[1] = lay.model_cc;
+  ctx->layout_model[2] = lay.model_ec;
+  ctx->layout_model[3] = lay.plain_cc;
+  ctx->layout_model[4] = lay.plain_ec;
+  ctx->dpos[0] = ctx->dpos[1] = 0;
+  for (int g = 0; g < 2 * ctx->slots; ++g)
+    ctx->dpos[g / 8] |= (uint64_t)(lay.dpos[g] & 31) << (8 * (g % 8));
+
   erecs.assign((size_t)64 * ctx->slots, EdgeRowRec{});
   crecs.assign((size_t)64 * ctx->slots, EdgeColRec{});
   for (auto &r : erecs) {
@@ -199,28 +235,36 @@ int build_tables(ldpc_ctx *ctx, std::vector<EdgeRowRec> &erecs, std::vector<Edge
     r.col = kNone;
   }
   for (int e = 0; e < ctx->E; ++e) {
-    erecs[e].col = crecs[e].col = (uint16_t)ecol[e];
+    EdgeRowRec &er = erecs[cell[e]];
+    EdgeColRec &ec = crecs[cell[e]];
+    er.col = ec.col = (uint16_t)pos[ecol[e]];
     int k = 0;
     for (int n : row_edges[erow[e]])
-      if (n != e) erecs[e].rn[k++] = (uint16_t)n;  // ascending column
+      if (n != e) er.rn[k++] = (uint16_t)cell[n];  // ascending column
     k = 0;
     for (int n : col_edges[ecol[e]])
-      if (n != e) crecs[e].cn[k++] = (uint16_t)n;  // ascending row
+      if (n != e) ec.cn[k++] = (uint16_t)cell[n];  // ascending row
   }
   cols.assign((size_t)64 * ctx->nw, ColRec{});
   for (auto &c : cols) {
     std::fill(std::begin(c.e), std::end(c.e), kNone);
     std::fill(std::begin(c.r), std::end(c.r), kNone);
   }
-  for (int i = 0; i < N; ++i)
+  lane_col.assign((size_t)64 * ctx->nw, kNone);
+  col_lane.assign((size_t)N, 0);
+  for (int i = 0; i < N; ++i) {
+    lane_col[pos[i]] = (uint16_t)i;
+    col_lane[i] = (uint8_t)pos[i];
     for (size_t k = 0; k < col_edges[i].size(); ++k) {
-      cols[i].e[k] = (uint16_t)col_edges[i][k];
-      cols[i].r[k] = (uint16_t)erow[col_edges[i][k]];
+      cols[pos[i]].e[k] = (uint16_t)cell[col_edges[i][k]];
+      cols[pos[i]].r[k] = (uint16_t)erow[col_edges[i][k]];
     }
+  }
   rowmask.assign((size_t)M * ctx->nw, 0);
   for (int j = 0; j < M; ++j)
     for (int i = 0; i < N; ++i)
-      if (H[(size_t)j * N + i]) rowmask[(size_t)j * ctx->nw + i / 64] |= 1ull << (i % 64);
+      if (H[(size_t)j * N + i])
+        rowmask[(size_t)j * ctx->nw + pos[i] / 64] |= 1ull << (pos[i] % 64);
   return LDPC_OK;
 }
 
@@ -351,6 +395,10 @@ ldpc::CodeView code_view(const ldpc_ctx *ctx) {
   v.ecol = ctx->d_ecol;
   v.cols = ctx->d_cols;
   v.rowmask = ctx->d_rowmask;
+  v.lane_col = ctx->d_lane_col;
+  v.col_lane = ctx->d_col_lane;
+  v.dpos[0] = ctx->dpos[0];
+  v.dpos[1] = ctx->dpos[1];
   v.M = ctx->M;
   v.N = ctx->N;
   v.E = ctx->E;
@@ -679,9 +727,13 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
   std::vector<EdgeColRec> crecs;
   std::vector<ColRec> cols;
   std::vector<uint64_t> rowmask;
+  std::vector<uint16_t> lane_col;
+  std::vector<uint8_t> col_lane;
   std::vector<int32_t> cp, ce, cr;
   int rc = LDPC_EUNSUPPORTED;
-  if (!(flags & LDPC_FLAG_GRAPH) && !ctx->H.empty()) rc = build_tables(ctx, erecs, crecs, cols, rowmask);
+  if (!(flags & LDPC_FLAG_GRAPH) && !ctx->H.empty())
+    rc = build_tables(ctx, erecs, crecs, cols, rowmask, lane_col, col_lane,
+                      !(flags & LDPC_FLAG_PLAIN_LAYOUT));
   if (rc == LDPC_EUNSUPPORTED) {
     ctx->err.clear();
     rc = build_graph(ctx, cp, ce, cr);
@@ -720,6 +772,8 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     upload(ctx, &ctx->d_ecol, crecs, "upload(ecol)", what, e);
     upload(ctx, &ctx->d_cols, cols, "upload(cols)", what, e);
     upload(ctx, &ctx->d_rowmask, rowmask, "upload(rowmask)", what, e);
+    upload(ctx, &ctx->d_lane_col, lane_col, "upload(lane_col)", what, e);
+    upload(ctx, &ctx->d_col_lane, col_lane, "upload(col_lane)", what, e);
     std::vector<uint32_t> zeros(LDPC_TICKET_SLOTS, 0);
     upload(ctx, &ctx->d_tickets, zeros, "upload(tickets)", what, e);
   }
@@ -779,6 +833,8 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->d_ecol) (void)hipFree(ctx->d_ecol);
   if (ctx->d_cols) (void)hipFree(ctx->d_cols);
   if (ctx->d_rowmask) (void)hipFree(ctx->d_rowmask);
+  if (ctx->d_lane_col) (void)hipFree(ctx->d_lane_col);
+  if (ctx->d_col_lane) (void)hipFree(ctx->d_col_lane);
   if (ctx->d_stage) (void)hipFree(ctx->d_stage);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
@@ -830,6 +886,39 @@ int ldpc_ctx_csr(const ldpc_ctx *ctx, int32_t *row_ptr_out, int32_t *col_idx_out
 int ldpc_ctx_path(const ldpc_ctx *ctx) {
   if (!ctx) return LDPC_EINVAL;
   return ctx->graph ? 1 : 0;
+}
+
+int ldpc_ctx_layout(const ldpc_ctx *ctx, int32_t *model_out) {
+  if (!ctx || !model_out) return LDPC_EINVAL;
+  if (ctx->graph) return LDPC_EUNSUPPORTED;
+  std::copy(ctx->layout_model, ctx->layout_model + 5, model_out);
+  return LDPC_OK;
+}
+
+int ldpc_plan_layout(const uint8_t *H, int M, int N, int flags, int32_t *cell_out_opt,
+                     int32_t *pos_out_opt, int32_t *model_out_opt) {
+  g_create_error.clear();
+  if (!valid_h(H, M, N)) return set_err(nullptr, LDPC_EINVAL, "H must be M x N (M < N) with 0/1 entries");
+  ldpc_ctx tmp;
+  tmp.M = M;
+  tmp.N = N;
+  tmp.H.assign(H, H + (size_t)M * N);
+  if (!(flags & LDPC_FLAG_NO_REORDER)) reorder_columns(tmp.H.data(), M, N, nullptr, nullptr, nullptr);
+  std::vector<EdgeRowRec> erecs;
+  std::vector<EdgeColRec> crecs;
+  std::vector<ColRec> cols;
+  std::vector<uint64_t> rowmask;
+  std::vector<uint16_t> lane_col;
+  std::vector<uint8_t> col_lane;
+  std::vector<int> cell;
+  const int rc = build_tables(&tmp, erecs, crecs, cols, rowmask, lane_col, col_lane,
+                              !(flags & LDPC_FLAG_PLAIN_LAYOUT), &cell);
+  if (rc != LDPC_OK) return set_err(nullptr, rc, tmp.err);
+  if (cell_out_opt) std::copy(cell.begin(), cell.end(), cell_out_opt);
+  if (pos_out_opt)
+    for (int i = 0; i < N; ++i) pos_out_opt[i] = col_lane[i];
+  if (model_out_opt) std::copy(tmp.layout_model, tmp.layout_model + 5, model_out_opt);
+  return tmp.E;
 }
 
 int ldpc_encode_device(ldpc_ctx *ctx, const uint8_t *d_data_bits, int B, uint8_t *d_codewords,

@@ -33,6 +33,7 @@
 
 #include "ldpc_device.hpp"
 #include "ldpc_kernels.hpp"
+#include "ldpc_layout.hpp"
 
 namespace ldpc {
 
@@ -98,7 +99,10 @@ __device__ __forceinline__ uint32_t lds_addr(const T *p) {
 }
 
 // Rewrites the 16-bit edge/column ids of a packed record (fields 0..nf-1)
-// as LDS byte addresses base + id * size; kNone becomes the dummy element.
+// as LDS element indices base/size + id (kNone: the dummy element), i.e.
+// LDS byte addresses in units of the element size, so they fit 16 bits for
+// every slice (a block's LDS can exceed 64 KiB); lds_at() turns a field back
+// into a byte address when the record is unpacked, once per frame.
 template <int W>
 __device__ __forceinline__ void relocate(uint32_t (&p)[W], int nf, uint32_t base, uint32_t size,
                                          uint32_t dummy) {
@@ -106,27 +110,47 @@ __device__ __forceinline__ void relocate(uint32_t (&p)[W], int nf, uint32_t base
   for (int k = 0; k < 2 * W; ++k) {
     if (k >= nf) break;
     const uint32_t id = (p[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
-    const uint32_t ad = id == kNone ? base + dummy * size : base + id * size;
+    const uint32_t ad = base / size + (id == kNone ? dummy : id);
     p[k >> 1] = (p[k >> 1] & ~(0xffffu << ((k & 1) * 16))) | (ad << ((k & 1) * 16));
   }
+}
+template <typename Real, int W>
+__device__ __forceinline__ uint32_t lds_at(const uint32_t (&p)[W], int k) {
+  return (uint32_t)field(p, k) * (uint32_t)sizeof(Real);
 }
 
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// Per-wave LDS slice (the workgroup's waves never share LDS):
-//   tb[64S + 2]  check-pass operand per edge (+ dummy at 64S)
-//   eb[64S + 2]  check->variable message per edge (+ dummy at 64S)
-//   rb[64 NW]    -tx per column;  sb[64 NW] min-sum column totals
-//   nr[64S + 64NW]  sum-product: -r of each edge slot's / column slot's column
-template <typename Real, int S, int NW>
+// Sum-product runs column-centric when that computes no more tanh calls than
+// the edge form (64 NW DVN <= 64 S; the reference's H: 192 = 192).
+template <int METHOD, int S, int NW, int DVN>
+__host__ __device__ constexpr bool cols_kernel() {
+#ifdef LDPC_NO_COLS
+  return false;
+#else
+  return METHOD == 1 && NW == 1 && DVN <= S;
+#endif
+}
+
+// Per-wave LDS slice (the workgroup's waves never share LDS), regions as
+// SliceLayout (ldpc_layout.hpp), the host's bank model of the same cells:
+//   tb[64S] + 32 identity cells   check-pass operand per edge cell
+//   eb[64S] + 32 zero cells       check->variable message per edge cell
+//   rb[64 NW], sb[64 NW]          -tx / min-sum column totals per column position
+//   nr[64S + 64NW]                sum-product: -r of each edge slot's / position's column
+//   jk[64 NW]                     column-centric: sink of missing-edge scatters
+template <typename Real, int METHOD, int S, int NW, int DVN>
 struct Layout {
-  size_t per_wave, total;
-  __host__ __device__ Layout() {
-    // tb, eb, rb, sb, then nr[64 S + 64 NW]: per-lane negated channel values
-    per_wave = align16((2 * (64 * S + 2) + 2 * 64 * NW + 64 * (S + NW)) * sizeof(Real));
-    total = (size_t)kWavesPerBlock * per_wave;
-  }
+  static constexpr SliceLayout L{S, NW, cols_kernel<METHOD, S, NW, DVN>()};
+  static constexpr size_t per_wave = align16((size_t)L.end * sizeof(Real));
+  static constexpr size_t total = (size_t)kWavesPerBlock * per_wave;
 };
+
+// identity cell of 32-lane edge group g (CodeView::dpos)
+__device__ __forceinline__ uint32_t dpos_of(const CodeView &code, int g) {
+  const uint64_t w = g < 8 ? code.dpos[0] : code.dpos[1];
+  return (uint32_t)(w >> (8 * (g & 7))) & 31u;
+}
 
 // Per-wave register-resident view of the code (packed 16-bit edge ids).
 template <int S, int NW>
@@ -152,9 +176,12 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
                                              const int64_t b, WaveTables<S, NW> &wt,
                                              Real *tb, Real *eb, Real *rb, Real *sb,
                                              const int lane, const fm::LogTabEntry *logtab,
-                                             const float (&xin)[NW]) {
+                                             const float (&xin)[NW], const int (&colq)[NW],
+                                             const uint32_t (&ppos)[2]) {
   const int M = code.M, N = code.N;
-  constexpr int kDummy = 64 * S;  // index of the per-wave identity element
+  // identity cells tb[64S ..+32] and zero cells eb[64S ..+32] (SliceLayout)
+  constexpr int kDummy = 64 * S;
+  constexpr SliceLayout L = Layout<Real, METHOD, S, NW, DVN>::L;
   // Channel samples xin = tx = Re(in) * polarity (:149-153, loaded by the
   // caller, 0 past N); r = -tx (:486, :318-321).
   Real post[NW];
@@ -191,13 +218,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
     return w;
   };
 
-#ifdef LDPC_NO_COLS
-  constexpr bool kCols = false;
-#else
-  // column-centric sum-product when it computes no more tanh calls than the
-  // edge-centric form (64 NW DVN <= 64 S; the reference's H: 192 = 192)
-  constexpr bool kCols = METHOD == 1 && NW == 1 && DVN <= S;
-#endif
+  constexpr bool kCols = cols_kernel<METHOD, S, NW, DVN>();
   if constexpr (kCols) {
     // Column-centric sum-product.  A column lane has all of its column's
     // check messages after one gather, so it computes the posterior
@@ -207,22 +228,23 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
     // and scatters tanh(M(j,i)/2) to the edges' tb slots.  The edge lanes
     // then only gather row neighbours.  Saves the edge form's per-edge
     // column gathers and repeated (E + r) sums.
-    const uint32_t eb_dummy = lds_addr(eb + kDummy);
-    const uint32_t junk = lds_addr(tb + kDummy + 1);  // stores of missing edges
-    constexpr uint32_t kTbEb = (64 * S + 2) * sizeof(Real);  // eb - tb in bytes
-    if (lane == 0) tb[kDummy] = Real(1);  // product identity (missing row neighbours)
+    // a missing column entry was relocated to this lane's zero cell
+    const uint32_t eb_dummy = lds_addr(eb + kDummy + (lane & 31));
+    constexpr uint32_t kTbEb = (uint32_t)(L.eb - L.tb) * sizeof(Real);  // eb - tb in bytes
+    if (lane < 32) tb[kDummy + lane] = Real(1);  // product identity (missing row neighbours)
     uint32_t ra[S][DCN], ea[NW][DVN], ta[NW][DVN];
 #pragma unroll
     for (int s = 0; s < S; ++s)
 #pragma unroll
-      for (int k = 0; k < DCN; ++k) ra[s][k] = (uint32_t)field(wt.rn[s], k);
+      for (int k = 0; k < DCN; ++k) ra[s][k] = lds_at<Real>(wt.rn[s], k);
     Real *nr = sb + 64 * NW;  // FIN: -r of the lane's column (missing edges' term)
 #pragma unroll
     for (int q = 0; q < NW; ++q)
 #pragma unroll
       for (int k = 0; k < DVN; ++k) {
-        const uint32_t e = (uint32_t)field(wt.ce[q], k);
-        ta[q][k] = e == eb_dummy ? junk : e - kTbEb;
+        const uint32_t e = lds_at<Real>(wt.ce[q], k);
+        // missing edges scatter into the lane's own sink cell (no bank conflict)
+        ta[q][k] = e == eb_dummy ? lds_addr(tb + L.jk + lane + 64 * q) : e - kTbEb;
         ea[q][k] = (FIN && e == eb_dummy) ? lds_addr(nr + lane + 64 * q) : e;
       }
     Real rc[NW];
@@ -373,29 +395,30 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
   } else if constexpr (METHOD == 1 || METHOD == 0) {
     // the tables were relocated to LDS byte addresses (decode_small_kernel):
     // rn -> tb, cn / ce -> eb, rn field 7 -> rb (sb = rb + 64 NW elements);
-    // missing neighbours point at the dummy elements tb[64S] (1.0 for the
-    // tanh product, DBL_MAX for the minimum) and eb[64S] (0.0: an exact no-op
-    // for the min-sum column sum, whose running value is never -0.0).
-    const uint32_t eb_dummy = lds_addr(eb + kDummy);
-    if (lane == 0) {
-      tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
-      eb[kDummy] = Real(0);
+    // missing neighbours point at identity cells tb[64S + ..] (1.0 for the
+    // tanh product, DBL_MAX for the minimum) and zero cells eb[64S + ..]
+    // (0.0: an exact no-op for the min-sum column sum, whose running value is
+    // never -0.0).
+    const uint32_t eb_dummy = lds_addr(eb + kDummy + (lane & 31));
+    if (lane < 32) {
+      tb[kDummy + lane] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
+      eb[kDummy + lane] = Real(0);
     }
     // unpacked once per frame into full registers: a gather is then one
     // ds_read with no address arithmetic in the iteration loop
     uint32_t col[S], ra[S][DCN], ca[S][DVN - 1], ea[NW][DVN];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      col[s] = (uint32_t)field(wt.rn[s], 7);
+      col[s] = lds_at<Real>(wt.rn[s], 7);
 #pragma unroll
-      for (int k = 0; k < DCN; ++k) ra[s][k] = (uint32_t)field(wt.rn[s], k);
+      for (int k = 0; k < DCN; ++k) ra[s][k] = lds_at<Real>(wt.rn[s], k);
 #pragma unroll
-      for (int k = 0; k < DVN - 1; ++k) ca[s][k] = (uint32_t)field(wt.cn[s], k);
+      for (int k = 0; k < DVN - 1; ++k) ca[s][k] = lds_at<Real>(wt.cn[s], k);
     }
 #pragma unroll
     for (int q = 0; q < NW; ++q)
 #pragma unroll
-      for (int k = 0; k < DVN; ++k) ea[q][k] = (uint32_t)field(wt.ce[q], k);
+      for (int k = 0; k < DVN; ++k) ea[q][k] = lds_at<Real>(wt.ce[q], k);
     if constexpr (METHOD == 1 && FIN) {
       Real *nr = sb + 64 * NW;
 #pragma unroll
@@ -613,28 +636,29 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
     }
   }
 
-  // ---- outputs ---------------------------------------------------------
+  // ---- outputs (hard / post are by lane position; colq = the column) -----
   if (lane == 0) {
     if (a.iters) a.iters[b] = used;
     if (a.synd) a.synd[b] = weight;
   }
 #pragma unroll
   for (int q = 0; q < NW; ++q) {
-    const int c = lane + 64 * q;
-    if (c < N) {
+    const int c = colq[q];
+    if (c >= 0) {
       if (a.bits) a.bits[b * N + c] = (uint8_t)((hard[q] >> lane) & 1);
       if (a.llr) a.llr[b * N + c] = (float)post[q];
     }
   }
-  // packed info bits M.., MSB first (:207-219)
-  for (int p = lane; p < code.KB; p += 64) {
+  // packed info bits M.., MSB first (:207-219): byte `lane` (KB <= 32)
+  if (lane < code.KB) {
     uint32_t o = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = M + 8 * p + j;
-      if (c < N) o |= (uint32_t)((word_at<NW>(hard, c >> 6) >> (c & 63)) & 1) << (7 - j);
+      const int c = M + 8 * lane + j;
+      const uint32_t p = (ppos[j >> 2] >> (8 * (j & 3))) & 255u;  // position of column c
+      if (c < N) o |= (uint32_t)((word_at<NW>(hard, (int)(p >> 6)) >> (p & 63)) & 1) << (7 - j);
     }
-    a.packed[b * code.KB + p] = (uint8_t)o;
+    a.packed[b * code.KB + lane] = (uint8_t)o;
   }
   // the next frame's rb writes must not overtake this frame's LDS reads
   wave_lds_sync();
@@ -663,7 +687,9 @@ __device__ uint64_t g_timeline[4 * kTimelineFrames];
 #endif
 
 #ifndef LDPC_SMALL_MIN_BLOCKS
-#define LDPC_SMALL_MIN_BLOCKS 1
+// occupancy hint: 3 waves per SIMD (for 4-wave workgroups the compiler's
+// default, 1, gives the same register budget)
+#define LDPC_SMALL_MIN_BLOCKS (kWavesPerBlock >= 4 ? 1 : 12 / kWavesPerBlock)
 #endif
 template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax>
 __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
@@ -673,7 +699,8 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int M = code.M;
-  const Layout<Real, S, NW> L;
+  typedef Layout<Real, METHOD, S, NW, DVN> LW;
+  constexpr SliceLayout L = LW::L;
   __shared__ fm::LogTabEntry logtab[1 << fm::kLogTabBits];
   if constexpr (METHOD == 1 && PREC == 0) stage_logtab(logtab);
 
@@ -707,23 +734,42 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
     }
   }
 
-  Real *tb = reinterpret_cast<Real *>(smem + (size_t)wave * L.per_wave);
-  Real *eb = tb + (64 * S + 2);
-  Real *rb = eb + (64 * S + 2);
-  Real *sb = rb + 64 * NW;
+  Real *tb = reinterpret_cast<Real *>(smem + (size_t)wave * LW::per_wave) + L.tb;
+  Real *eb = tb + (L.eb - L.tb);
+  Real *rb = tb + (L.rb - L.tb);
+  Real *sb = tb + (L.sb - L.tb);
   if constexpr (METHOD <= 1) {
-    // ids -> LDS byte addresses of this wave's slice (see decode_frame)
+    // ids -> LDS byte addresses of this wave's slice (see decode_frame).
+    // Missing row neighbours -> the identity cell of the lane's 32-lane group,
+    // missing column entries -> the lane's zero cell: banks no other lane of
+    // the group reads (ldpc_layout.hpp)
     constexpr uint32_t R = sizeof(Real), kDummy = 64 * S;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const uint32_t cid = (uint32_t)field(wt.rn[s], 7);
-      relocate(wt.rn[s], DCN, lds_addr(tb), R, kDummy);
-      const uint32_t ca = lds_addr(rb) + (cid == kNone ? 0u : cid) * R;
+      relocate(wt.rn[s], DCN, lds_addr(tb), R, kDummy + dpos_of(code, 2 * s + (lane >> 5)));
+      const uint32_t ca = lds_addr(rb) / R + (cid == kNone ? (uint32_t)lane : cid);
       wt.rn[s][3] = (wt.rn[s][3] & 0xffffu) | (ca << 16);
-      relocate(wt.cn[s], DVN - 1, lds_addr(eb), R, kDummy);
+      relocate(wt.cn[s], DVN - 1, lds_addr(eb), R, kDummy + (lane & 31));
     }
 #pragma unroll
-    for (int q = 0; q < NW; ++q) relocate(wt.ce[q], DVN, lds_addr(eb), R, kDummy);
+    for (int q = 0; q < NW; ++q) relocate(wt.ce[q], DVN, lds_addr(eb), R, kDummy + (lane & 31));
+  }
+  // column of each of the lane's positions, and the positions of the
+  // columns of packed byte `lane` (8 bits each; N <= 256)
+  int colq[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const uint32_t c = code.lane_col[lane + 64 * q];
+    colq[q] = c == kNone ? -1 : (int)c;
+  }
+  uint32_t ppos[2] = {0u, 0u};
+  if (lane < code.KB) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = M + 8 * lane + j;
+      if (c < code.N) ppos[j >> 2] |= (uint32_t)code.col_lane[c] << (8 * (j & 3));
+    }
   }
 
 #ifndef LDPC_NO_PREFETCH
@@ -737,10 +783,7 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
     const float *ps = frame_src(a, pb < a.B ? pb : b, ppol);
     (void)ppol;  // the prefetch only pulls the samples into L2
 #pragma unroll
-    for (int q = 0; q < NW; ++q) {
-      const int c = lane + 64 * q;
-      pf[q] = c < code.N ? ps[(int64_t)c * a.elem_stride] : 0.0f;
-    }
+    for (int q = 0; q < NW; ++q) pf[q] = colq[q] >= 0 ? ps[(int64_t)colq[q] * a.elem_stride] : 0.0f;
   }
   bool first = true;
 #endif
@@ -749,28 +792,26 @@ __global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     const uint64_t c_start = __builtin_amdgcn_s_memtime();
 #endif
-    // the frame's channel samples, one load per lane and 64-column slot
-    // (coalesced); the samples past N are 0
+    // the frame's channel samples, one load per lane and column position
+    // (a permutation of the frame's N samples); positions past N are 0
     float xin[NW], pol;
     const float *src = frame_src(a, b, pol);
 #pragma unroll
-    for (int q = 0; q < NW; ++q) {
-      const int c = lane + 64 * q;
-      xin[q] = c < code.N ? src[(int64_t)c * a.elem_stride] * pol : 0.0f;
-    }
+    for (int q = 0; q < NW; ++q)
+      xin[q] = colq[q] >= 0 ? src[(int64_t)colq[q] * a.elem_stride] * pol : 0.0f;
     if constexpr (METHOD == 1) {
       bool bad = false;
 #pragma unroll
       for (int q = 0; q < NW; ++q) bad |= !__builtin_isfinite(xin[q]);
       if (__ballot(bad) == 0)
         decode_frame<PREC, METHOD, S, NW, DCN, DVN, true>(code, a, b, wt, tb, eb, rb, sb, lane,
-                                                           logtab, xin);
+                                                           logtab, xin, colq, ppos);
       else
         decode_frame<PREC, METHOD, S, NW, DCN, DVN, false>(code, a, b, wt, tb, eb, rb, sb, lane,
-                                                            logtab, xin);
+                                                            logtab, xin, colq, ppos);
     } else {
       decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane, logtab,
-                                                  xin);
+                                                  xin, colq, ppos);
     }
 #ifndef LDPC_NO_PREFETCH
     if (first) {
@@ -855,6 +896,12 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
   }
   int col = field(rn, 7);
   col = col != kNone ? col : 0;
+  int colq[NW];  // column at each of the lane's positions (-1: none)
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const uint32_t c = code.lane_col[lane + 64 * q];
+    colq[q] = c == kNone ? -1 : (int)c;
+  }
 
   int64_t b = blockIdx.x;
   while (b < a.B) {
@@ -866,7 +913,7 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
     for (int q = 0; q < NW; ++q) {
       const int c = lane + 64 * q;
       float x = 0.0f;
-      if (c < N) x = src[(int64_t)c * a.elem_stride] * pol;
+      if (colq[q] >= 0) x = src[(int64_t)colq[q] * a.elem_stride] * pol;
       rb[c] = -(Real)x;
       post[q] = (Real)x;
     }
@@ -977,8 +1024,8 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
       }
 #pragma unroll
       for (int q = 0; q < NW; ++q) {
-        const int c = lane + 64 * q;
-        if (c < N) {
+        const int c = colq[q];
+        if (c >= 0) {
           if (a.bits) a.bits[b * N + c] = (uint8_t)((hard[q] >> lane) & 1);
           if (a.llr) a.llr[b * N + c] = (float)post[q];
         }
@@ -988,7 +1035,10 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int c = M + 8 * p + j;
-          if (c < N) o |= (uint32_t)((word_at<NW>(hard, c >> 6) >> (c & 63)) & 1) << (7 - j);
+          if (c < N) {
+            const int x = code.col_lane[c];  // position of column c
+            o |= (uint32_t)((word_at<NW>(hard, x >> 6) >> (x & 63)) & 1) << (7 - j);
+          }
         }
         a.packed[b * code.KB + p] = (uint8_t)o;
       }
@@ -1006,7 +1056,7 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
 template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax>
 static int launch_one(const CodeView &code, const DecodeArgs &a, hipStream_t st) {
   typedef typename Math<PREC>::Real Real;
-  const size_t lds = Layout<Real, S, NW>().total;
+  const size_t lds = Layout<Real, METHOD, S, NW, DVN>::total;
   if (lds > 65536 &&
       hipFuncSetAttribute((const void *)decode_small_kernel<PREC, METHOD, S, NW, DCN, DVN>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

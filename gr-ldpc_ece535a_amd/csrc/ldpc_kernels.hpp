@@ -11,7 +11,12 @@
 
 namespace ldpc {
 
-constexpr int kWavesPerBlock = 4;  // one frame (codeword) per 64-lane wave
+// one frame (codeword) per 64-lane wave; waves per workgroup of the one-wave
+// kernel (a workgroup's LDS is released when its last wave ends)
+#ifndef LDPC_WAVES_PER_BLOCK
+#define LDPC_WAVES_PER_BLOCK 4
+#endif
+constexpr int kWavesPerBlock = LDPC_WAVES_PER_BLOCK;
 constexpr int kThreads = 64 * kWavesPerBlock;
 constexpr int kDcMax = 8;          // check-degree limit of the small-code kernel
 constexpr int kDvMax = 4;          // variable-degree limit
@@ -42,11 +47,19 @@ struct alignas(16) ColRec {
   uint16_t r[kDvMax];
 };  // 16 bytes
 
+// Edge records live at their edge's cell (lane slot 64 s + lane) and column
+// records at their column's lane position (lane + 64 q), both chosen per H by
+// plan_layout (ldpc_layout.hpp) so the kernel's LDS gathers are free of bank
+// conflicts; record fields hold cells / positions.  Positions 0..N-1 hold the
+// columns (in some order), positions >= N none.
 struct CodeView {
-  const EdgeRowRec *erow;    // 64 * S records
-  const EdgeColRec *ecol;    // 64 * S records
-  const ColRec *cols;        // 64 * NW records; records >= N are all kNone
-  const uint64_t *rowmask;   // M x NW words: bit c of row j <=> H(j, c) == 1
+  const EdgeRowRec *erow;    // 64 * S records, by cell
+  const EdgeColRec *ecol;    // 64 * S records, by cell
+  const ColRec *cols;        // 64 * NW records by position; records >= N are all kNone
+  const uint64_t *rowmask;   // M x NW words: bit p of row j <=> H(j, column at position p)
+  const uint16_t *lane_col;  // 64 * NW: column at position p (kNone past N)
+  const uint8_t *col_lane;   // N: position of column c
+  uint64_t dpos[2];          // byte g: identity cell (tb[64 S + dpos]) of 32-lane group g
   int M, N, E, KB, rs;       // rs = ceil(M / 64)
   int dc_max, dv_max;        // largest check / variable degree
 };

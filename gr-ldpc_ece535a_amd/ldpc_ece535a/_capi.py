@@ -18,6 +18,7 @@ METHOD_LOGDOMAIN, METHOD_SUMPRODUCT, METHOD_BITFLIP, METHOD_HARD = 0, 1, 2, 3
 PREC_F64, PREC_F32, PREC_F64_LIBM = 0, 1, 2
 FLAG_NO_REORDER = 1
 FLAG_GRAPH = 2
+FLAG_PLAIN_LAYOUT = 4
 PATH_SMALL, PATH_GRAPH = 0, 1
 MODE_LATENCY, MODE_THROUGHPUT = 0, 1
 ERRORS = {0: "LDPC_OK", -1: "LDPC_EINVAL", -2: "LDPC_EUNSUPPORTED", -3: "LDPC_EDEVICE",
@@ -40,6 +41,8 @@ SIGNATURES = {
     "ldpc_create_csr": (_vp, [_i, _i, _i32p, _i32p, _i, _i]),
     "ldpc_ctx_csr": (_i, [_vp, _i32p, _i32p]),
     "ldpc_ctx_path": (_i, [_vp]),
+    "ldpc_ctx_layout": (_i, [_vp, _i32p]),
+    "ldpc_plan_layout": (_i, [_u8p, _i, _i, _i, _i32p, _i32p, _i32p]),
     "ldpc_set_work_limit": (_i, [_vp, _i64]),
     "ldpc_encode_device": (_i, [_vp, _vp, _i, _vp, _vp]),
     "ldpc_random_bits": (_i, [_vp, _i64, ctypes.c_uint64, _vp]),
@@ -132,16 +135,39 @@ def encode(Hr, data_bits):
     return out
 
 
+def plan_layout(H, reorder=True, plain=False):
+    """The small-code kernel's LDS layout for H (host only, no GPU): dict with
+    cell (E,) = lane slot of each edge in CSR order of the decoder's H, pos (N,)
+    = lane position of each column, and model = {searched, cc, ec, plain_cc,
+    plain_ec}: modelled extra LDS bank-conflict cycles per iteration of the
+    column-centric sum-product / min-sum kernels for this layout and for the
+    plain CSR layout (csrc/ldpc_layout.hpp)."""
+    H = np.ascontiguousarray(H, np.uint8)
+    M, N = H.shape
+    flags = (0 if reorder else FLAG_NO_REORDER) | (FLAG_PLAIN_LAYOUT if plain else 0)
+    cell = np.zeros(M * N, np.int32)
+    pos = np.zeros(N, np.int32)
+    model = np.zeros(5, np.int32)
+    E = _check(lib().ldpc_plan_layout(_p(H, _u8p), M, N, flags, _p(cell, _i32p), _p(pos, _i32p),
+                                      _p(model, _i32p)))
+    return dict(cell=cell[:E].copy(), pos=pos,
+                model=dict(zip(("searched", "cc", "ec", "plain_cc", "plain_ec"),
+                               (int(v) for v in model))))
+
+
 class Decoder:
     """One decode context (device tables + stream) for one H.
 
     H: dense (M, N) 0/1 matrix (reorderHMatrix applied unless reorder=False),
     or csr=(M, N, row_ptr, col_idx) for a sparse H used as given.
     force_graph=True selects the large-code (HBM message) kernels even for a
-    code the small-code kernel could take."""
+    code the small-code kernel could take; plain_layout=True keeps the
+    small-code kernel's edges and columns in CSR order (A/B and tests)."""
 
-    def __init__(self, H=None, reorder=True, device=0, csr=None, force_graph=False):
-        flags = (0 if reorder else FLAG_NO_REORDER) | (FLAG_GRAPH if force_graph else 0)
+    def __init__(self, H=None, reorder=True, device=0, csr=None, force_graph=False,
+                 plain_layout=False):
+        flags = ((0 if reorder else FLAG_NO_REORDER) | (FLAG_GRAPH if force_graph else 0) |
+                 (FLAG_PLAIN_LAYOUT if plain_layout else 0))
         if csr is not None:
             M, N, rp, ci = csr
             rp = np.ascontiguousarray(rp, np.int32)
@@ -167,6 +193,13 @@ class Decoder:
         _check(lib().ldpc_ctx_csr(self._ctx, _p(self.row_ptr, _i32p), _p(self.col_idx, _i32p)),
                self._ctx)
         self._H = None
+
+    @property
+    def layout_model(self):
+        """ldpc_ctx_layout: {searched, cc, ec, plain_cc, plain_ec} (see plan_layout)."""
+        m = np.zeros(5, np.int32)
+        _check(lib().ldpc_ctx_layout(self._ctx, _p(m, _i32p)), self._ctx)
+        return dict(zip(("searched", "cc", "ec", "plain_cc", "plain_ec"), (int(v) for v in m)))
 
     @property
     def H(self):

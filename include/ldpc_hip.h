@@ -66,6 +66,8 @@ extern "C" {
 /* ldpc_create flags */
 #define LDPC_FLAG_NO_REORDER 1 /* use H as given (skip reorderHMatrix) */
 #define LDPC_FLAG_GRAPH 2      /* force the large-code (HBM message) kernels */
+#define LDPC_FLAG_PLAIN_LAYOUT 4 /* small codes: edges / columns in CSR order (no
+                                    LDS bank-conflict layout search; A/B only) */
 
 /* error codes */
 #define LDPC_OK 0
@@ -108,6 +110,17 @@ int ldpc_encode(const uint8_t *H_reordered, int M, int N,
 int ldpc_alist_read(const char *path, int *M_out, int *N_out, int32_t *row_ptr_opt,
                     int32_t *col_idx_opt, int64_t col_idx_cap);
 
+/* The small-code kernel's LDS layout for H (no GPU; reorderHMatrix applied
+ * unless LDPC_FLAG_NO_REORDER, search skipped with LDPC_FLAG_PLAIN_LAYOUT):
+ * the cell (lane slot) of every edge in CSR order of the decoder's H, the lane
+ * position of every column, and model_out = {searched, modelled extra LDS
+ * bank-conflict cycles per iteration of the column-centric sum-product and of
+ * the min-sum kernel, the same two for the plain CSR layout}.  Returns E, or
+ * a negative code (a code outside the small-code kernel: LDPC_EUNSUPPORTED).
+ * Diagnostic / test helper; ldpc_create plans the same layout. */
+int ldpc_plan_layout(const uint8_t *H, int M, int N, int flags, int32_t *cell_out_opt,
+                     int32_t *pos_out_opt, int32_t *model_out_opt);
+
 /* ---- device context ----------------------------------------------- */
 
 /* Builds the decoder's view of H (reorderHMatrix unless
@@ -138,6 +151,9 @@ int ldpc_ctx_csr(const ldpc_ctx *ctx, int32_t *row_ptr_out, int32_t *col_idx_out
 /* 0: small-code kernel (frame per wave / workgroup, registers + LDS);
  * 1: large-code kernels (messages in HBM). */
 int ldpc_ctx_path(const ldpc_ctx *ctx);
+/* The context's layout model (5 ints, as ldpc_plan_layout's model_out);
+ * LDPC_EUNSUPPORTED for a large-code context. */
+int ldpc_ctx_layout(const ldpc_ctx *ctx, int32_t *model_out);
 
 /* ---- decode ------------------------------------------------------- */
 /* Common parameters:
