@@ -3,30 +3,28 @@
  * LDPC decoder block implementation (MI355X edition).
  *
  * general_work reproduces lib/ldpc_decoder_cb_impl.cc:133-234 of
- * gr-ldpc_ece535a output for output, for any chunking of the input:
- *
- *  - IN_SYNC / IN_SYNC_INVERTED: the windows at consumed, consumed+64, ...
- *    that fit the input and output buffers are decoded in ONE GPU launch
- *    with the state's polarity; the reference's per-frame decisions are then
- *    replayed in order.  A frame that fails (syndrome weight > M/8) bumps the
- *    error counter and is still emitted (:168-176, :207-225); the 11th
- *    failure drops sync, retries the same window negated -- with the quirk
- *    that the negation is relative to the polarity the window was decoded
- *    with (:180-191) -- and either re-syncs inverted or skips one sample.
- *    Results past a state change are discarded and re-decoded.
- *  - OUT_OF_SYNC: candidate start positions (1-sample steps, :194-198) are
- *    decoded at both polarities in one launch per batch, in batches of 64,
- *    256, 1024, ... positions; the first position whose +tx or, failing
- *    that, -tx decode passes the frame check wins, exactly as the
- *    reference's serial search would find, and the search stops at the first
- *    batch that holds one (a sync loss costs ~128 decodes when the frame
- *    boundary is near, not two decodes per visible sample).
+ * gr-ldpc_ece535a output for output, for any chunking of the input.  The
+ * reference loop decodes one window per step -- the N samples at the
+ * current position times +-1 -- and its state machine decides the next
+ * position.  Here the loop is replayed exactly over a memo of decoded
+ * windows; when it reaches a window not decoded yet, a dry run of the same
+ * loop goes ahead on guesses (a frame in sync passes, an out-of-sync
+ * position and a "-tx" retry fail) and collects every window it touches --
+ * the rest of the in-sync frames, and at each sync loss the retry plus the
+ * search positions up to the next frame boundary -- and all of them are
+ * decoded in ONE GPU launch (ldpc_decode_windows: any positions, either
+ * polarity, one staged copy of the input).  The exact replay then goes on;
+ * a wrong guess only means another launch.  An out-of-sync search that
+ * finds nothing within its budget (128 positions) widens it x4 per launch.
+ * A typical call costs two launches (the frames, then every sync loss's
+ * search) instead of three per sync loss.
  *
  * The H is the reference's default (make(method)), or a runtime H (dense,
  * reordered like the reference's constructor; CSR; or an alist file).
  *
- * Decoding is deterministic per window, so the batched schedule emits the
- * same bytes, consumes the same items and leaves the same state as the
+ * Decoding is deterministic per window and the replay only ever uses real
+ * decode results, so the block emits the same bytes, consumes the same
+ * items, prints the same sync messages and leaves the same state as the
  * reference's frame-at-a-time loop.
  */
 #include "ldpc_decoder_cb_impl.h"
@@ -47,8 +45,8 @@ namespace ldpc_ece535a {
 #define STATE_IN_SYNC_INVERTED 2
 
 namespace {
-const int kMaxWindows = 1 << 16;  // windows per launch (bounds staging memory)
-const int kSearchFirst = 64;      // first OUT_OF_SYNC batch; x4 per batch after
+const int kMaxWindows = 1 << 17;  // windows per launch (bounds staging memory)
+const int kSearchFirst = 128;     // out-of-sync positions a launch first guesses past; x4 after
 const size_t kDenseMax = (size_t)1 << 22;  // alist codes up to M N entries go dense
 
 void print_method(int method) {
@@ -175,44 +173,121 @@ void ldpc_decoder_cb_impl::forecast(int noutput_items, gr_vector_int &ninput_ite
   ninput_items_required[0] = noutput_items * d_N;
 }
 
-void ldpc_decoder_cb_impl::decode_both(const float *in, int64_t n_floats, int B) {
-  if (d_backend) {  // the test seam decodes one polarity per call
-    decode_windows(in, n_floats, 1, 1.0f, B, 0);
-    decode_windows(in, n_floats, 1, -1.0f, B, 1);
-    return;
-  }
+void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
   const int KB = (int)(d_N - d_M + 7) / 8;
-  d_packed[0].resize((size_t)2 * B * KB);
-  d_synd[0].resize((size_t)2 * B);
-  const int rc = ldpc_decode_strided_both(d_ctx, d_method, (int)d_iterations, 1, d_precision, in,
-                                          n_floats, 2, 2, 1.0f, B, d_packed[0].data(),
-                                          d_synd[0].data());
-  if (rc < 0)
-    throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
-                             ldpc_last_error(d_ctx));
-  // rows B.. are the -tx decodes
-  d_packed[1].assign(d_packed[0].begin() + (size_t)B * KB, d_packed[0].end());
-  d_synd[1].assign(d_synd[0].begin() + B, d_synd[0].end());
-  d_frames_decoded += 2 * (int64_t)B;
+  const int B = (int)d_want.size();
+  d_wsynd.assign((size_t)B, 0);
+  d_wpacked.assign((size_t)B * KB, 0);
+  if (d_backend) {
+    // the test seam decodes equally spaced windows of one polarity per call
+    for (int i = 0; i < B;) {
+      const int64_t p0 = d_want[i] >> 1, pol = d_want[i] & 1;
+      int j = i + 1;
+      int64_t step = 0;
+      if (j < B && (d_want[j] & 1) == pol && (d_want[j] >> 1) > p0) {
+        step = (d_want[j] >> 1) - p0;
+        while (j < B && (d_want[j] & 1) == pol && (d_want[j] >> 1) - (d_want[j - 1] >> 1) == step)
+          ++j;
+      }
+      const int n = j - i;
+      const int rc = d_backend(d_backend_user, in + 2 * p0, 2 * ((int64_t)nin - p0),
+                               2 * std::max<int64_t>(step, 1), 2, pol ? -1.0f : 1.0f, n,
+                               &d_wpacked[(size_t)i * KB], &d_wsynd[i]);
+      if (rc < 0) throw std::runtime_error("ldpc_decoder_cb: decode failed: backend error");
+      i = j;
+    }
+  } else {
+    const int rc = ldpc_decode_windows(d_ctx, d_method, (int)d_iterations, 1, d_precision, in,
+                                       2 * (int64_t)nin, 2, first ? 0 : 1, d_want.data(), B,
+                                       d_wpacked.data(), d_wsynd.data());
+    if (rc < 0)
+      throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
+                               ldpc_last_error(d_ctx));
+  }
+  for (int b = 0; b < B; ++b) {
+    d_memo[d_want[b] & 1][d_want[b] >> 1] = (int32_t)d_rsynd.size();
+    d_rsynd.push_back(d_wsynd[b]);
+    d_rpacked.insert(d_rpacked.end(), d_wpacked.begin() + (size_t)b * KB,
+                     d_wpacked.begin() + (size_t)(b + 1) * KB);
+  }
+  d_frames_decoded += B;
 }
 
-void ldpc_decoder_cb_impl::decode_windows(const float *in, int64_t n_floats, int stride,
-                                          float polarity, int B, int slot) {
-  const int KB = (int)(d_N - d_M + 7) / 8;
-  d_packed[slot].resize((size_t)B * KB);
-  d_synd[slot].resize((size_t)B);
-  int rc;
-  if (d_backend)
-    rc = d_backend(d_backend_user, in, n_floats, 2 * (int64_t)stride, 2, polarity, B,
-                   d_packed[slot].data(), d_synd[slot].data());
-  else
-    rc = ldpc_decode_strided(d_ctx, d_method, (int)d_iterations, 1, d_precision, in, n_floats,
-                             2 * (int64_t)stride, 2, polarity, B, d_packed[slot].data(),
-                             nullptr, nullptr, d_synd[slot].data(), nullptr);
-  if (rc < 0)
-    throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
-                             (d_ctx ? ldpc_last_error(d_ctx) : "backend error"));
-  d_frames_decoded += B;
+ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact, int nin,
+                                                           int noutput, unsigned char *out,
+                                                           int max_out, size_t max_want) {
+  const int N = (int)d_N;
+  const int mo = d_out_bytes;                      // :141 (M/8)
+  const int thr = (int)d_M / 8;                    // :142
+  const int KB = (N - (int)d_M + 7) / 8;
+  int out_run = 0;  // dry run: out-of-sync positions in a row with a guessed window
+  while ((nin - r.consumed) >= N && (noutput - r.produced) >= mo) {  // :146-147
+    const int pos = r.consumed;
+    const int pol = r.state == STATE_IN_SYNC_INVERTED ? 1 : 0;  // tx = Re * -1 (:149-153)
+    Replay n = r;
+    bool guessed_out = false, lost = false, inverted = false, synced = false;
+    // checkFrame(vhat, M/8) > M/8 (:166-168); it stops counting past the
+    // threshold, so comparing the full weight gives the same decision
+    int32_t use = d_memo[pol][pos];
+    bool pass;
+    if (use >= 0) {
+      pass = d_rsynd[use] <= thr;
+    } else {
+      if (exact) return STALLED;
+      d_want.push_back(((int64_t)pos << 1) | pol);
+      pass = r.state != STATE_OUT_OF_SYNC;  // frames in sync mostly pass
+      guessed_out = !pass;
+    }
+    if (!pass) {
+      if (n.state != STATE_OUT_OF_SYNC) {  // :169-176
+        n.errors++;
+        if (n.errors > 10) {
+          n.errors = 0;
+          n.state = STATE_OUT_OF_SYNC;
+          lost = true;
+        }
+      }
+      if (n.state == STATE_OUT_OF_SYNC) {  // the "-tx" retry, :178-198
+        const int32_t i2 = d_memo[pol ^ 1][pos];
+        bool pass2 = false;
+        if (i2 >= 0) {
+          pass2 = d_rsynd[i2] <= thr;
+        } else {
+          if (exact) return STALLED;
+          d_want.push_back(((int64_t)pos << 1) | (pol ^ 1));
+          guessed_out = true;  // a retry that fails mostly
+        }
+        if (pass2) {
+          n.state = STATE_IN_SYNC_INVERTED;
+          n.errors = 0;
+          use = i2;
+          inverted = true;
+        } else {
+          n.consumed += 1;  // skip one sample (:193-197)
+        }
+      }
+    } else if (n.state == STATE_OUT_OF_SYNC) {  // :201-205
+      n.state = STATE_IN_SYNC;
+      n.errors = 0;
+      synced = true;
+    }
+    if (n.state == STATE_IN_SYNC || n.state == STATE_IN_SYNC_INVERTED) {  // :207-225
+      if (exact) std::memcpy(out + n.produced, &d_rpacked[(size_t)use * KB], (size_t)mo);
+      n.consumed += N;
+      n.produced += mo;
+    }
+    if (exact) {
+      if (lost) std::cout << "MAX ERRORS; OUT OF SYNC" << std::endl;
+      if (inverted) std::cout << "IN SYNC; PHASE INVERTED" << std::endl;
+      if (synced) std::cout << "IN SYNC" << std::endl;
+    }
+    r = n;
+    if (!exact) {
+      out_run = (guessed_out && r.state == STATE_OUT_OF_SYNC) ? out_run + 1 : 0;
+      if (out_run >= max_out || d_want.size() >= max_want) return STALLED;
+    }
+  }
+  return DONE;
 }
 
 int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_items,
@@ -221,87 +296,35 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   const float *in = (const float *)input_items[0];  // interleaved re/im
   unsigned char *out = (unsigned char *)output_items[0];
   const int N = (int)d_N;
-  const int min_output_required = d_out_bytes;      // :141 (M/8)
-  const int frame_error_threshold = (int)d_M / 8;   // :142
-  const int KB = (N - (int)d_M + 7) / 8;
   const int nin = ninput_items[0];
+  const size_t npos = (size_t)std::max(nin - N + 1, 0);
+  d_memo[0].assign(npos, -1);
+  d_memo[1].assign(npos, -1);
+  d_rsynd.clear();
+  d_rpacked.clear();
 
-  int input_consumed = 0;
-  int output_produced = 0;
-  int search_batch = kSearchFirst;
-  // checkFrame(vhat, threshold) stops counting at threshold+1 (:247-249)
-  auto capped = [&](int32_t w) { return std::min<int32_t>(w, frame_error_threshold + 1); };
-  auto emit = [&](const uint8_t *bytes) {
-    std::memcpy(out + output_produced, bytes, (size_t)min_output_required);
-    input_consumed += N;
-    output_produced += min_output_required;
-  };
-
-  while ((nin - input_consumed) >= N && (noutput_items - output_produced) >= min_output_required) {
-    const float *here = in + 2 * (int64_t)input_consumed;
-    const int64_t avail = 2 * (int64_t)(nin - input_consumed);
-    if (d_state != STATE_OUT_OF_SYNC) {
-      const float pol = d_state == STATE_IN_SYNC_INVERTED ? -1.0f : 1.0f;
-      int W = (nin - input_consumed) / N;
-      if (min_output_required > 0)
-        W = std::min(W, (noutput_items - output_produced) / min_output_required);
-      W = std::min(W, kMaxWindows);
-      decode_windows(here, avail, N, pol, W, 0);
-      for (int w = 0; w < W; ++w) {
-        const int sNotZero = capped(d_synd[0][w]);
-        if (sNotZero > frame_error_threshold) {
-          d_errors++;
-          if (d_errors > 10) {  // :171-175
-            d_errors = 0;
-            d_state = STATE_OUT_OF_SYNC;
-            std::cout << "MAX ERRORS; OUT OF SYNC" << std::endl;
-            // retry this window with -tx, tx taken at the old polarity (:178-191)
-            const float *win = in + 2 * (int64_t)input_consumed;
-            decode_windows(win, 2 * (int64_t)(nin - input_consumed), N, -pol, 1, 1);
-            if (capped(d_synd[1][0]) <= frame_error_threshold) {
-              std::cout << "IN SYNC; PHASE INVERTED" << std::endl;
-              d_state = STATE_IN_SYNC_INVERTED;
-              d_errors = 0;
-              emit(d_packed[1].data());
-            } else {
-              input_consumed += 1;  // :194-198
-            }
-            break;  // the rest of the batch was decoded for the old state
-          }
-        }
-        emit(&d_packed[0][(size_t)w * KB]);
-      }
-    } else {
-      // start positions with a full window, both polarities in one launch,
-      // in growing batches (the first batch is small: the frame boundary is
-      // usually near); one failed position consumes one sample (:194-198)
-      int P = std::min(nin - input_consumed - N + 1, std::min(search_batch, kMaxWindows));
-      search_batch = std::min(4 * search_batch, kMaxWindows);
-      decode_both(here, avail, P);
-      for (int p = 0; p < P; ++p) {
-        if (capped(d_synd[0][p]) <= frame_error_threshold) {  // :201-205
-          search_batch = kSearchFirst;
-          std::cout << "IN SYNC" << std::endl;
-          d_state = STATE_IN_SYNC;
-          d_errors = 0;
-          emit(&d_packed[0][(size_t)p * KB]);
-          break;
-        }
-        if (capped(d_synd[1][p]) <= frame_error_threshold) {  // :189-192
-          search_batch = kSearchFirst;
-          std::cout << "IN SYNC; PHASE INVERTED" << std::endl;
-          d_state = STATE_IN_SYNC_INVERTED;
-          d_errors = 0;
-          emit(&d_packed[1][(size_t)p * KB]);
-          break;
-        }
-        input_consumed += 1;  // skip one sample and search on
-      }
-    }
+  Replay r{d_state, d_errors, 0, 0};
+  int out_budget = kSearchFirst;  // out-of-sync positions one launch may guess past
+  bool first = true, last_out = false;
+  while (replay(r, true, nin, noutput_items, out, 0, 0) == STALLED) {
+    // the loop needs a window not decoded yet: dry-run ahead from here to
+    // collect the windows it will probably need, and decode them at once
+    const bool now_out = r.state == STATE_OUT_OF_SYNC;
+    if (now_out && last_out)
+      out_budget = std::min(4 * out_budget, kMaxWindows);  // the search goes on: wider
+    else if (!now_out)
+      out_budget = kSearchFirst;
+    last_out = now_out;
+    d_want.clear();
+    Replay dry = r;
+    replay(dry, false, nin, noutput_items, nullptr, out_budget, (size_t)kMaxWindows);
+    decode_wanted(in, nin, first);
+    first = false;
   }
-
-  consume_each(input_consumed);
-  return output_produced;
+  d_state = r.state;
+  d_errors = r.errors;
+  consume_each(r.consumed);
+  return r.produced;
 }
 
 }  // namespace ldpc_ece535a

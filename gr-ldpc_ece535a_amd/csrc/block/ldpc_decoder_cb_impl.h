@@ -5,9 +5,9 @@
  * Keeps the reference's block contract (lib/ldpc_decoder_cb_impl.h:22-66):
  * 64 gr_complex in -> 4 bytes out per frame, methods 0..3, the frame-sync /
  * polarity state machine.  What changes is how frames are decoded: instead
- * of one CPU decode per 64-sample window, general_work decodes every window
- * it can already see in one GPU launch and then replays the reference's
- * state machine over the results (see ldpc_decoder_cb_impl.cc).
+ * of one CPU decode per 64-sample window, general_work predicts the windows
+ * the reference loop will decode, decodes them in one GPU launch and replays
+ * the reference's state machine over the results (see ldpc_decoder_cb_impl.cc).
  */
 #ifndef INCLUDED_LDPC_ECE535A_LDPC_DECODER_CB_IMPL_H
 #define INCLUDED_LDPC_ECE535A_LDPC_DECODER_CB_IMPL_H
@@ -36,16 +36,36 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   ldpc_block_backend_fn d_backend;  // test seam; null = GPU
   void *d_backend_user;
   int64_t d_frames_decoded;
-  std::vector<uint8_t> d_packed[2];
-  std::vector<int32_t> d_synd[2];
 
-  // Decodes B windows of the interleaved complex input starting at `in`
-  // (window b starts b*stride samples in), tx = Re * polarity.
-  void decode_windows(const float *in, int64_t n_floats, int stride, float polarity, int B,
-                      int slot);
-  // Decodes B one-sample-step windows at +tx into slot 0 and -tx into slot 1
-  // (one launch on the GPU).
-  void decode_both(const float *in, int64_t n_floats, int B);
+  // general_work's decode memo for the current call: the result of window
+  // (position p, polarity) -- p in samples from the call's first input item,
+  // polarity 0 = +tx, 1 = -tx -- is entry d_memo[pol][p] of d_rsynd /
+  // d_rpacked (-1: not decoded).  Keys are (p << 1) | pol.
+  std::vector<int32_t> d_memo[2];
+  std::vector<int32_t> d_rsynd;
+  std::vector<uint8_t> d_rpacked;
+  std::vector<int64_t> d_want;   // keys of the next launch
+  std::vector<int32_t> d_wsynd;  // its outputs
+  std::vector<uint8_t> d_wpacked;
+
+  // The reference loop's progress (:140-234), for exact replay and for the
+  // speculative dry run that picks the next launch's windows.
+  struct Replay {
+    int state;
+    unsigned int errors;
+    int consumed, produced;
+  };
+  enum Outcome { DONE, STALLED };
+  // Runs the reference loop from r over the memo.  exact: stops (without
+  // taking the step) at the first window not decoded yet and commits
+  // outputs; dry: guesses missing windows (pass while in sync, fail out of
+  // sync), records them in d_want and stops after max_out consecutive
+  // out-of-sync positions with missing windows, or max_want keys.
+  Outcome replay(Replay &r, bool exact, int nin, int noutput, unsigned char *out, int max_out,
+                 size_t max_want);
+  // Decodes the windows d_want of the call's input into the memo (one
+  // launch on the GPU; the test seam decodes runs of equally spaced windows).
+  void decode_wanted(const float *in, int nin, bool first);
   void adopt(ldpc_ctx *ctx);  // takes M, N from the context; checks the output shape
 
  public:

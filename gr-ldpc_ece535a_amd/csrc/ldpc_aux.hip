@@ -16,6 +16,8 @@
 //                  convention (apps/ldpc_lapack.cpp:629-636).
 //   count_errors   per-frame count of positions where two 0/1 arrays differ
 //                  (biterr, apps/ldpc_lapack.cpp:508-517, before the division).
+//   gather_windows the windows a decoder block asks for (any start sample, either
+//                  polarity) copied out of one staged sample span into frames.
 #include <hip/hip_runtime.h>
 
 #include "ldpc_aux.hpp"
@@ -191,6 +193,27 @@ int launch_encode_ira(const int32_t *rp, const int32_t *ci, int M, int K, const 
   if (B <= 0) return 0;
   k_encode_ira<<<B, 256, 0, (hipStream_t)stream>>>(rp, ci, M, K, data, cw);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+namespace {
+__global__ void __launch_bounds__(256) k_gather_windows(const float *span, const int64_t *win,
+                                                        int64_t total, int N, float *out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int64_t b = t / N, i = t - b * N;
+  const int64_t w = win[b];
+  const float v = span[(w >> 1) + i];
+  out[t] = (w & 1) ? -v : v;  // negation is exact: the decoder sees tx = -Re exactly
+}
+}  // namespace
+
+int launch_gather_windows(const float *span, const int64_t *win, int B, int N, float *out,
+                          void *stream) {
+  const int64_t total = (int64_t)B * N;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(k_gather_windows, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, span, win, total, N, out);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 }  // namespace ldpc

@@ -17,4 +17,9 @@ int launch_encode_small(const uint64_t *A, int M, int K, const uint8_t *data, in
 int launch_encode_ira(const int32_t *rp, const int32_t *ci, int M, int K, const uint8_t *data,
                       int B, uint8_t *cw, void *stream);
 
+// out[b*N + i] = +-span[(win[b] >> 1) + i]: the N samples of window b, negated
+// when bit 0 of win[b] is set (the block's decode-any-window batches).
+int launch_gather_windows(const float *span, const int64_t *win, int B, int N, float *out,
+                          void *stream);
+
 }  // namespace ldpc

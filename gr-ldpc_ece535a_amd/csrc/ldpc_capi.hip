@@ -44,6 +44,13 @@ struct ldpc_ctx {
   float *h_stage = nullptr;  // pinned host staging of host-buffer decodes
   size_t h_stage_bytes = 0;
   int32_t *h_ctrl = nullptr;  // pinned progress words of the min-sum pipeline
+  // ldpc_decode_windows: the staged sample span (device), window list and
+  // frames; span_samples > 0 while the staged span may be reused
+  void *d_wstage = nullptr;
+  size_t wstage_bytes = 0;
+  int64_t *h_win = nullptr;
+  size_t h_win_bytes = 0;
+  int64_t span_samples = 0;
   bool ms_pipeline = true;    // large-code min-sum: compressed messages + pipeline
   // small-code frame queues: one monotonic counter per stream that has
   // launched on this context (ldpc_kernels.hpp DecodeArgs::ticket)
@@ -838,6 +845,8 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->d_stage) (void)hipFree(ctx->d_stage);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
+  if (ctx->d_wstage) (void)hipFree(ctx->d_wstage);
+  if (ctx->h_win) (void)hipHostFree(ctx->h_win);
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
     if (p) (void)hipFree(p);
@@ -1131,9 +1140,107 @@ int decode_host_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, in
   return LDPC_OK;
 }
 
+// ldpc_decode_windows: span in ctx->d_wstage [0, span), then the window list,
+// the gathered frames and the outputs.
+int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+                        const float *in, int64_t n_in_floats, int elem_stride, int reuse_span,
+                        const int64_t *win, int B, uint8_t *out_packed, int32_t *syn_weight_opt) {
+  int rc = check_decode_args(ctx, method, max_iters, et_period, precision, B, elem_stride,
+                             ctx ? ctx->N : 1);
+  if (rc != LDPC_OK) return rc;
+  if (B == 0) return LDPC_OK;
+  if (!in || !win || !out_packed) return set_err(ctx, LDPC_EINVAL, "null buffer");
+  const int N = ctx->N;
+  const int64_t S = (n_in_floats + elem_stride - 1) / elem_stride;  // samples in the span
+  for (int b = 0; b < B; ++b)
+    if (win[b] < 0 || (win[b] >> 1) + N > S)
+      return set_err(ctx, LDPC_EINVAL, "window outside the input span");
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t b_span = al((size_t)S * 4), b_win = al((size_t)B * 8),
+               b_fr = al((size_t)B * N * 4), b_pk = al((size_t)B * ctx->KB),
+               b_sy = al((size_t)B * 4);
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  const size_t need = b_span + b_win + b_fr + b_pk + b_sy;
+  if (need > ctx->wstage_bytes) {
+    // a bigger span moves everything: the staged span is gone
+    if (ctx->d_wstage) {
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipFree(ctx->d_wstage);
+      ctx->d_wstage = nullptr;
+      ctx->wstage_bytes = 0;
+    }
+    ctx->span_samples = 0;
+    const size_t want = std::max(need + need / 2, (size_t)4 << 20);
+    if ((e = hipMalloc(&ctx->d_wstage, want)) != hipSuccess)
+      return hip_err(ctx, e, "hipMalloc(window staging)");
+    ctx->wstage_bytes = want;
+  }
+  if ((size_t)B * 8 > ctx->h_win_bytes) {
+    if (ctx->h_win) {
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipHostFree(ctx->h_win);
+      ctx->h_win = nullptr;
+    }
+    const size_t want = std::max((size_t)B * 8, (size_t)1 << 16);
+    if ((e = hipHostMalloc((void **)&ctx->h_win, want, hipHostMallocDefault)) != hipSuccess)
+      return hip_err(ctx, e, "hipHostMalloc(windows)");
+    ctx->h_win_bytes = want;
+  }
+  // the span sits at the start of the staging area; a reused span must be the
+  // one staged last, with the same length (then it ends before span_cap)
+  char *base = (char *)ctx->d_wstage;
+  const size_t span_cap = ctx->wstage_bytes - (b_win + b_fr + b_pk + b_sy);
+  float *d_span = (float *)base;
+  int64_t *d_win = (int64_t *)(base + span_cap);
+  float *d_fr = (float *)(base + span_cap + b_win);
+  uint8_t *d_pk = (uint8_t *)(base + span_cap + b_win + b_fr);
+  int32_t *d_sy = (int32_t *)(base + span_cap + b_win + b_fr + b_pk);
+  if (!(reuse_span && ctx->span_samples == S)) {
+    rc = ensure_host_stage(ctx, (size_t)S * 4);
+    if (rc != LDPC_OK) return rc;
+    float *h = ctx->h_stage;
+    if (elem_stride == 1)
+      memcpy(h, in, (size_t)S * 4);
+    else
+      for (int64_t i = 0; i < S; ++i) h[i] = in[i * elem_stride];
+    if ((e = hipMemcpyAsync(d_span, h, (size_t)S * 4, hipMemcpyHostToDevice, ctx->stream)) !=
+        hipSuccess)
+      return hip_err(ctx, e, "hipMemcpyAsync(span)");
+    ctx->span_samples = S;
+  }
+  // the previous call's copy out of h_win has completed (it synchronised)
+  memcpy(ctx->h_win, win, (size_t)B * 8);
+  if ((e = hipMemcpyAsync(d_win, ctx->h_win, (size_t)B * 8, hipMemcpyHostToDevice,
+                          ctx->stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipMemcpyAsync(windows)");
+  if (ldpc::launch_gather_windows(d_span, d_win, B, N, d_fr, ctx->stream) != 0)
+    return set_err(ctx, LDPC_EDEVICE, "gather_windows launch failed");
+  rc = decode_device_impl(ctx, method, max_iters, et_period, precision, d_fr, N, 1, 1.0f, B, 0,
+                          d_pk, nullptr, nullptr, syn_weight_opt ? d_sy : nullptr, nullptr,
+                          ctx->stream);
+  if (rc != LDPC_OK) return rc;
+  if ((e = hipMemcpyAsync(out_packed, d_pk, (size_t)B * ctx->KB, hipMemcpyDeviceToHost,
+                          ctx->stream)) != hipSuccess ||
+      (syn_weight_opt && (e = hipMemcpyAsync(syn_weight_opt, d_sy, (size_t)B * 4,
+                                             hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess))
+    return hip_err(ctx, e, "hipMemcpyAsync(out)");
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipStreamSynchronize");
+  return LDPC_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int ldpc_decode_windows(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+                        const float *in, int64_t n_in_floats, int elem_stride, int reuse_span,
+                        const int64_t *windows, int B, uint8_t *out_packed,
+                        int32_t *syn_weight_opt) {
+  return decode_windows_impl(ctx, method, max_iters, et_period, precision, in, n_in_floats,
+                             elem_stride, reuse_span, windows, B, out_packed, syn_weight_opt);
+}
 
 int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
                        const float *d_in, int64_t cw_stride, int elem_stride, float polarity,
@@ -1182,10 +1289,12 @@ int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu) {
 int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode) {
   if (!ctx || (mode != LDPC_MODE_LATENCY && mode != LDPC_MODE_THROUGHPUT))
     return set_err(ctx, LDPC_EINVAL, "mode must be LDPC_MODE_LATENCY or LDPC_MODE_THROUGHPUT");
-  // measured on the config-2 batch (profiles/round2/ab_launch_mode.txt):
-  // one launch at a time: 12 waves per CU, priority for starved waves;
-  // overlapping launches: 10 waves per CU, no priority games
-  ctx->waves_per_cu = mode == LDPC_MODE_THROUGHPUT ? 10 : 0;
+  // measured on the config-2 batch (profiles/round2/ab_launch_mode.txt,
+  // profiles/round2/layout/sweep_inflight_wpc.txt): one launch at a time: 12
+  // waves per CU, priority for starved waves; overlapping launches: 6 waves
+  // per CU each (3 launches in flight fill the CU's 12 wave slots with room
+  // for the next launch's first waves), no priority games
+  ctx->waves_per_cu = mode == LDPC_MODE_THROUGHPUT ? 6 : 0;
   ctx->fair_cycles = mode == LDPC_MODE_THROUGHPUT ? 0 : 1800;
   return LDPC_OK;
 }

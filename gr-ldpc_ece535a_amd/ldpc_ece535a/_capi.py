@@ -59,6 +59,8 @@ SIGNATURES = {
                                 _vp, _vp, _vp, _vp, _vp, _vp]),
     "ldpc_decode_strided_both": (_i, [_vp, _i, _i, _i, _i, _f32p, _i64, _i64, _i,
                                      ctypes.c_float, _i, _u8p, _i32p]),
+    "ldpc_decode_windows": (_i, [_vp, _i, _i, _i, _i, _f32p, _i64, _i, _i,
+                                 ctypes.POINTER(ctypes.c_int64), _i, _u8p, _i32p]),
     "ldpc_alist_read": (_i, [ctypes.c_char_p, _i32p, _i32p, _i32p, _i32p, _i64]),
     "ldpc_set_waves_per_cu": (_i, [_vp, _i]),
     "ldpc_set_launch_mode": (_i, [_vp, _i]),
@@ -268,6 +270,22 @@ class Decoder:
                                               x.size, int(cw_stride), int(elem_stride),
                                               float(polarity), int(B), _p(packed, _u8p),
                                               _p(synd, _i32p)), self._ctx)
+        return dict(packed=packed, synd=synd)
+
+    def decode_windows(self, samples, windows, method=METHOD_SUMPRODUCT, max_iters=50,
+                       et_period=1, precision=PREC_F64, elem_stride=1, reuse_span=False):
+        """ldpc_decode_windows: windows (B,) int64 = (start << 1) | negate over
+        one host sample span.  Returns dict(packed (B,KB), synd (B,))."""
+        x = np.ascontiguousarray(samples, np.float32).reshape(-1)
+        w = np.ascontiguousarray(windows, np.int64)
+        B = w.size
+        packed = np.zeros((B, self.KB), np.uint8)
+        synd = np.zeros(B, np.int32)
+        _check(lib().ldpc_decode_windows(self._ctx, int(method), int(max_iters), int(et_period),
+                                         int(precision), _p(x, _f32p), x.size, int(elem_stride),
+                                         1 if reuse_span else 0,
+                                         w.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), B,
+                                         _p(packed, _u8p), _p(synd, _i32p)), self._ctx)
         return dict(packed=packed, synd=synd)
 
     def decode_device(self, d_in, B, d_packed, method=METHOD_SUMPRODUCT, max_iters=50,

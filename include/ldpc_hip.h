@@ -12,7 +12,8 @@
  *       lib/ldpc_decoder_cb_impl.cc:35-117 (H setup + reorderHMatrix :104-106);
  *       ldpc_create_csr takes H as a sparse row list, for codes whose dense
  *       M x N matrix the reference could not hold
- *   ldpc_decode, ldpc_decode_strided, ldpc_decode_strided_both, ldpc_decode_device
+ *   ldpc_decode, ldpc_decode_strided, ldpc_decode_strided_both, ldpc_decode_windows,
+ *   ldpc_decode_device
  *       decodeLogDomainSimple :309-412, decodeSumProductSoft :478-557,
  *       decodeBitFlipping :414-476, decodeHard :559-572 and the early-exit
  *       checkFrame(vhat, 0) they call, dispatched as general_work :155-164;
@@ -204,6 +205,22 @@ int ldpc_decode_strided_both(ldpc_ctx *ctx, int method, int max_iters,
                              int elem_stride, float polarity, int B,
                              uint8_t *out_packed, int32_t *syn_weight_opt);
 
+/* Any windows of one host sample span, each at its own polarity (the block's
+ * batched replay of general_work :133-234, where every decode is "the N
+ * samples at position p, times +-1").  Sample i of the span is
+ * in[i*elem_stride] (elem_stride 2: the real parts of gr_complex), i <
+ * ceil(n_in_floats / elem_stride).  windows[b] = (p << 1) | neg: window b is
+ * samples p .. p+N-1, negated when neg = 1 (tx = -Re, exact).  Outputs per
+ * window as for ldpc_decode_strided (packed B x KB, syn_weight_opt B).
+ * reuse_span = 1: the span is unchanged since the previous
+ * ldpc_decode_windows call on this context and has the same length, so it is
+ * not copied again.  Synchronous.  (Replaces the per-window decode calls of
+ * :155-164 and :178-187.) */
+int ldpc_decode_windows(ldpc_ctx *ctx, int method, int max_iters, int et_period,
+                        int precision, const float *in, int64_t n_in_floats,
+                        int elem_stride, int reuse_span, const int64_t *windows, int B,
+                        uint8_t *out_packed, int32_t *syn_weight_opt);
+
 /* Device-resident buffers (already in HBM); enqueues on `hip_stream`
  * (hipStream_t, NULL = the context's own stream) and returns without
  * synchronising.  One host thread may enqueue on several streams: small-code
@@ -226,9 +243,9 @@ int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu);
  * general_work): 12 persistent waves per CU, and a wave whose last iteration
  * was slow gets issue priority, so the frames that end a batch are not
  * starved.  LDPC_MODE_THROUGHPUT: for callers that keep several decodes in
- * flight on different streams: 10 waves per CU, no priority management (the
- * next batch fills the SIMDs a batch's last frames leave idle).  Overrides an
- * earlier ldpc_set_waves_per_cu. */
+ * flight on different streams (3 is best for 4096-frame batches): 6 waves per
+ * CU per launch, no priority management (the other batches fill the SIMDs a
+ * batch's last frames leave idle).  Overrides an earlier ldpc_set_waves_per_cu. */
 #define LDPC_MODE_LATENCY 0
 #define LDPC_MODE_THROUGHPUT 1
 int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode);

@@ -98,3 +98,34 @@ def test_encoder_block_roundtrip(Hr):
     blk = L.ldpc_decoder_cb(1, _backend=oracle_backend(1, Hr))
     out, _ = blk.general_work(10 ** 6, sym)
     assert (out == payload).all()
+
+
+def _hard_stream(Hr, seed, frames=32, db=1.0):
+    """Low-SNR frames (sync losses every few frames), a polarity flip, a
+    misaligned garbage stretch and frames again: exercises every branch of
+    the replayed state machine and the speculative search windows."""
+    rng = np.random.default_rng(seed)
+    M, N = Hr.shape
+    data = rng.integers(0, 2, size=(frames, N - M), dtype=np.uint8)
+    x = 2.0 * L.encode(Hr, data) - 1.0
+    y = x + np.sqrt(10 ** (-db / 10)) * rng.standard_normal(x.shape)
+    half = frames // 2
+    s = np.concatenate([rng.standard_normal(17), y[:half].ravel(), rng.standard_normal(N + 29),
+                        -y[half:].ravel()]).astype(np.float32)
+    return s.astype(np.complex64)
+
+
+@pytest.mark.parametrize("method,iters", [(0, 5), (1, 5), (1, 20), (2, 5), (3, 1)])
+@pytest.mark.parametrize("chunk,out_space", [(None, 1 << 20), (200, 12), (777, 1 << 20)])
+def test_block_low_snr_streams_match_restated_general_work(Hr, method, iters, chunk, out_space):
+    s = _hard_stream(Hr, 100 + method * 7 + iters)
+    exp = orc.run_stream(method, Hr, s, iterations=iters,
+                         chunks=None if chunk is None else [chunk] * (len(s) // chunk + 1),
+                         out_space=out_space)
+    blk = L.ldpc_decoder_cb(method, iterations=iters, _backend=oracle_backend(method, Hr, iters))
+    tb = fg.top_block(chunk=chunk, out_space=out_space)
+    src, dst = fg.vector_source_c(s), fg.vector_sink_b()
+    tb.connect(src, blk, dst)
+    tb.run()
+    assert len(exp) > 0
+    assert (dst.array() == exp).all()
