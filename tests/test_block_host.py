@@ -118,7 +118,7 @@ def _hard_stream(Hr, seed, frames=32, db=1.0):
 @pytest.mark.parametrize("method,iters", [(0, 5), (1, 5), (1, 20), (2, 5), (3, 1)])
 @pytest.mark.parametrize("chunk,out_space", [(None, 1 << 20), (200, 12), (777, 1 << 20)])
 def test_block_low_snr_streams_match_restated_general_work(Hr, method, iters, chunk, out_space):
-    s = _hard_stream(Hr, 100 + method * 7 + iters)
+    s = _hard_stream(Hr, 100 + method * 7 + iters, db=1.0 if method <= 1 else 3.0)
     exp = orc.run_stream(method, Hr, s, iterations=iters,
                          chunks=None if chunk is None else [chunk] * (len(s) // chunk + 1),
                          out_space=out_space)
