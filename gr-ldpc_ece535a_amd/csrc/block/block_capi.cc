@@ -134,6 +134,8 @@ int ldpc_decoder_cb_state(const ldpc_block *blk, uint32_t *errors_opt) {
   return blk->dec->state();
 }
 
+int64_t ldpc_decoder_cb_launches(const ldpc_block *blk) { return blk->dec->launches(); }
+
 int64_t ldpc_decoder_cb_frames_decoded(const ldpc_block *blk) {
   return blk->dec->frames_decoded();
 }

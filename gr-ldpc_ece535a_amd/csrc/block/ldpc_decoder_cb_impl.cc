@@ -9,9 +9,10 @@
  * position.  Here the loop is replayed exactly over a memo of decoded
  * windows; when it reaches a window not decoded yet, a dry run of the same
  * loop goes ahead on guesses (a frame in sync passes, an out-of-sync
- * position and a "-tx" retry fail) and collects every window it touches --
- * the rest of the in-sync frames, and at each sync loss the retry plus the
- * search positions up to the next frame boundary -- and all of them are
+ * position fails) and collects every window it touches -- the rest of the
+ * in-sync frames at both polarities (so every later "-tx" retry is known,
+ * not guessed), and at each sync loss the search positions up to the next
+ * frame boundary -- and all of them are
  * decoded in ONE GPU launch (ldpc_decode_windows: any positions, either
  * polarity, one staged copy of the input).  The exact replay then goes on;
  * a wrong guess only means another launch.  An out-of-sync search that
@@ -211,6 +212,7 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
                      d_wpacked.begin() + (size_t)(b + 1) * KB);
   }
   d_frames_decoded += B;
+  d_launches += 1;
 }
 
 ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact, int nin,
@@ -237,6 +239,12 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       d_want.push_back(((int64_t)pos << 1) | pol);
       pass = r.state != STATE_OUT_OF_SYNC;  // frames in sync mostly pass
       guessed_out = !pass;
+      // a frame in sync is also wanted at the other polarity: a sync loss
+      // retries it there (:178-187), and the retry passes often enough (a
+      // complemented codeword violates only the odd-weight rows) that the
+      // dry run must follow the real branch, not a guess
+      if (pass && d_spec_both && d_memo[pol ^ 1][pos] < 0)
+        d_want.push_back(((int64_t)pos << 1) | (pol ^ 1));
     }
     if (!pass) {
       if (n.state != STATE_OUT_OF_SYNC) {  // :169-176
@@ -318,6 +326,10 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
     d_want.clear();
     Replay dry = r;
     replay(dry, false, nin, noutput_items, nullptr, out_budget, (size_t)kMaxWindows);
+    if (d_debug)
+      std::cerr << "ldpc_decoder_cb: stall at " << r.consumed << " state " << r.state
+                << " errors " << r.errors << ": launch " << d_want.size()
+                << " windows, dry run to " << dry.consumed << " state " << dry.state << std::endl;
     decode_wanted(in, nin, first);
     first = false;
   }

@@ -16,6 +16,8 @@
 #include <ldpc_ece535a/ldpc_decoder_cb.h>
 #include <ldpc_hip.h>
 
+#include <stdlib.h>
+
 #include <string>
 #include <vector>
 
@@ -36,6 +38,10 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   ldpc_block_backend_fn d_backend;  // test seam; null = GPU
   void *d_backend_user;
   int64_t d_frames_decoded;
+  int64_t d_launches = 0;
+  bool d_debug = getenv("LDPC_BLOCK_DEBUG") != nullptr;  // one line per launch on stderr
+  // A/B knob: LDPC_BLOCK_SPEC_BOTH=0 speculates in-sync frames at one polarity
+  bool d_spec_both = !(getenv("LDPC_BLOCK_SPEC_BOTH") && getenv("LDPC_BLOCK_SPEC_BOTH")[0] == '0');
 
   // general_work's decode memo for the current call: the result of window
   // (position p, polarity) -- p in samples from the call's first input item,
@@ -89,6 +95,7 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   int state() const { return d_state; }
   unsigned int errors() const { return d_errors; }
   int64_t frames_decoded() const { return d_frames_decoded; }
+  int64_t launches() const { return d_launches; }
   unsigned int frame_samples() const { return d_N; }
   int frame_bytes() const { return d_out_bytes; }
   int frame_checks() const { return (int)d_M; }

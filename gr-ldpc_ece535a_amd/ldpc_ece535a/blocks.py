@@ -35,6 +35,7 @@ SIGNATURES = {
     "ldpc_decoder_cb_general_work": (_i, [_vp, _i, _i, _f32p, _u8p, _i32p]),
     "ldpc_decoder_cb_state": (_i, [_vp, _u32p]),
     "ldpc_decoder_cb_frames_decoded": (ctypes.c_int64, [_vp]),
+    "ldpc_decoder_cb_launches": (ctypes.c_int64, [_vp]),
     "ldpc_decoder_cb_destroy": (None, [_vp]),
     "ldpc_decoder_cb_make_with_backend": (_vp, [_i, _i, BACKEND_FN, _vp]),
     "ldpc_decoder_cb_make_h": (_vp, [_i, _i, _i, _i, _u8p, _i, _i, _i]),
@@ -155,6 +156,10 @@ class ldpc_decoder_cb:
     @property
     def frames_decoded(self):
         return lib().ldpc_decoder_cb_frames_decoded(self._h)
+
+    @property
+    def launches(self):
+        return lib().ldpc_decoder_cb_launches(self._h)
 
 
 class ldpc_encoder_bc:

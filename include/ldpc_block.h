@@ -64,6 +64,8 @@ int ldpc_decoder_cb_state(const ldpc_block *blk, uint32_t *errors_opt);
 
 /* Frames decoded by the GPU so far (speculative decodes included). */
 int64_t ldpc_decoder_cb_frames_decoded(const ldpc_block *blk);
+/* Decode launches (ldpc_decode_windows calls, or test-seam batches) so far. */
+int64_t ldpc_decoder_cb_launches(const ldpc_block *blk);
 
 void ldpc_decoder_cb_destroy(ldpc_block *blk);
 
