@@ -12,7 +12,7 @@ convention (sigma = sqrt(10^(-EbN0/10)), apps/ldpc_lapack.cpp:635-642).
 Data are made on the GPU before timing: Philox bits (ldpc_random_bits) ->
 systematic GF(2) encode (ldpc_encode_device) -> BPSK + AWGN
 (ldpc_bpsk_awgn); the first frames are cross-checked against the host
-encoder.  D distinct batches are made (D = --inflight, default 3): step k
+encoder.  D distinct batches are made (D = --inflight, default 4): step k
 decodes batch k mod D on stream k mod D, so D batches are in flight -- the
 next batch's frames fill the SIMDs the previous batch's last long frames
 leave idle (a streaming receiver's steady state).  Every step decodes its
@@ -67,7 +67,7 @@ def parse(argv=None):
     # the first ~100-200 launches of a fresh process run slower while the clock
     # ramps (profiles/round1/warmup_clock.txt); the default warmup covers them
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight (consecutive steps on alternating streams)")
     ap.add_argument("--strong", action="store_true",
                     help="N > 1: split one global batch over the ranks (default: weak scaling)")
@@ -517,8 +517,9 @@ def main():
     torch.cuda.synchronize(dev)
     sweeps(L, torch, dec, args, dev)
 
-    # several batches in flight: the throughput launch mode (6 waves per CU per
-    # launch, no issue-priority management; include/ldpc_hip.h ldpc_set_launch_mode)
+    # several batches in flight: the throughput launch mode (4 waves per CU per
+    # launch, four-waves-per-SIMD build, no issue-priority management;
+    # include/ldpc_hip.h ldpc_set_launch_mode)
     if not dvb:
         dec.set_launch_mode(1 if D > 1 else 0)
         if args.waves_per_cu:

@@ -1290,11 +1290,11 @@ int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode) {
   if (!ctx || (mode != LDPC_MODE_LATENCY && mode != LDPC_MODE_THROUGHPUT))
     return set_err(ctx, LDPC_EINVAL, "mode must be LDPC_MODE_LATENCY or LDPC_MODE_THROUGHPUT");
   // measured on the config-2 batch (profiles/round2/ab_launch_mode.txt,
-  // profiles/round2/layout/sweep_inflight_wpc.txt): one launch at a time: 12
-  // waves per CU, priority for starved waves; overlapping launches: 6 waves
-  // per CU each (3 launches in flight fill the CU's 12 wave slots with room
-  // for the next launch's first waves), no priority games
-  ctx->waves_per_cu = mode == LDPC_MODE_THROUGHPUT ? 6 : 0;
+  // profiles/round2/layout/): one launch at a time: 12 waves per CU, priority
+  // for starved waves; overlapping launches: 4 waves per CU each (4 launches
+  // in flight fill the CU's 16 wave slots of the throughput build), no
+  // priority games
+  ctx->waves_per_cu = mode == LDPC_MODE_THROUGHPUT ? 4 : 0;
   ctx->fair_cycles = mode == LDPC_MODE_THROUGHPUT ? 0 : 1800;
   return LDPC_OK;
 }

@@ -691,8 +691,13 @@ __device__ uint64_t g_timeline[4 * kTimelineFrames];
 // default, 1, gives the same register budget)
 #define LDPC_SMALL_MIN_BLOCKS (kWavesPerBlock >= 4 ? 1 : 12 / kWavesPerBlock)
 #endif
-template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax>
-__global__ void __launch_bounds__(kThreads, LDPC_SMALL_MIN_BLOCKS)
+// MINB = 4 (four waves per SIMD, <= 128 VGPRs): the throughput build of the
+// sum-product f64 kernel (several launches in flight share the CUs); one
+// launch at a time runs faster with the larger register budget
+// (profiles/round2/layout/ab_min_blocks.txt).
+template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax,
+          int MINB = LDPC_SMALL_MIN_BLOCKS>
+__global__ void __launch_bounds__(kThreads, MINB)
     decode_small_kernel(CodeView code, DecodeArgs a) {
   typedef typename Math<PREC>::Real Real;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -1053,16 +1058,17 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
 // ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
-template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax>
+template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax,
+          int MINB = LDPC_SMALL_MIN_BLOCKS>
 static int launch_one(const CodeView &code, const DecodeArgs &a, hipStream_t st) {
   typedef typename Math<PREC>::Real Real;
   const size_t lds = Layout<Real, METHOD, S, NW, DVN>::total;
   if (lds > 65536 &&
-      hipFuncSetAttribute((const void *)decode_small_kernel<PREC, METHOD, S, NW, DCN, DVN>,
+      hipFuncSetAttribute((const void *)decode_small_kernel<PREC, METHOD, S, NW, DCN, DVN, MINB>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -3;
   const dim3 grid((unsigned)((a.waves + kWavesPerBlock - 1) / kWavesPerBlock));
-  hipLaunchKernelGGL((decode_small_kernel<PREC, METHOD, S, NW, DCN, DVN>), grid, dim3(kThreads),
+  hipLaunchKernelGGL((decode_small_kernel<PREC, METHOD, S, NW, DCN, DVN, MINB>), grid, dim3(kThreads),
                      lds, st, code, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
@@ -1101,6 +1107,13 @@ static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots, hi
   // slot get loops sized to their degrees
   if constexpr (NW == 1 && METHOD <= 1) {
     if (code.dc_max <= 6 && code.dv_max <= 3) {
+      // throughput mode (no issue-priority management): the 4-waves-per-SIMD build
+      if constexpr (PREC == 0 && METHOD == 1)
+        if (a.fair_cycles == 0) switch (slots) {
+            case 3: return launch_one<PREC, METHOD, 3, NW, 5, 3, 4>(code, a, st);
+            case 4: return launch_one<PREC, METHOD, 4, NW, 5, 3, 4>(code, a, st);
+            default: break;
+          }
       switch (slots) {
         case 1: return launch_one<PREC, METHOD, 1, NW, 5, 3>(code, a, st);
         case 2: return launch_one<PREC, METHOD, 2, NW, 5, 3>(code, a, st);

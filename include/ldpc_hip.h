@@ -243,9 +243,10 @@ int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu);
  * general_work): 12 persistent waves per CU, and a wave whose last iteration
  * was slow gets issue priority, so the frames that end a batch are not
  * starved.  LDPC_MODE_THROUGHPUT: for callers that keep several decodes in
- * flight on different streams (3 is best for 4096-frame batches): 6 waves per
- * CU per launch, no priority management (the other batches fill the SIMDs a
- * batch's last frames leave idle).  Overrides an earlier ldpc_set_waves_per_cu. */
+ * flight on different streams (4 is best for 4096-frame batches): 4 waves per
+ * CU per launch, a build with four waves per SIMD, no priority management (the
+ * other batches fill the SIMDs a batch's last frames leave idle).  Overrides an
+ * earlier ldpc_set_waves_per_cu. */
 #define LDPC_MODE_LATENCY 0
 #define LDPC_MODE_THROUGHPUT 1
 int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode);

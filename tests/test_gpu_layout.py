@@ -82,3 +82,23 @@ def test_planned_layout_matches_oracle(golden, name, method):
 def test_default_layout_model(golden):
     m = L.Decoder().layout_model
     assert m["searched"] == 1 and m["cc"] == 0 and m["ec"] == 0, m
+
+
+@pytest.mark.parametrize("prec", [0, 1, 2])
+@pytest.mark.parametrize("method", [0, 1])
+def test_throughput_build_equals_latency_build(golden, method, prec):
+    """The throughput launch mode runs a different build of the kernel (four
+    waves per SIMD, no issue priority) on the reference's H: same outputs."""
+    from oracle import oracle as orc
+    dec = L.Decoder()
+    y = frames(dec.H, 2048, 2.0, 31)
+    dec.set_launch_mode(0)
+    a = dec.decode(y, method=method, max_iters=50, precision=prec, want_llr=True)
+    dec.set_launch_mode(1)
+    b = dec.decode(y, method=method, max_iters=50, precision=prec, want_llr=True)
+    for k in ("packed", "bits", "iters", "synd"):
+        assert (a[k] == b[k]).all(), k
+    assert np.array_equal(a["llr"], b["llr"], equal_nan=True)
+    if prec != 1:
+        ref = orc.decode_batch(method, dec.H, y, 50, nthreads=8)
+        assert (b["packed"] == ref["packed"]).all() and (b["iters"] == ref["iters"]).all()
