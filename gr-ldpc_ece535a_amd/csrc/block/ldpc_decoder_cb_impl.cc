@@ -24,9 +24,13 @@
  * reordered like the reference's constructor; CSR; or an alist file).
  *
  * Decoding is deterministic per window and the replay only ever uses real
- * decode results, so the block emits the same bytes, consumes the same
- * items, prints the same sync messages and leaves the same state as the
- * reference's frame-at-a-time loop.
+ * decode results, so given the window decodes the block emits the same
+ * bytes, consumes the same items, prints the same sync messages and leaves
+ * the same state as the reference's frame-at-a-time loop.  The window
+ * decodes themselves are the reference's arithmetic as DESIGN.md section 3
+ * states it: min-sum exact; sum-product in the default f64 mode within 3 ulp
+ * per tanh / 1 ulp per log of glibc, with zero decision mismatches measured
+ * (not guaranteed) over the parity sweeps.
  */
 #include "ldpc_decoder_cb_impl.h"
 
