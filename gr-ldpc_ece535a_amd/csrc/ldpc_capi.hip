@@ -26,7 +26,7 @@ using ldpc::EdgeRowRec;
 using ldpc::kNone;
 
 struct ldpc_ctx {
-  int M = 0, N = 0, E = 0, K = 0, KB = 0, dc_max = 0, dv_max = 0;
+  int M = 0, N = 0, E = 0, K = 0, KB = 0, dc_max = 0, dv_max = 0, dc_min = 0;
   int slots = 0, nw = 0, rs = 0;
   int device = 0;
   std::vector<uint8_t> H;  // the decoder's (reordered) H
@@ -196,6 +196,8 @@ int build_tables(ldpc_ctx *ctx, std::vector<EdgeRowRec> &erecs, std::vector<Edge
   ctx->dc_max = 0;
   ctx->dv_max = 0;
   for (auto &r : row_edges) ctx->dc_max = std::max(ctx->dc_max, (int)r.size());
+  ctx->dc_min = ctx->dc_max;
+  for (auto &r : row_edges) ctx->dc_min = std::min(ctx->dc_min, (int)r.size());
   for (auto &c : col_edges) ctx->dv_max = std::max(ctx->dv_max, (int)c.size());
   if (ctx->E == 0) return set_err(ctx, LDPC_EINVAL, "H has no ones");
   if (N > ldpc::kNMax || M > ldpc::kMMax || ctx->E > 64 * ldpc::kSlotsMax ||
@@ -413,6 +415,7 @@ ldpc::CodeView code_view(const ldpc_ctx *ctx) {
   v.rs = ctx->rs;
   v.dc_max = ctx->dc_max;
   v.dv_max = ctx->dv_max;
+  v.dc_min = ctx->dc_min;
   return v;
 }
 

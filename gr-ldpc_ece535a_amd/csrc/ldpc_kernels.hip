@@ -231,7 +231,10 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
     // a missing column entry was relocated to this lane's zero cell
     const uint32_t eb_dummy = lds_addr(eb + kDummy + (lane & 31));
     constexpr uint32_t kTbEb = (uint32_t)(L.eb - L.tb) * sizeof(Real);  // eb - tb in bytes
-    if (lane < 32) tb[kDummy + lane] = Real(1);  // product identity (missing row neighbours)
+    if (lane < 32) {
+      tb[kDummy + lane] = Real(1);  // product identity (missing row neighbours)
+      eb[kDummy + lane] = Real(0);  // padding edge cells' row "neighbours": T = 0
+    }
     uint32_t ra[S][DCN], ea[NW][DVN], ta[NW][DVN];
 #pragma unroll
     for (int s = 0; s < S; ++s)
@@ -291,8 +294,25 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       }
       if constexpr (FIN && PREC == 0 && LDPC_TANH_SPLIT > 0) {
         if (open) {
+#ifdef LDPC_NO_BATCH_DIV
 #pragma unroll
           for (int s = 0; s < S; ++s) eb[lane + 64 * s] = fm::log_ratio_tab_open(Ts[s], logtab);
+#else
+          // the S quotients (1+T)/(1-T) from one reciprocal: every 1 - T > 0
+          // here (|T| <= tanh(8) for real edges of rows of degree >= 2; the
+          // padding cells read zero "neighbours", T = 0); a code with a
+          // degree-1 row (T = 1, the reference's log(2/0) = inf) divides
+          // one quotient at a time
+          if (code.dc_min >= 2) {
+            Real Es[S];
+            fm::log_ratio_tab_open_n<S>(Ts, logtab, Es);
+#pragma unroll
+            for (int s = 0; s < S; ++s) eb[lane + 64 * s] = Es[s];
+          } else {
+#pragma unroll
+            for (int s = 0; s < S; ++s) eb[lane + 64 * s] = fm::log_ratio_tab_open(Ts[s], logtab);
+          }
+#endif
         } else {
 #pragma unroll
           for (int s = 0; s < S; ++s) eb[lane + 64 * s] = Math<PREC>::check_msg(Ts[s], logtab);
@@ -370,9 +390,18 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           for (int k = 0; k < DVN; ++k) wide |= !(__builtin_fabs(mv[q][k]) <= LDPC_TANH_SPLIT);
         if (__builtin_amdgcn_ballot_w64(wide) == 0) {
 #pragma unroll
-          for (int q = 0; q < NW; ++q)
+          for (int q = 0; q < NW; ++q) {
+#ifdef LDPC_NO_BATCH_DIV
 #pragma unroll
             for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], fm::tanh_half_small(mv[q][k]));
+#else
+            // the column's DVN quotients -t/(t+2) from one reciprocal
+            Real th[DVN];
+            fm::tanh_half_small_n<DVN>(mv[q], th);
+#pragma unroll
+            for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], th[k]);
+#endif
+          }
           open = FIN;
         } else {
 #pragma unroll
@@ -752,7 +781,10 @@ __global__ void __launch_bounds__(kThreads, MINB)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const uint32_t cid = (uint32_t)field(wt.rn[s], 7);
-      relocate(wt.rn[s], DCN, lds_addr(tb), R, kDummy + dpos_of(code, 2 * s + (lane >> 5)));
+      // padding cells (no edge) read zero cells, so their product T is 0, not 1
+      relocate(wt.rn[s], DCN, lds_addr(tb), R,
+               cid == kNone ? (uint32_t)(L.ebd - L.tb) + (lane & 31)
+                            : kDummy + dpos_of(code, 2 * s + (lane >> 5)));
       const uint32_t ca = lds_addr(rb) / R + (cid == kNone ? (uint32_t)lane : cid);
       wt.rn[s][3] = (wt.rn[s][3] & 0xffffu) | (ca << 16);
       relocate(wt.cn[s], DVN - 1, lds_addr(eb), R, kDummy + (lane & 31));

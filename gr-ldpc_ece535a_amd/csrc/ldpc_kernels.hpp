@@ -62,6 +62,7 @@ struct CodeView {
   uint64_t dpos[2];          // byte g: identity cell (tb[64 S + dpos]) of 32-lane group g
   int M, N, E, KB, rs;       // rs = ceil(M / 64)
   int dc_max, dv_max;        // largest check / variable degree
+  int dc_min;                // smallest check degree
 };
 
 struct DecodeArgs {

@@ -78,7 +78,8 @@ struct Model {
     for (int k = 0; k < dcn; ++k) {
       for (int l = 0; l < 32; ++l) {
         const int e = edge_at[32 * g + l];
-        a[l] = (e >= 0 && k < (int)nbr[e].size()) ? L.tb + slot[nbr[e][k]] : L.tbd + r;
+        a[l] = e < 0 ? L.ebd + l  // padding cell: a zero cell
+                     : k < (int)nbr[e].size() ? L.tb + slot[nbr[e][k]] : L.tbd + r;
       }
       c += group_cost(a, 32, 32);
     }

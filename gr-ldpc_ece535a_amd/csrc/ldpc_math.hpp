@@ -378,6 +378,36 @@ LDPC_HD double div_fast(double n, double d) {
   return fma_(fma_(-d, q, n), y, q);
 }
 
+// n quotients num[i] / den[i] from ONE reciprocal (Montgomery's batch
+// inversion): prefix products p_i = den[0]..den[i], y = 1/p_{n-1} (one
+// reciprocal + Newton step), then backwards 1/den[i] = y p_{i-1}, y *= den[i].
+// Each quotient gets div_fast's residual correction q + (num - den q) / den,
+// so it carries div_fast's accuracy (the few-ulp error of the batched
+// reciprocal is squared away); a v_rcp_f64 (16 issue cycles) and a Newton
+// step are traded for three multiplies per extra quotient.  For operands
+// whose product stays normal: den in [1, 2] (tanh_half_small_n) or
+// [2^-23, 2] (log_ratio_tab_open_n).
+template <int n>
+LDPC_HD void div_fast_n(const double (&num)[n], const double (&den)[n], double (&q)[n]) {
+  double p[n];
+  p[0] = den[0];
+  for (int i = 1; i < n; ++i) p[i] = p[i - 1] * den[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+  double y = __builtin_amdgcn_rcp(p[n - 1]);
+#else
+  double y = 1.0 / p[n - 1];
+#endif
+  y = fma_(fma_(-p[n - 1], y, 1.0), y, y);
+  for (int i = n - 1; i > 0; --i) {
+    const double inv = y * p[i - 1];
+    y = y * den[i];
+    const double qi = num[i] * inv;
+    q[i] = fma_(fma_(-den[i], qi, num[i]), inv, qi);
+  }
+  const double q0 = num[0] * y;
+  q[0] = fma_(fma_(-den[0], q0, num[0]), y, q0);
+}
+
 // expm1(z) for z in [-44, 44]: z = n ln2 + r, |r| <= ln2/2, expm1(r) =
 // r + r^2 p(r), p the Chebyshev-economised degree-9 fit of (e^r - 1 - r)/r^2
 // on [-0.3466, 0.3466] (tools/gen_expm1_poly.py; dropped mass 1.0e-16, within
@@ -475,6 +505,19 @@ LDPC_HD double tanh_half_fast(double m) {
 LDPC_HD double tanh_half_small(double m) {
   const double t = expm1_mid_f64(-__builtin_fabs(m));
   return __builtin_copysign(div_fast(-t, t + 2.0), m);
+}
+
+// tanh_half_small of n values with one batched division (div_fast_n).
+template <int n>
+LDPC_HD void tanh_half_small_n(const double (&m)[n], double (&out)[n]) {
+  double num[n], den[n];
+  for (int i = 0; i < n; ++i) {
+    const double t = expm1_mid_f64(-__builtin_fabs(m[i]));
+    num[i] = -t;
+    den[i] = t + 2.0;
+  }
+  div_fast_n<n>(num, den, out);
+  for (int i = 0; i < n; ++i) out[i] = __builtin_copysign(out[i], m[i]);
 }
 
 // tanh(m / 2) with fdlibm's two ranges (s_tanh.c) on x = |m| / 2:
@@ -580,10 +623,10 @@ LDPC_HD double log_ratio_tab(double T, const LogTabEntry *tab) {
   return __builtin_fabs(T) < 1.0 ? y : T * __builtin_inf();
 }
 
-LDPC_HD double log_ratio_tab_open(double T, const LogTabEntry *tab) {
+// log(q) of log_ratio_tab_open, q = (1+T)/(1-T) already formed.
+LDPC_HD double log_q_tab_open(double q, const LogTabEntry *tab) {
   const double ln2_hi = 6.93147180369123816490e-01;
   const double ln2_lo = 1.90821492927058770002e-10;
-  const double q = div_fast(1.0 + T, 1.0 - T);
   uint64_t ix;
   __builtin_memcpy(&ix, &q, 8);
   const uint32_t hx = (uint32_t)(ix >> 32);
@@ -607,6 +650,23 @@ LDPC_HD double log_ratio_tab_open(double T, const LogTabEntry *tab) {
   p = fma_(p, r, 1.0 / 3.0);
   p = fma_(p, r, -0.5);
   return fma_(r2, p, lo) + hi;
+}
+
+LDPC_HD double log_ratio_tab_open(double T, const LogTabEntry *tab) {
+  return log_q_tab_open(div_fast(1.0 + T, 1.0 - T), tab);
+}
+
+// log_ratio_tab_open of n products with one batched division (div_fast_n);
+// every |T| <= tanh(LDPC_TANH_SPLIT / 2), so each 1 - T >= 2^-23.
+template <int n>
+LDPC_HD void log_ratio_tab_open_n(const double (&T)[n], const LogTabEntry *tab, double (&out)[n]) {
+  double num[n], den[n], q[n];
+  for (int i = 0; i < n; ++i) {
+    num[i] = 1.0 + T[i];
+    den[i] = 1.0 - T[i];
+  }
+  div_fast_n<n>(num, den, q);
+  for (int i = 0; i < n; ++i) out[i] = log_q_tab_open(q[i], tab);
 }
 
 }  // namespace fm

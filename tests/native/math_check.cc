@@ -108,3 +108,32 @@ void check_logtab(const double *x, int64_t n, int64_t *out) {
   out[0] = mism; out[1] = maxu;
 }
 }
+extern "C" {
+// batched forms (div_fast_n) vs their one-at-a-time forms: fn 0 tanh_half_small_n<3>
+// vs tanh_half_small, fn 1 log_ratio_tab_open_n<3> vs log_ratio_tab_open, fn 2 / 3
+// the same against glibc.  x holds 3 operands per call.  out[0] mismatches,
+// out[1] max ulp
+void check_batch(int fn, const double *x, int64_t n, int64_t *out) {
+  int64_t mism = 0, maxu = 0;
+  for (int64_t i = 0; i + 3 <= n; i += 3) {
+    const double v[3] = {x[i], x[i + 1], x[i + 2]};
+    double a[3], b[3];
+    if (fn == 0 || fn == 2) {
+      ldpc::fm::tanh_half_small_n<3>(v, a);
+      for (int j = 0; j < 3; ++j)
+        b[j] = fn == 0 ? ldpc::fm::tanh_half_small(v[j]) : tanh(v[j] / 2.0);
+    } else {
+      ldpc::fm::log_ratio_tab_open_n<3>(v, kTab, a);
+      for (int j = 0; j < 3; ++j)
+        b[j] = fn == 1 ? ldpc::fm::log_ratio_tab_open(v[j], kTab)
+                       : log((1.0 + v[j]) / (1.0 - v[j]));
+    }
+    for (int j = 0; j < 3; ++j) {
+      const int64_t u = ulps(a[j], b[j]);
+      if (u) ++mism;
+      if (u > maxu) maxu = u;
+    }
+  }
+  out[0] = mism; out[1] = maxu;
+}
+}

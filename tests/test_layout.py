@@ -73,8 +73,10 @@ def model(Hr, cell, pos, cols):
                 a = []
                 for l in range(32):
                     e = edge_at[32 * g + l]
-                    a.append(Ls["tb"] + cell[nbr[e][k]] if e >= 0 and k < len(nbr[e])
-                             else Ls["tbd"] + r)
+                    if e < 0:  # padding cell: reads a zero cell (T = 0)
+                        a.append(Ls["ebd"] + l)
+                    else:
+                        a.append(Ls["tb"] + cell[nbr[e][k]] if k < len(nbr[e]) else Ls["tbd"] + r)
                 c += group_cost(a, 32)
             best = c if best is None else min(best, c)
         cost += best
