@@ -23,15 +23,16 @@
 // Frame pipeline: S slots (a few 64-frame chunks) are in flight; every pass
 // advances each running slot by one iteration; a slot whose frame stops
 // (early exit under the reference's rule, or the cap) writes that frame's
-// outputs and loads the next frame of the batch.  Per pass:
-//   ms_check   one wave = 4 rows x 64 slots: syndrome parities of the last
-//              decisions, L(q) = LQ - L(r_old), the row state of the new L(r)
-//   ms_decide  one block per chunk: stop / run / refill per slot
-//   ms_flush   packed bytes, iterations (+ bits / posteriors) of stopped frames
-//   ms_synd    syndrome weight of frames stopped at the cap (uncapped checkFrame)
-//   ms_var     one wave = 4 columns x 64 slots: L(r) from the row states,
-//              s = sum L(r) ascending rows, LQ = Lci + s, vhat = LQ < 0
-//   ms_refill  channel values of the frames the freed slots take
+// outputs and loads the next frame of the batch.  Four launches per pass:
+//   ms_check     one wave = 4 rows x 64 slots: syndrome parities of the last
+//                decisions, L(q) = LQ - L(r_old), the row state of the new L(r)
+//   ms_decide    one block per chunk: stop / run / refill per slot
+//   ms_post      packed bytes and iterations of the stopped frames, and the
+//                syndrome weight of those stopped at the cap
+//   (ms_flush_cols  bits / posteriors of the stopped frames, when asked for)
+//   ms_var_fill  one wave = 4 columns x 64 slots: running slots: L(r) from the
+//                row states, s = sum L(r) ascending rows, LQ = Lci + s, vhat =
+//                LQ < 0; refilled slots: Lci = LQ = -tx of their new frame
 // A slot refilled in pass p runs its first horizontal step in pass p+1.
 #include <hip/hip_runtime.h>
 
@@ -64,10 +65,8 @@ __device__ __forceinline__ int alpha_of(uint64_t neg, uint64_t zero, int lane) {
 
 // ---------------------------------------------------------------------------
 template <int PREC, int DC>
-__global__ void __launch_bounds__(256) ms_check(GraphView g, MsWork w) {
+__device__ __forceinline__ void check_rows(const GraphView &g, const MsWork &w, int k) {
   typedef typename Math<PREC>::Real Real;
-  const int k = blockIdx.y;
-  if (!w.live_w[k]) return;
   const int lane = threadIdx.x & 63;
   const int64_t chunks = w.chunks;
   const bool fresh = w.it[k * 64 + lane] == 0;  // first horizontal step: L(q) = Lci
@@ -138,13 +137,29 @@ __global__ void __launch_bounds__(256) ms_check(GraphView g, MsWork w) {
   if (lane == 0) w.odd[(int64_t)wg * chunks + k] = odd;
 }
 
+template <int PREC, int DC>
+__global__ void __launch_bounds__(256) ms_check(GraphView g, MsWork w) {
+  const int k = blockIdx.y;
+  if (w.live_w[k]) check_rows<PREC, DC>(g, w, k);
+}
+
+__device__ void decide_chunk(MsWork w, int k, int max_iters, int et_period, int B, int32_t *synd);
+
+// One block per chunk.  (Deciding in ms_check's last block instead needs
+// agent-scope fences in every block, which write back the XCD's L2: slower.)
+__global__ void __launch_bounds__(256) ms_decide(MsWork w, int max_iters, int et_period, int B,
+                                                 int32_t *synd) {
+  decide_chunk(w, blockIdx.x, max_iters, et_period, B, synd);
+}
+
 // One 256-thread block per chunk.  A running slot that has executed `it`
 // iterations stops at the cap, or -- min-sum's rule (:406-408) -- when
 // it < cap, it % et_period == 0 and its decision satisfies every check.
 // Freed (and empty) slots take the next frames of the batch in lane order.
-__global__ void __launch_bounds__(256) ms_decide(MsWork w, int max_iters, int et_period, int B) {
+// (256 threads)
+__device__ void decide_chunk(MsWork w, int k, int max_iters, int et_period, int B, int32_t *synd) {
   __shared__ uint64_t part[4];
-  const int k = blockIdx.x, lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63;
   const int64_t chunks = w.chunks;
   uint64_t odd = 0;
   if (w.live_w[k])
@@ -173,6 +188,7 @@ __global__ void __launch_bounds__(256) ms_decide(MsWork w, int max_iters, int et
   const bool fill = nf >= 0;
   const bool run = running && !stop;
   if (stop) w.used[slot] = it;
+  if (stop && synd) synd[f] = 0;  // ms_post adds the weight of frames stopped at the cap
   w.nxt[slot] = want ? nf : f;
   w.it[slot] = run ? it + 1 : 0;
   const uint64_t sw = __ballot(stop), rw = __ballot(run), fw = __ballot(fill);
@@ -188,14 +204,15 @@ __global__ void __launch_bounds__(256) ms_decide(MsWork w, int max_iters, int et
 }
 
 // Outputs of the frames that stopped in this pass: packed info bits (bits
-// M.., MSB first, :207-219) through an LDS transpose, iterations, syndrome 0
-// (ms_synd adds the weight of frames stopped at the cap).
-__global__ void __launch_bounds__(256) ms_flush_packed(GraphView g, MsWork w, DecodeArgs a) {
-  const int k = blockIdx.y;
+// M.., MSB first, :207-219) through an LDS transpose and iterations
+// (decide_chunk zeroed their syndrome weight; flush_synd adds it for the
+// frames stopped at the cap).
+__device__ void flush_packed(const GraphView &g, const MsWork &w, const DecodeArgs &a, int bx,
+                             int k) {
   const uint64_t sel = w.stop_w[k];
   if (!sel) return;
   __shared__ uint8_t tile[64][65];
-  const int q0 = blockIdx.x * 64, lane = threadIdx.x & 63, wv = wave_id();
+  const int q0 = bx * 64, lane = threadIdx.x & 63, wv = wave_id();
   const int64_t chunks = w.chunks;
   for (int qq = wv; qq < 64; qq += 4) {
     const int q = q0 + qq;
@@ -212,10 +229,9 @@ __global__ void __launch_bounds__(256) ms_flush_packed(GraphView g, MsWork w, De
     const int f = i >> 6, qq = i & 63, q = q0 + qq;
     if (lane_bit(sel, f) && q < g.KB) a.packed[(int64_t)w.frame[k * 64 + f] * g.KB + q] = tile[f][qq];
   }
-  if (blockIdx.x == 0 && threadIdx.x < 64 && lane_bit(sel, threadIdx.x)) {
+  if (bx == 0 && threadIdx.x < 64 && lane_bit(sel, threadIdx.x)) {
     const int slot = k * 64 + threadIdx.x, fr = w.frame[slot];
     if (a.iters) a.iters[fr] = w.used[slot];
-    if (a.synd) a.synd[fr] = 0;
   }
 }
 
@@ -245,14 +261,13 @@ __global__ void __launch_bounds__(256) ms_flush_cols(GraphView g, MsWork w, uint
 }
 
 // Uncapped syndrome weight of the frames that stopped at the cap with
-// unsatisfied checks (added to the zero ms_flush_packed wrote).
-__global__ void __launch_bounds__(256) ms_synd(GraphView g, MsWork w, int32_t *synd) {
-  const int k = blockIdx.y;
+// unsatisfied checks (added to the zero decide_chunk wrote).
+__device__ void flush_synd(const GraphView &g, const MsWork &w, int32_t *synd, int bx, int k) {
   const uint64_t sel = w.cap_w[k];
   if (!sel || !synd) return;
   const int lane = threadIdx.x & 63;
   const int64_t chunks = w.chunks;
-  const int j0 = (blockIdx.x * 4 + wave_id()) * kMsRows;
+  const int j0 = (bx * 4 + wave_id()) * kMsRows;
   int cnt = 0;
   for (int j = j0; j < min(j0 + kMsRows, g.M); ++j) {
     uint64_t par = 0;
@@ -263,14 +278,31 @@ __global__ void __launch_bounds__(256) ms_synd(GraphView g, MsWork w, int32_t *s
   if (cnt && lane_bit(sel, lane)) atomicAdd(&synd[w.frame[k * 64 + lane]], cnt);
 }
 
+// blocks [0, nb_flush): flush_packed; the rest: flush_synd
+__global__ void __launch_bounds__(256) ms_post(GraphView g, MsWork w, DecodeArgs a, int nb_flush) {
+  const int k = blockIdx.y;
+  if ((int)blockIdx.x < nb_flush)
+    flush_packed(g, w, a, blockIdx.x, k);
+  else
+    flush_synd(g, w, a.synd, blockIdx.x - nb_flush, k);
+}
+
 // Vertical step (:379-403) for the running slots: L(r_ji) of every edge of
 // the column from its row's state, s = sum_j L(r_ji) in ascending j,
 // LQ = Lci + s, vhat = LQ < 0.
 template <typename Real, int DV>
-__global__ void __launch_bounds__(256) ms_var(GraphView g, MsWork w) {
+__global__ void __launch_bounds__(256) ms_var_fill(GraphView g, MsWork w, DecodeArgs a) {
   const int k = blockIdx.y;
-  if (!w.run_w[k]) return;
+  const uint64_t run = w.run_w[k], fill = w.fill_w[k];
   const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {  // the slots' frames move on (after ms_post)
+    const int slot = k * 64 + threadIdx.x;
+    if (lane_bit(w.stop_w[k] | fill, threadIdx.x)) w.frame[slot] = w.nxt[slot];
+  }
+  if (!(run | fill)) return;
+  const bool filling = lane_bit(fill, lane) != 0;
+  // a refilled slot's new frame (the decide's choice)
+  const float *src = filling ? a.in + (int64_t)w.nxt[k * 64 + lane] * a.cw_stride : nullptr;
   const int64_t chunks = w.chunks;
   const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
   Real *LQ = (Real *)w.LQ;
@@ -278,8 +310,15 @@ __global__ void __launch_bounds__(256) ms_var(GraphView g, MsWork w) {
   for (int cc = 0; cc < kMsCols; ++cc) {
     const int c = c0 + cc;
     if (c >= g.N) break;
+    // Lci = -tx as float (exact: tx is a float), LQ = Lci (:318-321, :328-331)
+    const float xf = filling ? -(src[(int64_t)c * a.elem_stride] * a.polarity) : 0.0f;
+    if (filling) w.L[at(c, k, g.N, lane)] = xf;
+    if (!run) {  // only refills in this chunk
+      if (filling) LQ[at(c, k, g.N, lane)] = (Real)xf;
+      continue;
+    }
     const int k0 = g.cp[c], d = g.cp[c + 1] - k0;
-    const Real lci = (Real)w.L[at(c, k, g.N, lane)];
+    const Real lci = filling ? (Real)xf : (Real)w.L[at(c, k, g.N, lane)];
     Real r[DV];
 #pragma unroll
     for (int t = 0; t < DV; ++t) {
@@ -298,48 +337,12 @@ __global__ void __launch_bounds__(256) ms_var(GraphView g, MsWork w) {
 #pragma unroll
     for (int t = 0; t < DV; ++t)
       if (t < d) s = s + r[t];
-    const Real lq = lci + s;
+    // a refilled lane's row states are stale: its sum is dead, LQ = Lci
+    const Real lq = filling ? lci : lci + s;
     LQ[at(c, k, g.N, lane)] = lq;
     const uint64_t bw = __ballot(lq < Real(0));
     if (lane == 0) w.hard[(int64_t)c * chunks + k] = bw;
     if (w.post) w.post[at(c, k, g.N, lane)] = (float)lq;
-  }
-}
-
-// Channel values of the frames the freed slots take: Lci = -tx (:318-321)
-// as float (exact) and LQ = Lci, through an LDS transpose (the block reads
-// each new frame's 64 samples along the frame).  Block 0 of each chunk also
-// moves the slots' frame indices forward.
-template <typename Real>
-__global__ void __launch_bounds__(256) ms_refill(GraphView g, MsWork w, DecodeArgs a) {
-  const int k = blockIdx.y;
-  const uint64_t fill = w.fill_w[k];
-  const int lane = threadIdx.x & 63, wv = wave_id();
-  if (blockIdx.x == 0 && threadIdx.x < 64) {
-    const int slot = k * 64 + threadIdx.x;
-    if (lane_bit(w.stop_w[k] | fill, threadIdx.x)) w.frame[slot] = w.nxt[slot];
-  }
-  if (!fill) return;
-  __shared__ float tile[64][65];
-  const int c0 = blockIdx.x * 64;
-  for (int f = wv; f < 64; f += 4) {
-    float x = 0.0f;
-    const int c = c0 + lane;
-    if (lane_bit(fill, f) && c < g.N) {
-      const int64_t fr = w.nxt[k * 64 + f];
-      x = a.in[fr * a.cw_stride + (int64_t)c * a.elem_stride] * a.polarity;
-    }
-    tile[f][lane] = x;
-  }
-  __syncthreads();
-  if (!lane_bit(fill, lane)) return;
-  Real *LQ = (Real *)w.LQ;
-  for (int cc = wv; cc < 64; cc += 4) {
-    const int c = c0 + cc;
-    if (c >= g.N) break;
-    const float x = tile[lane][cc];
-    w.L[at(c, k, g.N, lane)] = -x;
-    LQ[at(c, k, g.N, lane)] = -(Real)x;
   }
 }
 
@@ -373,17 +376,16 @@ void ms_pass(const GraphView &g, const MsWork &w, const DecodeArgs &a, int metho
     ms_check<PREC, 16><<<rgrid, 256, 0, st>>>(g, w);
   else
     ms_check<PREC, 32><<<rgrid, 256, 0, st>>>(g, w);
-  ms_decide<<<w.chunks, 256, 0, st>>>(w, method_iters, a.et_period, a.B);
-  ms_flush_packed<<<dim3((g.KB + 63) / 64, w.chunks), 256, 0, st>>>(g, w, a);
+  ms_decide<<<w.chunks, 256, 0, st>>>(w, method_iters, a.et_period, a.B, a.synd);
   if (a.bits || (a.llr && w.post)) ms_flush_cols<<<tgrid, 256, 0, st>>>(g, w, a.bits, a.llr);
-  ms_synd<<<rgrid, 256, 0, st>>>(g, w, a.synd);
+  const int nb_flush = (g.KB + 63) / 64;
+  ms_post<<<dim3(nb_flush + w.check_waves / 4, w.chunks), 256, 0, st>>>(g, w, a, nb_flush);
   if (g.dv_max <= 4)
-    ms_var<Real, 4><<<cgrid, 256, 0, st>>>(g, w);
+    ms_var_fill<Real, 4><<<cgrid, 256, 0, st>>>(g, w, a);
   else if (g.dv_max <= 8)
-    ms_var<Real, 8><<<cgrid, 256, 0, st>>>(g, w);
+    ms_var_fill<Real, 8><<<cgrid, 256, 0, st>>>(g, w, a);
   else
-    ms_var<Real, 16><<<cgrid, 256, 0, st>>>(g, w);
-  ms_refill<Real><<<tgrid, 256, 0, st>>>(g, w, a);
+    ms_var_fill<Real, 16><<<cgrid, 256, 0, st>>>(g, w, a);
 }
 
 }  // namespace
