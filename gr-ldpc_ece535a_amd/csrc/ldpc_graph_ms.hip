@@ -46,8 +46,14 @@
 namespace ldpc {
 namespace {
 
-constexpr int kMsRows = 4;  // check rows per wave
-constexpr int kMsCols = 4;  // columns per wave
+#ifndef LDPC_MS_ROWS
+#define LDPC_MS_ROWS 8
+#endif
+#ifndef LDPC_MS_COLS
+#define LDPC_MS_COLS 4
+#endif
+constexpr int kMsRows = LDPC_MS_ROWS;  // check rows per wave
+constexpr int kMsCols = LDPC_MS_COLS;  // columns per wave
 
 __device__ __forceinline__ int wave_id() {
   return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
