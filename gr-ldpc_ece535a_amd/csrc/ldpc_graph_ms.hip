@@ -143,10 +143,117 @@ __device__ __forceinline__ void check_rows(const GraphView &g, const MsWork &w, 
   if (lane == 0) w.odd[(int64_t)wg * chunks + k] = odd;
 }
 
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// check_rows for a wave whose rows have at most 64 edges together (8 rows of
+// degree <= 8): the rows' edges are consecutive in CSR order, so lane l
+// loads edge e_first + l's column, alpha words and hard word with one vector
+// load each, and every per-edge value the row loop needs is a readlane --
+// instead of three dependent scalar loads per edge (alpha misses the scalar
+// cache: 16 B x E x chunks).  The new alpha words go back the same way, one
+// vector store per wave.  Same arithmetic, same order as check_rows.
+template <int PREC, int DC>
+__device__ __forceinline__ void check_rows_lanes(const GraphView &g, const MsWork &w, int k) {
+  typedef typename Math<PREC>::Real Real;
+  const int lane = threadIdx.x & 63;
+  const int64_t chunks = w.chunks;
+  const bool fresh = w.it[k * 64 + lane] == 0;  // first horizontal step: L(q) = Lci
+  const Real *LQ = (const Real *)w.LQ;
+  Real *m1 = (Real *)w.m1, *m2 = (Real *)w.m2;
+  const int wg = blockIdx.x * 4 + wave_id();
+  const int j0 = wg * kMsRows;
+  const int j1 = min(j0 + kMsRows, g.M);
+  if (j0 >= j1) {  // a wave past the last row still reports "no row unsatisfied"
+    if (lane == 0) w.odd[(int64_t)wg * chunks + k] = 0;
+    return;
+  }
+  const int eb = g.rp[j0], ne = g.rp[j1] - eb;  // <= 64: 8 rows of degree <= 8
+  const bool has = lane < ne;
+  const int my_c = has ? g.ci[eb + lane] : 0;
+  uint64_t my_neg = 0, my_zero = 0, my_h = 0;
+  if (has) {
+    const uint64_t *aw = w.alpha + ((int64_t)(eb + lane) * chunks + k) * 2;
+    my_neg = aw[0];
+    my_zero = aw[1];
+    my_h = w.hard[(int64_t)my_c * chunks + k];
+  }
+  uint64_t odd = 0;  // checkFrame (:236-253) of the last decisions, 64 slots per word
+  uint64_t new_neg = 0, new_zero = 0;  // this lane's edge's new alpha words
+  for (int j = j0; j < j1; ++j) {
+    const int e0 = g.rp[j] - eb, d = g.rp[j + 1] - g.rp[j];
+    uint64_t par = 0;
+    for (int t = 0; t < d; ++t) par ^= readlane64(my_h, e0 + t);
+    odd |= par;
+    const int64_t ro = at(j, k, g.M, lane);
+    const Real om1 = m1[ro], om2 = m2[ro];
+    const int omt = w.meta[ro];
+    const int oP = (omt >> 6) - 1, oi1 = (omt & 63) - 1;
+    Real q[DC];
+#pragma unroll
+    for (int t = 0; t < DC; ++t) {
+      if (t < d) {
+        const int c = __builtin_amdgcn_readlane(my_c, e0 + t);
+        const Real lq = LQ[at(c, k, g.N, lane)];
+        const int al = alpha_of(readlane64(my_neg, e0 + t), readlane64(my_zero, e0 + t), lane);
+        // the previous L(r) of the edge (:376), then L(q) = LQ - L(r) (:387-392)
+        const Real r = fresh ? Real(0) : (Real)(oP * al) * (t == oi1 ? om2 : om1);
+        q[t] = lq - r;
+      } else {
+        q[t] = Real(0);
+      }
+    }
+    // horizontal step (:340-376): sign product, smallest and second smallest
+    // |L(q)| with the reference's strict < (NaN never passes)
+    int P = 1, i1 = -1;
+    Real a1 = Math<PREC>::max_(), a2 = Math<PREC>::max_();
+#pragma unroll
+    for (int t = 0; t < DC; ++t)
+      if (t < d) {
+        P *= sgn(q[t]);
+        const Real a = Math<PREC>::abs_(q[t]);
+        if (a < a1) {
+          a2 = a1;
+          a1 = a;
+          i1 = t;
+        } else if (a < a2) {
+          a2 = a;
+        }
+      }
+    m1[ro] = a1;
+    m2[ro] = a2;
+    w.meta[ro] = (uint8_t)(((P + 1) << 6) | (i1 + 1));
+#pragma unroll
+    for (int t = 0; t < DC; ++t)
+      if (t < d) {
+        const uint64_t neg = __ballot(q[t] < Real(0));
+        const uint64_t zero = __ballot(!(q[t] > Real(0)) && !(q[t] < Real(0)));
+        new_neg = lane == e0 + t ? neg : new_neg;
+        new_zero = lane == e0 + t ? zero : new_zero;
+      }
+  }
+  if (has) {
+    uint64_t *aw = w.alpha + ((int64_t)(eb + lane) * chunks + k) * 2;
+    aw[0] = new_neg;
+    aw[1] = new_zero;
+  }
+  if (lane == 0) w.odd[(int64_t)wg * chunks + k] = odd;
+}
+
 template <int PREC, int DC>
 __global__ void __launch_bounds__(256) ms_check(GraphView g, MsWork w) {
   const int k = blockIdx.y;
-  if (w.live_w[k]) check_rows<PREC, DC>(g, w, k);
+  if (!w.live_w[k]) return;
+#ifndef LDPC_MS_SCALAR_META
+  if constexpr (DC * kMsRows <= 64) {
+    check_rows_lanes<PREC, DC>(g, w, k);
+    return;
+  }
+#endif
+  check_rows<PREC, DC>(g, w, k);
 }
 
 __device__ void decide_chunk(MsWork w, int k, int max_iters, int et_period, int B, int32_t *synd);
@@ -313,6 +420,29 @@ __global__ void __launch_bounds__(256) ms_var_fill(GraphView g, MsWork w, Decode
   const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
   Real *LQ = (Real *)w.LQ;
   const int c0 = (blockIdx.x * 4 + wave_id()) * kMsCols;
+  // the wave's columns' CSC edges are consecutive: lane l takes edge cp[c0] + l
+  // (its row, its place in the row, its alpha words) with one vector load
+  // each, when they fit the wave (as check_rows_lanes)
+  int kb = 0, my_j = 0, my_pos = 0;
+  uint64_t my_neg = 0, my_zero = 0;
+  bool lanes_meta = false;
+#ifndef LDPC_MS_SCALAR_META
+  if constexpr (DV * kMsCols <= 64) {
+    if (run && c0 < g.N) {
+      lanes_meta = true;
+      kb = g.cp[c0];
+      const int ne = g.cp[min(c0 + kMsCols, g.N)] - kb;
+      if (lane < ne) {
+        const int e = g.ce[kb + lane];
+        my_j = g.cr[kb + lane];
+        my_pos = e - g.rp[my_j];
+        const uint64_t *aw = w.alpha + ((int64_t)e * chunks + k) * 2;
+        my_neg = aw[0];
+        my_zero = aw[1];
+      }
+    }
+  }
+#endif
   for (int cc = 0; cc < kMsCols; ++cc) {
     const int c = c0 + cc;
     if (c >= g.N) break;
@@ -326,17 +456,34 @@ __global__ void __launch_bounds__(256) ms_var_fill(GraphView g, MsWork w, Decode
     const int k0 = g.cp[c], d = g.cp[c + 1] - k0;
     const Real lci = filling ? (Real)xf : (Real)w.L[at(c, k, g.N, lane)];
     Real r[DV];
+    if (lanes_meta) {
+      // this column's edges are lanes k0 - kb .. of the wave's edge lanes
+      const int l0 = k0 - kb;
 #pragma unroll
-    for (int t = 0; t < DV; ++t) {
-      r[t] = Real(0);
-      if (t < d) {
-        const int e = g.ce[k0 + t], j = g.cr[k0 + t];
-        const int pos = e - g.rp[j];  // the edge's place in its row
-        const int64_t ro = at(j, k, g.M, lane);
-        const int mt = w.meta[ro];
-        const uint64_t *aw = w.alpha + ((int64_t)e * chunks + k) * 2;
-        const int al = alpha_of(aw[0], aw[1], lane);
-        r[t] = (Real)(((mt >> 6) - 1) * al) * (pos == (mt & 63) - 1 ? m2[ro] : m1[ro]);
+      for (int t = 0; t < DV; ++t) {
+        r[t] = Real(0);
+        if (t < d) {
+          const int j = __builtin_amdgcn_readlane(my_j, l0 + t);
+          const int pos = __builtin_amdgcn_readlane(my_pos, l0 + t);
+          const int64_t ro = at(j, k, g.M, lane);
+          const int mt = w.meta[ro];
+          const int al = alpha_of(readlane64(my_neg, l0 + t), readlane64(my_zero, l0 + t), lane);
+          r[t] = (Real)(((mt >> 6) - 1) * al) * (pos == (mt & 63) - 1 ? m2[ro] : m1[ro]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < DV; ++t) {
+        r[t] = Real(0);
+        if (t < d) {
+          const int e = g.ce[k0 + t], j = g.cr[k0 + t];
+          const int pos = e - g.rp[j];  // the edge's place in its row
+          const int64_t ro = at(j, k, g.M, lane);
+          const int mt = w.meta[ro];
+          const uint64_t *aw = w.alpha + ((int64_t)e * chunks + k) * 2;
+          const int al = alpha_of(aw[0], aw[1], lane);
+          r[t] = (Real)(((mt >> 6) - 1) * al) * (pos == (mt & 63) - 1 ? m2[ro] : m1[ro]);
+        }
       }
     }
     Real s = Real(0);
