@@ -86,7 +86,7 @@ def main():
             for r in rows(os.path.join(a.dir, p, "**", "*counter_collection.csv")):
                 if a.per_decode in r["Kernel_Name"]:
                     tot[r["Counter_Name"]] += float(r["Counter_Value"])
-        decodes = sum(1 for r in kt if "g_reset" in r["Kernel_Name"])
+        decodes = sum(1 for r in kt if "g_reset" in r["Kernel_Name"] or "ms_init" in r["Kernel_Name"])
         span = collections.defaultdict(float)
         for r in kt:
             if a.per_decode in r["Kernel_Name"]:

@@ -6,7 +6,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 args="--code dvbs2 --steps 2 --warmup 0 --inflight 1 --no-cpu-baseline"
-for v in ms edge; do
+for v in ${DVB_VARIANTS:-ms edge}; do
   out=gpurun_out/prof/dvb_$v
   mkdir -p $out
   if [ $v = edge ]; then export LDPC_MS_PIPELINE=0; else unset LDPC_MS_PIPELINE; fi
