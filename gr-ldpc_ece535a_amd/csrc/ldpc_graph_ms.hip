@@ -63,6 +63,12 @@ __device__ __forceinline__ int64_t at(int64_t x, int k, int64_t n, int lane) {
   return ((int64_t)k * n + x) * 64 + lane;
 }
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+// lane l's 64-bit value, to every lane (l uniform)
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
 
 // alpha of an edge for this lane from its two words
 __device__ __forceinline__ int alpha_of(uint64_t neg, uint64_t zero, int lane) {
@@ -141,12 +147,6 @@ __device__ __forceinline__ void check_rows(const GraphView &g, const MsWork &w, 
       }
   }
   if (lane == 0) w.odd[(int64_t)wg * chunks + k] = odd;
-}
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
-  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-  return ((uint64_t)hi << 32) | lo;
 }
 
 // check_rows for a wave whose rows have at most 64 edges together (8 rows of
@@ -325,16 +325,18 @@ __device__ void flush_packed(const GraphView &g, const MsWork &w, const DecodeAr
   const uint64_t sel = w.stop_w[k];
   if (!sel) return;
   __shared__ uint8_t tile[64][65];
+  __shared__ uint64_t hw[512];  // hard words of the block's 512 columns (one vector load each)
   const int q0 = bx * 64, lane = threadIdx.x & 63, wv = wave_id();
   const int64_t chunks = w.chunks;
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int c = g.M + q0 * 8 + i;
+    hw[i] = c < g.N ? w.hard[(int64_t)c * chunks + k] : 0ull;
+  }
+  __syncthreads();
   for (int qq = wv; qq < 64; qq += 4) {
-    const int q = q0 + qq;
     unsigned o = 0;
-    if (q < g.KB)
-      for (int j = 0; j < 8; ++j) {
-        const int c = g.M + q * 8 + j;
-        if (c < g.N) o |= (unsigned)lane_bit(w.hard[(int64_t)c * chunks + k], lane) << (7 - j);
-      }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o |= (unsigned)lane_bit(hw[qq * 8 + j], lane) << (7 - j);
     tile[lane][qq] = (uint8_t)o;
   }
   __syncthreads();
@@ -381,12 +383,25 @@ __device__ void flush_synd(const GraphView &g, const MsWork &w, int32_t *synd, i
   const int lane = threadIdx.x & 63;
   const int64_t chunks = w.chunks;
   const int j0 = (bx * 4 + wave_id()) * kMsRows;
+  const int j1 = min(j0 + kMsRows, g.M);
+  if (j0 >= j1) return;
   int cnt = 0;
-  for (int j = j0; j < min(j0 + kMsRows, g.M); ++j) {
-    uint64_t par = 0;
-    const int e1 = g.rp[j + 1];
-    for (int e = g.rp[j]; e < e1; ++e) par ^= w.hard[(int64_t)g.ci[e] * chunks + k];
-    cnt += (int)lane_bit(par, lane);
+  const int eb = g.rp[j0], ne = g.rp[j1] - eb;
+  if (g.dc_max * kMsRows <= 64) {  // the rows' edges in the wave's lanes (check_rows_lanes)
+    const uint64_t my_h = lane < ne ? w.hard[(int64_t)g.ci[eb + lane] * chunks + k] : 0ull;
+    for (int j = j0; j < j1; ++j) {
+      uint64_t par = 0;
+      const int e0 = g.rp[j] - eb, d = g.rp[j + 1] - g.rp[j];
+      for (int t = 0; t < d; ++t) par ^= readlane64(my_h, e0 + t);
+      cnt += (int)lane_bit(par, lane);
+    }
+  } else {
+    for (int j = j0; j < j1; ++j) {
+      uint64_t par = 0;
+      const int e1 = g.rp[j + 1];
+      for (int e = g.rp[j]; e < e1; ++e) par ^= w.hard[(int64_t)g.ci[e] * chunks + k];
+      cnt += (int)lane_bit(par, lane);
+    }
   }
   if (cnt && lane_bit(sel, lane)) atomicAdd(&synd[w.frame[k * 64 + lane]], cnt);
 }
