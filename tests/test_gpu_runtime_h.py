@@ -171,3 +171,39 @@ def test_native_make_caller_alist(tmp_path):
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert (np.fromfile(fout, np.uint8) == orc.run_stream(1, Hr, s, iterations=20)).all()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("method", [0, 1])
+def test_decode_windows_any_positions(graph, method):
+    """ldpc_decode_windows (the block's launches): windows at arbitrary sample
+    positions of one interleaved gr_complex span, either polarity, equal the
+    strided single-window decodes of the same samples; a reused span gives
+    the same results."""
+    dec = L.Decoder(force_graph=graph)
+    N = dec.N
+    rng = np.random.default_rng(9)
+    x = _noisy_frames(dec.H, 24, 2.0, 77).ravel()
+    span = np.concatenate([rng.standard_normal(37).astype(np.float32), x])
+    cx = np.zeros(2 * span.size, np.float32)
+    cx[0::2] = span
+    cx[1::2] = rng.standard_normal(span.size)  # imaginary parts are ignored
+    pos = np.concatenate([37 + N * np.arange(20), rng.integers(0, span.size - N, 40)])
+    neg = rng.integers(0, 2, pos.size)
+    win = (pos.astype(np.int64) << 1) | neg
+    out = dec.decode_windows(cx, win, method=method, max_iters=20, elem_stride=2)
+    again = dec.decode_windows(cx, win[::-1].copy(), method=method, max_iters=20, elem_stride=2,
+                               reuse_span=True)
+    for b, (p, n) in enumerate(zip(pos, neg)):
+        ref = dec.decode(span[p:p + N], method=method, max_iters=20, polarity=-1.0 if n else 1.0)
+        assert (out["packed"][b] == ref["packed"][0]).all(), b
+        assert out["synd"][b] == ref["synd"][0], b
+    assert (again["packed"][::-1] == out["packed"]).all()
+    assert (again["synd"][::-1] == out["synd"]).all()
+
+
+def test_decode_windows_rejects_out_of_span():
+    dec = L.Decoder()
+    cx = np.zeros(2 * 100, np.float32)
+    with pytest.raises(L.LdpcError):
+        dec.decode_windows(cx, np.array([(40 << 1)], np.int64), elem_stride=2)  # 40 + 64 > 100

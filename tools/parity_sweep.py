@@ -14,6 +14,10 @@ from oracle import oracle as orc  # noqa: E402
 
 d = L.Decoder()
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+# launch mode: 0 latency build (the block), 1 throughput build (bench.py)
+mode = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+d.set_launch_mode(mode)
+print("launch mode %d, %d frames per cell" % (mode, B), flush=True)
 threads = max(1, min(16, len(os.sched_getaffinity(0))))
 for method in (1, 0):
     for amp in (1.0, 2.0, 4.0, 8.0, 16.0):
