@@ -380,7 +380,9 @@ def block_variant(L, torch, blocks, dev, args, d_y, B):
 
 def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
     """DVB-S2-like N=64800 code, min-sum, 1024 frames (config 4) on the
-    large-code path; optional parity of the first frames vs the sparse oracle."""
+    large-code path.  Returns (results, check): check() runs the parity of
+    the first `cpu_sample` frames vs the sparse oracle on the CPU -- called
+    after every GPU measurement, so the GPU does not idle between them."""
     from ldpc_ece535a import codes
     csr = codes.dvbs2_like(0)
     dec = L.Decoder(csr=csr, device=dev.index or 0)
@@ -388,6 +390,7 @@ def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
     d_y, d_bits = synth_device(L, torch, dec, B, args.ebn0, seed, dev)
     data = d_bits.cpu().numpy()
     out = {}
+    kept = {}
     for name, p in (("f64", 0), ("f32", 1)):
         r = time_decoder(dec, torch, [d_y], B, 0, args.iters, 1, p, steps, warmup)
         it = r["iters"]
@@ -400,23 +403,71 @@ def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
             "alg_GB/s": round(alg / (k * 1e-3) / 1e9, 1),
             "frames_decoded_to_sent_data": int((pk == np.packbits(data, axis=1)).all(axis=1).sum())}
         if p == 0 and cpu_sample:
-            from oracle import oracle as orc
-            y = d_y[:cpu_sample].cpu().numpy()
-            threads, _ = cpu_share()
-            t0 = time.perf_counter()
-            ref = orc.decode_batch_sparse(0, csr[2], csr[3], csr[0], csr[1], y, args.iters,
-                                          nthreads=threads, want_bits=False)
-            cpu_s = time.perf_counter() - t0
-            out["min-sum f64"]["parity_sample"] = {
-                "frames": cpu_sample,
-                "packed_mismatch_frames": int((ref["packed"] != pk[:cpu_sample]).any(axis=1).sum()),
-                "iters_mismatch_frames": int((ref["iters"] != it[:cpu_sample]).sum()),
-                "checker": "oracle sparse restatement (orc_decode_batch_sparse)",
-                "cpu_Mbit/s": round(cpu_sample * dec.K / cpu_s / 1e6, 4), "cpu_threads": threads}
+            kept = dict(y=d_y[:cpu_sample].cpu().numpy(), pk=pk[:cpu_sample],
+                        it=it[:cpu_sample], K=dec.K)
     out["code"] = ("DVB-S2-like N=64800 K=32400 E=226799 (synthetic rate-1/2 address table, "
                    "ldpc_ece535a.codes.dvbs2_like(0)), B=1024, %d-iteration cap" % args.iters)
     dec.close()
-    return out
+
+    def check():
+        if not kept:
+            return
+        from oracle import oracle as orc
+        threads, _ = cpu_share()
+        t0 = time.perf_counter()
+        ref = orc.decode_batch_sparse(0, csr[2], csr[3], csr[0], csr[1], kept["y"], args.iters,
+                                      nthreads=threads, want_bits=False)
+        cpu_s = time.perf_counter() - t0
+        out["min-sum f64"]["parity_sample"] = {
+            "frames": cpu_sample,
+            "packed_mismatch_frames": int((ref["packed"] != kept["pk"]).any(axis=1).sum()),
+            "iters_mismatch_frames": int((ref["iters"] != kept["it"]).sum()),
+            "checker": "oracle sparse restatement (orc_decode_batch_sparse)",
+            "cpu_Mbit/s": round(cpu_sample * kept["K"] / cpu_s / 1e6, 4), "cpu_threads": threads}
+    return out, check
+
+
+def gpu_variants(L, torch, dec, args, dev, inputs, B, D, prec, dvb, world, rank):
+    """Everything the line reports beside the headline that runs on the GPU:
+    config 4, the block, one batch in flight, the other methods / precisions.
+    Returns dict(variants, serial, outs, config4_check)."""
+    res = dict(variants={}, serial=None, outs={}, config4_check=None)
+    if args.no_variants:
+        return res
+    var = res["variants"]
+    if not dvb and not args.no_config4:
+        var["config4"], res["config4_check"] = config4_variant(
+            L, torch, dev, args, args.seed + 31,
+            cpu_sample=0 if (args.no_cpu_baseline or rank != 0) else 64)
+    if not dvb and not args.no_block and world == 1:
+        from ldpc_ece535a import blocks
+        with _quiet_stdout():
+            var["block general_work (host buffers)"] = block_variant(L, torch, blocks, dev,
+                                                                     args, inputs[0], B)
+    if D > 1:  # single batch in flight (latency per batch)
+        if not dvb:
+            dec.set_launch_mode(0)  # one launch at a time: the latency mode
+        st = max(10, args.steps // 2)
+        r1 = time_decoder(dec, torch, inputs[:1], B, args.method, args.iters, args.et_period,
+                          prec, st, 5, inflight=1)
+        if not dvb:
+            dec.set_launch_mode(1)
+        res["serial"] = {"Mbit/s": round(B * dec.K * st / r1["wall"] / 1e6, 2),
+                         "latency_ms_per_batch": round(r1["per_launch_ms"], 5)}
+    if not dvb:
+        for name, (m, p) in {"sum-product f32": (1, 1), "sum-product f64": (1, 0),
+                             "min-sum f64": (0, 0), "min-sum f32": (0, 1)}.items():
+            if (m, p) == (args.method, prec):
+                continue
+            st = max(5, args.steps // 2)
+            r2 = time_decoder(dec, torch, inputs, B, m, args.iters, args.et_period, p, st, 4,
+                              inflight=D)
+            it2 = r2["iters"]
+            var[name] = {"Mbit/s": round(B * dec.K * st / r2["wall"] / 1e6, 2),
+                         "ms_per_batch": round(r2["wall"] / st * 1e3, 5),
+                         "mean_iters": round(float(it2.mean()), 3)}
+            res["outs"][name] = (m, r2["outs"][0][0].cpu().numpy(), it2)
+    return res
 
 
 def relaunch_distributed(args):
@@ -524,6 +575,13 @@ def main():
         dec.set_launch_mode(1 if D > 1 else 0)
         if args.waves_per_cu:
             dec.set_waves_per_cu(args.waves_per_cu)
+    # The variants (other methods / precisions, latency, the block, config 4)
+    # are measured first, on every rank, so the headline's K steps run on a
+    # GPU that has been busy for a while (its clock ramps from ~2.0 to
+    # ~2.33 GHz over the first ~20 ms of work, profiles/round1/
+    # warmup_clock.txt) and every rank arrives in the same state.  Their CPU
+    # checks run after the headline.
+    pre = gpu_variants(L, torch, dec, args, dev, inputs, B, D, prec, dvb, world, rank)
     r = time_decoder(dec, torch, inputs, B, args.method, args.iters, args.et_period, prec,
                      args.steps, args.warmup, dist, inflight=D)
     wall = r["wall"]
@@ -619,42 +677,16 @@ def main():
     line["timing"] = {"device_span_ms_per_launch": round(r["per_launch_ms"], 5),
                       "wall_ms_per_step": round(per_launch_ms, 5),
                       "note": "span = HIP events: start on stream 0 (other streams wait on it) "
-                              "to the last stream's end, / K"}
+                              "to the last stream's end, / K",
+                      "order": "measured after the GPU variants below (same process), so the "
+                               "K steps see the GPU's steady clock; --no-variants times a "
+                               "cold GPU"}
 
-    # ---- single batch in flight (latency per batch), same process ----------
-    if D > 1 and not args.no_variants:
-        if not dvb:
-            dec.set_launch_mode(0)  # one launch at a time: the latency mode
-        r1 = time_decoder(dec, torch, inputs[:1], B, args.method, args.iters, args.et_period,
-                          prec, max(10, args.steps // 2), 5, inflight=1)
-        if not dvb:
-            dec.set_launch_mode(1)
-        line["serial_1_batch_in_flight"] = {
-            "Mbit/s": round(B * dec.K * max(10, args.steps // 2) / r1["wall"] / 1e6, 2),
-            "latency_ms_per_batch": round(r1["per_launch_ms"], 5)}
-
-    # ---- variants measured in the same process (not the headline) ----------
-    variant_outs = {}
-    if not args.no_variants and not dvb:
-        var = {}
-        for name, (m, p) in {"sum-product f32": (1, 1), "sum-product f64": (1, 0),
-                             "min-sum f64": (0, 0), "min-sum f32": (0, 1)}.items():
-            if (m, p) == (args.method, prec):
-                continue
-            st = max(5, args.steps // 2)
-            r2 = time_decoder(dec, torch, inputs, B, m, args.iters, args.et_period, p, st, 4,
-                              inflight=D)
-            it2 = r2["iters"]
-            var[name] = {"Mbit/s": round(B * dec.K * st / r2["wall"] / 1e6, 2),
-                         "ms_per_batch": round(r2["wall"] / st * 1e3, 5),
-                         "mean_iters": round(float(it2.mean()), 3)}
-            variant_outs[name] = (m, r2["outs"][0][0].cpu().numpy(), it2)
-        line["variants_1gpu"] = var
-        if not args.no_block and world == 1:
-            from ldpc_ece535a import blocks
-            with _quiet_stdout():
-                var["block general_work (host buffers)"] = block_variant(L, torch, blocks, dev,
-                                                                         args, inputs[0], B)
+    if pre["serial"]:
+        line["serial_1_batch_in_flight"] = pre["serial"]
+    if pre["variants"]:
+        line["variants_1gpu"] = pre["variants"]
+    variant_outs = pre["outs"]
 
     # ---- CPU baseline + parity (the oracle as checker) ----------------------
     if not args.no_cpu_baseline:
@@ -723,9 +755,8 @@ def main():
                                                et_period=args.et_period)
                 line["variants_1gpu"][name]["packed_mismatch_frames"] = int(
                     (refs[m]["packed"] != pk).any(axis=1).sum())
-    if not args.no_variants and not dvb and not args.no_config4:
-        line.setdefault("variants_1gpu", {})["config4"] = config4_variant(
-            L, torch, dev, args, args.seed + 31, cpu_sample=0 if args.no_cpu_baseline else 64)
+    if pre["config4_check"] is not None:
+        pre["config4_check"]()
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -995,7 +995,8 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
                        const float *d_in, int64_t cw_stride, int elem_stride, float polarity,
                        int B, int pm_half, uint8_t *d_out_packed, uint8_t *d_out_bits_opt,
                        int32_t *d_iters_used_opt, int32_t *d_syn_weight_opt,
-                       float *d_llr_out_opt, void *hip_stream) {
+                       float *d_llr_out_opt, void *hip_stream,
+                       const int64_t *d_win = nullptr) {
   int rc = check_decode_args(ctx, method, max_iters, et_period, precision, B, elem_stride,
                              cw_stride);
   if (rc != LDPC_OK) return rc;
@@ -1008,6 +1009,7 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   a.polarity = polarity;
   a.B = B;
   a.pm_half = 0;
+  a.win = d_win;
   a.max_iters = max_iters;
   a.et_period = et_period;
   a.packed = d_out_packed;
@@ -1019,6 +1021,7 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   void *st = hip_stream ? hip_stream : (void *)ctx->stream;
   if (ctx->graph) {
+    if (d_win) return set_err(ctx, LDPC_EUNSUPPORTED, "window lists: small-code kernels only");
     // one workspace per context: order this decode after the previous one
     // when it was enqueued on another stream
     if (!ctx->graph_done &&
@@ -1105,7 +1108,10 @@ int decode_host_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, in
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   rc = ensure_stage(ctx, b_in + b_pk + b_bits + b_it + b_sy + b_llr);
   if (rc != LDPC_OK) return rc;
-  rc = ensure_host_stage(ctx, (size_t)n_stage * 4);
+  // the pinned stage carries the input in and, after the kernel (stream
+  // order), every output back in one copy of the adjacent device outputs
+  const size_t b_out = b_pk + b_bits + b_it + b_sy + b_llr;
+  rc = ensure_host_stage(ctx, std::max((size_t)n_stage * 4, b_out));
   if (rc != LDPC_OK) return rc;
   char *base = (char *)ctx->d_stage;
   float *d_in = (float *)base;
@@ -1125,21 +1131,21 @@ int decode_host_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, in
   rc = decode_device_impl(ctx, method, max_iters, et_period, precision, d_in, cw, es, polarity,
                           BO, both ? B : 0, d_pk, d_bits, d_it, d_sy, d_llr, ctx->stream);
   if (rc != LDPC_OK) return rc;
-  struct {
-    void *dst;
-    const void *src;
-    size_t n;
-  } back[] = {{out_packed, d_pk, (size_t)BO * ctx->KB},
-              {out_bits_opt, d_bits, (size_t)BO * ctx->N},
-              {iters_used_opt, d_it, (size_t)BO * 4},
-              {syn_weight_opt, d_sy, (size_t)BO * 4},
-              {llr_out_opt, d_llr, (size_t)BO * ctx->N * 4}};
-  for (auto &c : back)
-    if (c.dst && (e = hipMemcpyAsync(c.dst, c.src, c.n, hipMemcpyDeviceToHost, ctx->stream)) !=
-                     hipSuccess)
-      return hip_err(ctx, e, "hipMemcpyAsync(out)");
+  if ((e = hipMemcpyAsync(h, d_pk, b_out, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipMemcpyAsync(out)");
   if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
     return hip_err(ctx, e, "hipStreamSynchronize");
+  const char *ho = (const char *)h;
+  struct {
+    void *dst;
+    size_t off, n;
+  } back[] = {{out_packed, 0, (size_t)BO * ctx->KB},
+              {out_bits_opt, b_pk, (size_t)BO * ctx->N},
+              {iters_used_opt, b_pk + b_bits, (size_t)BO * 4},
+              {syn_weight_opt, b_pk + b_bits + b_it, (size_t)BO * 4},
+              {llr_out_opt, b_pk + b_bits + b_it + b_sy, (size_t)BO * ctx->N * 4}};
+  for (auto &c : back)
+    if (c.dst) memcpy(c.dst, ho + c.off, c.n);
   return LDPC_OK;
 }
 
@@ -1179,13 +1185,17 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
       return hip_err(ctx, e, "hipMalloc(window staging)");
     ctx->wstage_bytes = want;
   }
-  if ((size_t)B * 8 > ctx->h_win_bytes) {
+  // pinned: the window list in, then the packed words and syndrome weights
+  // out in one copy (d_pk .. d_sy are adjacent in the staging area), so no
+  // transfer goes through a pageable bounce
+  const size_t h_need = b_win + b_pk + b_sy;
+  if (h_need > ctx->h_win_bytes) {
     if (ctx->h_win) {
       (void)hipStreamSynchronize(ctx->stream);
       (void)hipHostFree(ctx->h_win);
       ctx->h_win = nullptr;
     }
-    const size_t want = std::max((size_t)B * 8, (size_t)1 << 16);
+    const size_t want = std::max(h_need + h_need / 2, (size_t)1 << 16);
     if ((e = hipHostMalloc((void **)&ctx->h_win, want, hipHostMallocDefault)) != hipSuccess)
       return hip_err(ctx, e, "hipHostMalloc(windows)");
     ctx->h_win_bytes = want;
@@ -1217,19 +1227,27 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   if ((e = hipMemcpyAsync(d_win, ctx->h_win, (size_t)B * 8, hipMemcpyHostToDevice,
                           ctx->stream)) != hipSuccess)
     return hip_err(ctx, e, "hipMemcpyAsync(windows)");
-  if (ldpc::launch_gather_windows(d_span, d_win, B, N, d_fr, ctx->stream) != 0)
-    return set_err(ctx, LDPC_EDEVICE, "gather_windows launch failed");
-  rc = decode_device_impl(ctx, method, max_iters, et_period, precision, d_fr, N, 1, 1.0f, B, 0,
-                          d_pk, nullptr, nullptr, syn_weight_opt ? d_sy : nullptr, nullptr,
-                          ctx->stream);
+  if (ctx->graph) {  // the large-code kernels read frames at a fixed stride: gather first
+    if (ldpc::launch_gather_windows(d_span, d_win, B, N, d_fr, ctx->stream) != 0)
+      return set_err(ctx, LDPC_EDEVICE, "gather_windows launch failed");
+    rc = decode_device_impl(ctx, method, max_iters, et_period, precision, d_fr, N, 1, 1.0f, B,
+                            0, d_pk, nullptr, nullptr, syn_weight_opt ? d_sy : nullptr, nullptr,
+                            ctx->stream);
+  } else {  // the small-code kernels read each window in place (DecodeArgs::win)
+    rc = decode_device_impl(ctx, method, max_iters, et_period, precision, d_span, N, 1, 1.0f, B,
+                            0, d_pk, nullptr, nullptr, syn_weight_opt ? d_sy : nullptr, nullptr,
+                            ctx->stream, d_win);
+  }
   if (rc != LDPC_OK) return rc;
-  if ((e = hipMemcpyAsync(out_packed, d_pk, (size_t)B * ctx->KB, hipMemcpyDeviceToHost,
-                          ctx->stream)) != hipSuccess ||
-      (syn_weight_opt && (e = hipMemcpyAsync(syn_weight_opt, d_sy, (size_t)B * 4,
-                                             hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess))
+  uint8_t *h_out = (uint8_t *)ctx->h_win + b_win;
+  const size_t out_bytes = syn_weight_opt ? b_pk + (size_t)B * 4 : (size_t)B * ctx->KB;
+  if ((e = hipMemcpyAsync(h_out, d_pk, out_bytes, hipMemcpyDeviceToHost, ctx->stream)) !=
+      hipSuccess)
     return hip_err(ctx, e, "hipMemcpyAsync(out)");
   if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
     return hip_err(ctx, e, "hipStreamSynchronize");
+  memcpy(out_packed, h_out, (size_t)B * ctx->KB);
+  if (syn_weight_opt) memcpy(syn_weight_opt, h_out + b_pk, (size_t)B * 4);
   return LDPC_OK;
 }
 

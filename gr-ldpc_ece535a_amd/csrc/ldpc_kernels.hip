@@ -696,6 +696,11 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 // Frame b's first sample and polarity (DecodeArgs::pm_half: the second half
 // of a both-polarities launch re-reads the first half's windows negated).
 __device__ __forceinline__ const float *frame_src(const DecodeArgs &a, int64_t b, float &pol) {
+  if (a.win) {
+    const int64_t w = a.win[b];
+    pol = (w & 1) ? -a.polarity : a.polarity;
+    return a.in + (w >> 1) * a.elem_stride;
+  }
   pol = a.polarity;
   if (a.pm_half > 0 && b >= a.pm_half) {
     b -= a.pm_half;

@@ -75,6 +75,10 @@ struct DecodeArgs {
   // when pm_half > 0, frames b >= pm_half decode window b - pm_half with
   // -polarity (B = 2 * pm_half)
   int pm_half;
+  // windows of one span (ldpc_decode_windows): when set, frame b is the N
+  // samples from in + (win[b] >> 1) * elem_stride, negated when win[b] & 1
+  // (cw_stride and pm_half unused)
+  const int64_t *win;
   int max_iters;
   int et_period;
   uint8_t *packed;           // B x KB
