@@ -344,37 +344,50 @@ class _quiet_stdout:
         os.close(self.saved)
 
 
-def block_variant(L, torch, blocks, dev, args, d_y, B):
+def drive_stream(blk, cx, B):
+    """Feed a continuous stream to the block as a GR scheduler does: calls of
+    at most B frames of input, unconsumed input carried over.  The first call
+    (acquisition from a fresh block) is not timed.  Returns (seconds, output
+    bytes, calls, launches, windows decoded) of the timed calls."""
+    chunk = B * 64
+    pos = 0
+    o, used = blk.general_work(B * 4, cx[:chunk])
+    pos += used
+    l0, f0 = blk.launches, blk.frames_decoded
+    made = calls = 0
+    t0 = time.perf_counter()
+    while pos + 64 <= cx.size:
+        o, used = blk.general_work(B * 4, cx[pos:pos + chunk])
+        pos += used
+        made += o.size
+        calls += 1
+        if used == 0:
+            break
+    return (time.perf_counter() - t0, made, calls, blk.launches - l0, blk.frames_decoded - f0)
+
+
+def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4):
     """The drop-in block's own throughput: ldpc_decoder_cb (method 1, 50
-    iterations, f64) general_work over a stream of gr_complex frames in host
-    memory, as a GNU Radio scheduler drives it (lib/ldpc_decoder_cb_impl.cc:
-    133-234): one call per B-frame chunk, input consumed, packed bytes out."""
+    iterations, f64) general_work over a continuous stream of gr_complex
+    frames in host memory, as a GNU Radio scheduler drives it
+    (lib/ldpc_decoder_cb_impl.cc:133-234): calls of B frames of input,
+    packed bytes out."""
     out = {}
     for name, ebn0 in (("in-sync stream (4 dB)", 4.0), ("2 dB stream (sync losses)", 2.0)):
         dec = L.Decoder(device=dev.index or 0)
-        y, _ = synth_device(L, torch, dec, B, ebn0, args.seed + 77, dev, check_frames=0)
+        y, _ = synth_device(L, torch, dec, (reps + 1) * B, ebn0, args.seed + 77, dev,
+                            check_frames=0)
         dec.close()
         stream = np.zeros(2 * y.numel(), np.float32)
         stream[0::2] = y.cpu().numpy().ravel()
         cx = stream.view(np.complex64)
         blk = blocks.ldpc_decoder_cb(1, iterations=args.iters, precision=0, device=dev.index or 0)
-        reps = 4
-        pos, made, calls = 0, 0, 0
-        blk.general_work(B * 4, cx[:64 * 8])  # acquire sync on the first frames
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            pos = 0
-            while pos + 64 <= cx.size:
-                o, used = blk.general_work(B * 4, cx[pos:])
-                pos += used
-                made += o.size
-                calls += 1
-                if used == 0:
-                    break
-        dt = time.perf_counter() - t0
+        dt, made, calls, launches, windows = drive_stream(blk, cx, B)
         out[name] = {"Mbit/s": round(made * 8 / dt / 1e6, 2), "calls": calls,
                      "ms_per_call": round(dt / max(1, calls) * 1e3, 4),
-                     "frames_decoded": int(blk.frames_decoded), "bytes_out": int(made)}
+                     "launches_per_call": round(launches / max(1, calls), 2),
+                     "windows_per_output_frame": round(windows / max(1, made // 4), 2),
+                     "bytes_out": int(made)}
     return out
 
 

@@ -8,17 +8,27 @@
  * current position times +-1 -- and its state machine decides the next
  * position.  Here the loop is replayed exactly over a memo of decoded
  * windows; when it reaches a window not decoded yet, a dry run of the same
- * loop goes ahead on guesses (a frame in sync passes, an out-of-sync
- * position fails) and collects every window it touches -- the rest of the
- * in-sync frames at both polarities (so every later "-tx" retry is known,
- * not guessed), and at each sync loss the search positions up to the next
- * frame boundary -- and all of them are
- * decoded in ONE GPU launch (ldpc_decode_windows: any positions, either
- * polarity, one staged copy of the input).  The exact replay then goes on;
- * a wrong guess only means another launch.  An out-of-sync search that
- * finds nothing within its budget (128 positions) widens it x4 per launch.
- * A typical call costs two launches (the frames, then every sync loss's
- * search) instead of three per sync loss.
+ * loop goes ahead on guesses and collects every window it touches, and all of
+ * them are decoded in ONE GPU launch (ldpc_decode_windows: any positions,
+ * either polarity, one staged copy of the input).  The exact replay then goes
+ * on; a wrong guess only means another launch.
+ *
+ * The guesses follow the stream's grid: the phase (mod N) where two frames in
+ * a row last passed in sync.  A window on the grid passes, any other fails --
+ * a misaligned window passes the M/8 threshold ~1 % of the time.  So after a
+ * sync loss the dry run searches one sample at a time up to the next grid
+ * position and syncs there; after a false sync on a misaligned window it
+ * follows the 11 failing frames (:169-176), the retry and the search back to
+ * the grid, instead of decoding the rest of the input on the wrong grid.
+ * Frames on the grid are wanted at both polarities, so a sync loss's "-tx"
+ * retry (:178-187) is known.  An out-of-sync search that finds nothing within
+ * its budget (128 positions) widens x4 per launch.  Measured on one MI355X
+ * (profiles/round2/block/block_plans.txt): 4 dB stream 32 -> 75 Mbit/s, 2 dB
+ * 11 -> 19 Mbit/s against guessing that every frame in sync passes.
+ * A launch costs ~63 us (one 50-iteration frame's latency, ~40 us, plus the
+ * host round trip), as much as ~2000 extra windows, so optional branch
+ * speculation (LDPC_BLOCK_FORK=1: the windows needed if a search position
+ * syncs) is off: it saves launches only as fast as it adds windows.
  *
  * The H is the reference's default (make(method)), or a runtime H (dense,
  * reordered like the reference's constructor; CSR; or an alist file).
@@ -52,6 +62,8 @@ namespace ldpc_ece535a {
 namespace {
 const int kMaxWindows = 1 << 17;  // windows per launch (bounds staging memory)
 const int kSearchFirst = 128;     // out-of-sync positions a launch first guesses past; x4 after
+const int kForkFrames = 13;       // frames a guessed sync at a search position is followed for
+const int kForkSearch = 3;        // x N: the search after such a sync is lost, per fork
 const size_t kDenseMax = (size_t)1 << 22;  // alist codes up to M N entries go dense
 
 void print_method(int method) {
@@ -219,6 +231,37 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
   d_launches += 1;
 }
 
+void ldpc_decoder_cb_impl::want(int64_t pos, int pol, int nin) {
+  if (pos < 0 || pos + (int64_t)d_N > nin || d_want.size() >= (size_t)kMaxWindows) return;
+  int32_t &m = d_memo[pol][pos];
+  if (m == -1) {
+    m = -2;  // pending: wanted by this launch
+    d_want.push_back((pos << 1) | pol);
+  }
+}
+
+void ldpc_decoder_cb_impl::fork(int64_t q, int nin) {
+  // The search position q may pass (the check's threshold of M/8 unsatisfied
+  // rows lets misaligned windows through now and then).  The loop would then
+  // stay "in sync" on q's grid until 11 frames fail (:169-176), retry at the
+  // other polarity and search again from one sample on (:178-198): decode
+  // that branch's windows in the same launch, at both polarities.
+  const int64_t N = d_N;
+  for (int j = 1; j <= kForkFrames; ++j) {
+    want(q + N * j, 0, nin);
+    want(q + N * j, 1, nin);
+  }
+  int64_t end = q + 11 * N + kForkSearch * N;
+  if (d_anchor >= 0) {  // the search ends on the grid, at most 2 frames later than 11 failures
+    const int64_t s0 = q + 13 * N + 1;
+    end = s0 + (((d_anchor - (d_abs + s0)) % N) + N) % N;
+  }
+  for (int64_t p = q + 11 * N + 1; p <= end; ++p) {
+    want(p, 0, nin);
+    want(p, 1, nin);
+  }
+}
+
 ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact, int nin,
                                                            int noutput, unsigned char *out,
                                                            int max_out, size_t max_want) {
@@ -227,6 +270,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
   const int thr = (int)d_M / 8;                    // :142
   const int KB = (N - (int)d_M + 7) / 8;
   int out_run = 0;  // dry run: out-of-sync positions in a row with a guessed window
+  int searches = 0;  // dry run: runs of such positions so far
   while ((nin - r.consumed) >= N && (noutput - r.produced) >= mo) {  // :146-147
     const int pos = r.consumed;
     const int pol = r.state == STATE_IN_SYNC_INVERTED ? 1 : 0;  // tx = Re * -1 (:149-153)
@@ -235,20 +279,29 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
     // checkFrame(vhat, M/8) > M/8 (:166-168); it stops counting past the
     // threshold, so comparing the full weight gives the same decision
     int32_t use = d_memo[pol][pos];
+    // the dry run's guess: a window on the grid the stream was last seen in
+    // sync on passes, any other fails (a misaligned window passes ~1 % of the
+    // time); with no grid seen yet, frames in sync pass
+    const bool on_grid = d_anchor < 0 || (d_abs + pos) % N == d_anchor;
     bool pass;
     if (use >= 0) {
       pass = d_rsynd[use] <= thr;
     } else {
       if (exact) return STALLED;
-      d_want.push_back(((int64_t)pos << 1) | pol);
-      pass = r.state != STATE_OUT_OF_SYNC;  // frames in sync mostly pass
+      want(pos, pol, nin);
+      pass = d_anchor_guess ? (on_grid && (r.state != STATE_OUT_OF_SYNC || d_anchor >= 0))
+                            : r.state != STATE_OUT_OF_SYNC;
       guessed_out = !pass;
-      // a frame in sync is also wanted at the other polarity: a sync loss
-      // retries it there (:178-187), and the retry passes often enough (a
-      // complemented codeword violates only the odd-weight rows) that the
-      // dry run must follow the real branch, not a guess
-      if (pass && d_spec_both && d_memo[pol ^ 1][pos] < 0)
-        d_want.push_back(((int64_t)pos << 1) | (pol ^ 1));
+      // a frame in sync is also wanted at the other polarity when its result
+      // decides a sync loss's "-tx" retry (:178-187)
+      if (pass && d_spec_both) want(pos, pol ^ 1, nin);
+      if (!pass && r.state == STATE_OUT_OF_SYNC) d_forks.push_back(pos);
+    }
+    if (exact && pass && r.state != STATE_OUT_OF_SYNC) {
+      // two frames in a row pass in sync: their grid is the stream's (a
+      // misaligned pair passes ~1e-4 of the time)
+      if (d_last_pass == d_abs + pos - N) d_anchor = (int)((d_abs + pos) % N);
+      d_last_pass = d_abs + pos;
     }
     if (!pass) {
       if (n.state != STATE_OUT_OF_SYNC) {  // :169-176
@@ -266,8 +319,9 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
           pass2 = d_rsynd[i2] <= thr;
         } else {
           if (exact) return STALLED;
-          d_want.push_back(((int64_t)pos << 1) | (pol ^ 1));
+          want(pos, pol ^ 1, nin);
           guessed_out = true;  // a retry that fails mostly
+          if (use >= 0 && r.state == STATE_OUT_OF_SYNC) d_forks.push_back(pos);
         }
         if (pass2) {
           n.state = STATE_IN_SYNC_INVERTED;
@@ -293,6 +347,9 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       if (inverted) std::cout << "IN SYNC; PHASE INVERTED" << std::endl;
       if (synced) std::cout << "IN SYNC" << std::endl;
     }
+    if (!exact && d_searches > 0 && guessed_out && n.state == STATE_OUT_OF_SYNC &&
+        out_run == 0 && searches++ >= d_searches)
+      return STALLED;  // a later search: the first one likely syncs off the grid first
     r = n;
     if (!exact) {
       out_run = (guessed_out && r.state == STATE_OUT_OF_SYNC) ? out_run + 1 : 0;
@@ -328,17 +385,27 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       out_budget = kSearchFirst;
     last_out = now_out;
     d_want.clear();
+    d_forks.clear();
     Replay dry = r;
     replay(dry, false, nin, noutput_items, nullptr, out_budget, (size_t)kMaxWindows);
+    // then the branches where a search position passes, nearest first, while
+    // the launch has room: windows up to about one per wave slot of the GPU
+    // cost little more than the launch's latency (50 iterations of one frame)
+    if (d_fork)
+      for (int64_t q : d_forks) {
+        if (d_want.size() >= (size_t)d_budget) break;
+        fork(q, nin);
+      }
     if (d_debug)
       std::cerr << "ldpc_decoder_cb: stall at " << r.consumed << " state " << r.state
-                << " errors " << r.errors << ": launch " << d_want.size()
+                << " errors " << r.errors << " grid " << d_anchor << ": launch " << d_want.size()
                 << " windows, dry run to " << dry.consumed << " state " << dry.state << std::endl;
     decode_wanted(in, nin, first);
     first = false;
   }
   d_state = r.state;
   d_errors = r.errors;
+  d_abs += r.consumed;
   consume_each(r.consumed);
   return r.produced;
 }

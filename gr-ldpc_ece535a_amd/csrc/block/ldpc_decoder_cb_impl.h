@@ -42,11 +42,29 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   bool d_debug = getenv("LDPC_BLOCK_DEBUG") != nullptr;  // one line per launch on stderr
   // A/B knob: LDPC_BLOCK_SPEC_BOTH=0 speculates in-sync frames at one polarity
   bool d_spec_both = !(getenv("LDPC_BLOCK_SPEC_BOTH") && getenv("LDPC_BLOCK_SPEC_BOTH")[0] == '0');
+  // A/B knob: LDPC_BLOCK_FORK=1 also decodes the branches where a search position syncs
+  bool d_fork = getenv("LDPC_BLOCK_FORK") && getenv("LDPC_BLOCK_FORK")[0] == '1';
+  // A/B knob: LDPC_BLOCK_ANCHOR=0 guesses every in-sync window passes
+  bool d_anchor_guess = !(getenv("LDPC_BLOCK_ANCHOR") && getenv("LDPC_BLOCK_ANCHOR")[0] == '0');
+  // A/B knob: LDPC_BLOCK_SEARCHES=k stops a dry run at its (k+1)-th guessed
+  // search (0: no limit).  Each search passes a misaligned window somewhere
+  // with high probability (~1 % per window, ~126 windows) and the searches
+  // after such a false sync move, yet a limit of 1 or 2 costs more launches
+  // than the windows it saves (tools/block_policy_sim.py)
+  int d_searches = getenv("LDPC_BLOCK_SEARCHES") ? atoi(getenv("LDPC_BLOCK_SEARCHES")) : 0;
+  // windows a launch is filled up to with branch speculation (LDPC_BLOCK_BUDGET)
+  int d_budget = getenv("LDPC_BLOCK_BUDGET") ? atoi(getenv("LDPC_BLOCK_BUDGET")) : 3072;
+  // grid: absolute sample index of the call's first input item; the phase
+  // (mod N) of the last two consecutive frames that passed in sync (-1: none yet)
+  int64_t d_abs = 0;
+  int d_anchor = -1;
+  int64_t d_last_pass = -1;  // absolute position of the last window passing in sync
+  std::vector<int64_t> d_forks;  // dry run: search positions guessed to fail
 
   // general_work's decode memo for the current call: the result of window
   // (position p, polarity) -- p in samples from the call's first input item,
   // polarity 0 = +tx, 1 = -tx -- is entry d_memo[pol][p] of d_rsynd /
-  // d_rpacked (-1: not decoded).  Keys are (p << 1) | pol.
+  // d_rpacked (-1: not decoded, -2: wanted by the launch being planned).  Keys are (p << 1) | pol.
   std::vector<int32_t> d_memo[2];
   std::vector<int32_t> d_rsynd;
   std::vector<uint8_t> d_rpacked;
@@ -69,6 +87,10 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   // out-of-sync positions with missing windows, or max_want keys.
   Outcome replay(Replay &r, bool exact, int nin, int noutput, unsigned char *out, int max_out,
                  size_t max_want);
+  // Dry run: adds window (pos, pol) to d_want unless decoded or wanted (memo -2)
+  void want(int64_t pos, int pol, int nin);
+  // Dry run: the windows the loop needs if search position q syncs
+  void fork(int64_t q, int nin);
   // Decodes the windows d_want of the call's input into the memo (one
   // launch on the GPU; the test seam decodes runs of equally spaced windows).
   void decode_wanted(const float *in, int nin, bool first);

@@ -1196,7 +1196,10 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
       ctx->h_win = nullptr;
     }
     const size_t want = std::max(h_need + h_need / 2, (size_t)1 << 16);
-    if ((e = hipHostMalloc((void **)&ctx->h_win, want, hipHostMallocDefault)) != hipSuccess)
+    // mapped and coherent: the small-code kernels read the window list and
+    // write their outputs here directly (no copy either way; see below)
+    if ((e = hipHostMalloc((void **)&ctx->h_win, want,
+                           hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
       return hip_err(ctx, e, "hipHostMalloc(windows)");
     ctx->h_win_bytes = want;
   }
@@ -1224,9 +1227,24 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   }
   // the previous call's copy out of h_win has completed (it synchronised)
   memcpy(ctx->h_win, win, (size_t)B * 8);
-  if ((e = hipMemcpyAsync(d_win, ctx->h_win, (size_t)B * 8, hipMemcpyHostToDevice,
-                          ctx->stream)) != hipSuccess)
+  uint8_t *h_out = (uint8_t *)ctx->h_win + b_win;
+  // Small codes: the kernel reads the (pinned, mapped) window list and writes
+  // its packed bytes and syndrome weights into pinned memory itself -- a few
+  // bytes per window over the bus, and no DMA round trip on a launch whose
+  // latency is that of one frame (LDPC_WIN_COPY=1: the copies instead)
+  static const bool copy_mode = getenv("LDPC_WIN_COPY") && getenv("LDPC_WIN_COPY")[0] == '1';
+  const bool direct = !ctx->graph && !copy_mode;
+  if (direct) {
+    void *dv = nullptr;
+    if ((e = hipHostGetDevicePointer(&dv, ctx->h_win, 0)) != hipSuccess)
+      return hip_err(ctx, e, "hipHostGetDevicePointer(windows)");
+    d_win = (int64_t *)dv;
+    d_pk = (uint8_t *)dv + b_win;
+    d_sy = (int32_t *)((uint8_t *)dv + b_win + b_pk);
+  } else if ((e = hipMemcpyAsync(d_win, ctx->h_win, (size_t)B * 8, hipMemcpyHostToDevice,
+                                 ctx->stream)) != hipSuccess) {
     return hip_err(ctx, e, "hipMemcpyAsync(windows)");
+  }
   if (ctx->graph) {  // the large-code kernels read frames at a fixed stride: gather first
     if (ldpc::launch_gather_windows(d_span, d_win, B, N, d_fr, ctx->stream) != 0)
       return set_err(ctx, LDPC_EDEVICE, "gather_windows launch failed");
@@ -1239,13 +1257,21 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
                             ctx->stream, d_win);
   }
   if (rc != LDPC_OK) return rc;
-  uint8_t *h_out = (uint8_t *)ctx->h_win + b_win;
   const size_t out_bytes = syn_weight_opt ? b_pk + (size_t)B * 4 : (size_t)B * ctx->KB;
-  if ((e = hipMemcpyAsync(h_out, d_pk, out_bytes, hipMemcpyDeviceToHost, ctx->stream)) !=
-      hipSuccess)
+  if (!direct && (e = hipMemcpyAsync(h_out, d_pk, out_bytes, hipMemcpyDeviceToHost,
+                                     ctx->stream)) != hipSuccess)
     return hip_err(ctx, e, "hipMemcpyAsync(out)");
-  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
-    return hip_err(ctx, e, "hipStreamSynchronize");
+  // the block waits on one frame's latency per launch: poll rather than
+  // sleep on the completion (LDPC_WIN_SPIN=0: hipStreamSynchronize)
+  static const bool no_spin = getenv("LDPC_WIN_SPIN") && getenv("LDPC_WIN_SPIN")[0] == '0';
+  if (no_spin) {
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+      return hip_err(ctx, e, "hipStreamSynchronize");
+  } else {
+    while ((e = hipStreamQuery(ctx->stream)) == hipErrorNotReady) {
+    }
+    if (e != hipSuccess) return hip_err(ctx, e, "hipStreamQuery");
+  }
   memcpy(out_packed, h_out, (size_t)B * ctx->KB);
   if (syn_weight_opt) memcpy(syn_weight_opt, h_out + b_pk, (size_t)B * 4);
   return LDPC_OK;

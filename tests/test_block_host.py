@@ -129,3 +129,27 @@ def test_block_low_snr_streams_match_restated_general_work(Hr, method, iters, ch
     tb.run()
     assert len(exp) > 0
     assert (dst.array() == exp).all()
+
+
+@pytest.mark.parametrize("ebn0", [1.0, 3.0])
+def test_grid_guesses_exact_and_fewer_windows(Hr, ebn0, monkeypatch):
+    """The dry run's grid guesses (ldpc_decoder_cb_impl.cc header) change
+    only which windows are decoded, never the stream: both plans give the
+    restated general_work's output, the grid plan with fewer windows."""
+    import bench
+    y, _ = bench.synth(Hr, 192, ebn0, 31)
+    x = np.zeros(2 * y.size, np.float32)
+    x[0::2] = y.ravel()
+    s = x.view(np.complex64)
+    exp = orc.run_stream(1, Hr, s, iterations=5, chunks=[64 * 48] * 4)
+    decoded = {}
+    for plan in ("0", "1"):
+        monkeypatch.setenv("LDPC_BLOCK_ANCHOR", plan)
+        blk = L.ldpc_decoder_cb(1, _backend=oracle_backend(1, Hr))
+        tb = fg.top_block(chunk=64 * 48, out_space=4 * 48)
+        src, dst = fg.vector_source_c(s), fg.vector_sink_b()
+        tb.connect(src, blk, dst)
+        tb.run()
+        assert (dst.array() == exp).all()
+        decoded[plan] = blk.frames_decoded
+    assert decoded["1"] < decoded["0"]
