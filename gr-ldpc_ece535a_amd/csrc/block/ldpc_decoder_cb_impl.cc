@@ -193,8 +193,12 @@ void ldpc_decoder_cb_impl::forecast(int noutput_items, gr_vector_int &ninput_ite
 void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
   const int KB = (int)(d_N - d_M + 7) / 8;
   const int B = (int)d_want.size();
-  d_wsynd.assign((size_t)B, 0);
-  d_wpacked.assign((size_t)B * KB, 0);
+  // results land straight at the end of the memo's result arrays
+  const size_t base = d_rsynd.size();
+  d_rsynd.resize(base + B);
+  d_rpacked.resize((base + B) * KB);
+  int32_t *synd = d_rsynd.data() + base;
+  uint8_t *packed = d_rpacked.data() + base * KB;
   if (d_backend) {
     // the test seam decodes equally spaced windows of one polarity per call
     for (int i = 0; i < B;) {
@@ -209,24 +213,19 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
       const int n = j - i;
       const int rc = d_backend(d_backend_user, in + 2 * p0, 2 * ((int64_t)nin - p0),
                                2 * std::max<int64_t>(step, 1), 2, pol ? -1.0f : 1.0f, n,
-                               &d_wpacked[(size_t)i * KB], &d_wsynd[i]);
+                               packed + (size_t)i * KB, synd + i);
       if (rc < 0) throw std::runtime_error("ldpc_decoder_cb: decode failed: backend error");
       i = j;
     }
   } else {
     const int rc = ldpc_decode_windows(d_ctx, d_method, (int)d_iterations, 1, d_precision, in,
                                        2 * (int64_t)nin, 2, first ? 0 : 1, d_want.data(), B,
-                                       d_wpacked.data(), d_wsynd.data());
+                                       packed, synd);
     if (rc < 0)
       throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
                                ldpc_last_error(d_ctx));
   }
-  for (int b = 0; b < B; ++b) {
-    d_memo[d_want[b] & 1][d_want[b] >> 1] = (int32_t)d_rsynd.size();
-    d_rsynd.push_back(d_wsynd[b]);
-    d_rpacked.insert(d_rpacked.end(), d_wpacked.begin() + (size_t)b * KB,
-                     d_wpacked.begin() + (size_t)(b + 1) * KB);
-  }
+  for (int b = 0; b < B; ++b) d_memo[d_want[b] & 1][d_want[b] >> 1] = (int32_t)(base + b);
   d_frames_decoded += B;
   d_launches += 1;
 }

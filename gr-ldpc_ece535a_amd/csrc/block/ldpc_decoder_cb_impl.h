@@ -69,8 +69,6 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   std::vector<int32_t> d_rsynd;
   std::vector<uint8_t> d_rpacked;
   std::vector<int64_t> d_want;   // keys of the next launch
-  std::vector<int32_t> d_wsynd;  // its outputs
-  std::vector<uint8_t> d_wpacked;
 
   // The reference loop's progress (:140-234), for exact replay and for the
   // speculative dry run that picks the next launch's windows.
