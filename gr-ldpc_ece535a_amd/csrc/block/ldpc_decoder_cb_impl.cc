@@ -281,13 +281,13 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
     // the dry run's guess: a window on the grid the stream was last seen in
     // sync on passes, any other fails (a misaligned window passes ~1 % of the
     // time); with no grid seen yet, frames in sync pass
-    const bool on_grid = d_anchor < 0 || (d_abs + pos) % N == d_anchor;
     bool pass;
     if (use >= 0) {
       pass = d_rsynd[use] <= thr;
     } else {
       if (exact) return STALLED;
       want(pos, pol, nin);
+      const bool on_grid = d_anchor < 0 || (d_abs + pos) % N == d_anchor;
       pass = d_anchor_guess ? (on_grid && (r.state != STATE_OUT_OF_SYNC || d_anchor >= 0))
                             : r.state != STATE_OUT_OF_SYNC;
       guessed_out = !pass;
