@@ -226,6 +226,7 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
                                ldpc_last_error(d_ctx));
   }
   for (int b = 0; b < B; ++b) d_memo[d_want[b] & 1][d_want[b] >> 1] = (int32_t)(base + b);
+  d_touched.insert(d_touched.end(), d_want.begin(), d_want.end());
   d_frames_decoded += B;
   d_launches += 1;
 }
@@ -261,6 +262,28 @@ void ldpc_decoder_cb_impl::fork(int64_t q, int nin) {
   }
 }
 
+int ldpc_decoder_cb_impl::pass_run(int pol, int pos, int nin) {
+  // frames pos, pos + N, ... that are decoded at `pol` and pass (:166-168);
+  // d_skip jumps over runs found before (memo entries are not removed within
+  // a call, so a run stays a run), and the path is compressed to its end
+  const int N = (int)d_N, thr = (int)d_M / 8;
+  int32_t *skip = d_skip[pol].data();
+  const int32_t *memo = d_memo[pol].data();
+  int p = pos;
+  while (p + N <= nin) {
+    const int32_t u = memo[p];
+    if (u < 0 || d_rsynd[u] > thr) break;
+    p = skip[p] > p ? skip[p] : p + N;
+  }
+  for (int q = pos; q < p;) {
+    const int nx = skip[q] > q ? skip[q] : q + N;
+    if (skip[q] == 0) d_skip_touched.push_back(((int64_t)q << 1) | pol);
+    skip[q] = p;
+    q = nx;
+  }
+  return (p - pos) / N;
+}
+
 ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact, int nin,
                                                            int noutput, unsigned char *out,
                                                            int max_out, size_t max_want) {
@@ -273,6 +296,25 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
   while ((nin - r.consumed) >= N && (noutput - r.produced) >= mo) {  // :146-147
     const int pos = r.consumed;
     const int pol = r.state == STATE_IN_SYNC_INVERTED ? 1 : 0;  // tx = Re * -1 (:149-153)
+    if (r.state != STATE_OUT_OF_SYNC) {
+      // frames in sync that are decoded and pass change nothing but the
+      // position and the output (:207-225): take the whole run at once
+      const int k = std::min(pass_run(pol, pos, nin), (noutput - r.produced) / mo);
+      if (k > 0) {
+        if (exact) {
+          for (int i = 0; i < k; ++i)
+            std::memcpy(out + r.produced + (size_t)i * mo,
+                        &d_rpacked[(size_t)d_memo[pol][pos + i * N] * KB], (size_t)mo);
+          // two frames in a row pass in sync: their grid is the stream's
+          if (k > 1 || d_last_pass == d_abs + pos - N) d_anchor = (int)((d_abs + pos) % N);
+          d_last_pass = d_abs + pos + (int64_t)(k - 1) * N;
+        }
+        r.consumed += k * N;
+        r.produced += k * mo;
+        out_run = 0;
+        continue;
+      }
+    }
     Replay n = r;
     bool guessed_out = false, lost = false, inverted = false, synced = false;
     // checkFrame(vhat, M/8) > M/8 (:166-168); it stops counting past the
@@ -366,8 +408,17 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   const int N = (int)d_N;
   const int nin = ninput_items[0];
   const size_t npos = (size_t)std::max(nin - N + 1, 0);
-  d_memo[0].assign(npos, -1);
-  d_memo[1].assign(npos, -1);
+  // the memo and the jump table keep their size between calls: only the
+  // entries the last call set go back to "not decoded" (a full reset was
+  // 2 x 4 bytes per input sample per call)
+  for (int64_t key : d_touched) d_memo[key & 1][key >> 1] = -1;
+  for (int64_t key : d_skip_touched) d_skip[key & 1][key >> 1] = 0;
+  d_touched.clear();
+  d_skip_touched.clear();
+  for (int pl = 0; pl < 2; ++pl) {
+    if (d_memo[pl].size() < npos) d_memo[pl].resize(npos, -1);
+    if (d_skip[pl].size() < npos) d_skip[pl].resize(npos, 0);
+  }
   d_rsynd.clear();
   d_rpacked.clear();
 

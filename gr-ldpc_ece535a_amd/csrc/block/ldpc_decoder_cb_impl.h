@@ -67,6 +67,10 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   // d_rpacked (-1: not decoded, -2: wanted by the launch being planned).  Keys are (p << 1) | pol.
   std::vector<int32_t> d_memo[2];
   std::vector<int32_t> d_rsynd;
+  // d_skip[pol][p] > p: frames p, p + N, ... before it are decoded and pass
+  std::vector<int32_t> d_skip[2];
+  // keys whose memo / jump entries this call set (reset at the next call)
+  std::vector<int64_t> d_touched, d_skip_touched;
   std::vector<uint8_t> d_rpacked;
   std::vector<int64_t> d_want;   // keys of the next launch
 
@@ -85,6 +89,8 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   // out-of-sync positions with missing windows, or max_want keys.
   Outcome replay(Replay &r, bool exact, int nin, int noutput, unsigned char *out, int max_out,
                  size_t max_want);
+  // Frames pos, pos + N, ... decoded at pol that pass, counted (jump table)
+  int pass_run(int pol, int pos, int nin);
   // Dry run: adds window (pos, pol) to d_want unless decoded or wanted (memo -2)
   void want(int64_t pos, int pol, int nin);
   // Dry run: the windows the loop needs if search position q syncs
