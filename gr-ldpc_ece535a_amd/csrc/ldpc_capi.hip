@@ -1218,6 +1218,8 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
     float *h = ctx->h_stage;
     if (elem_stride == 1)
       memcpy(h, in, (size_t)S * 4);
+    else if (elem_stride == 2)  // gr_complex real parts (the block): a constant stride vectorises
+      for (int64_t i = 0; i < S; ++i) h[i] = in[2 * i];
     else
       for (int64_t i = 0; i < S; ++i) h[i] = in[i * elem_stride];
     if ((e = hipMemcpyAsync(d_span, h, (size_t)S * 4, hipMemcpyHostToDevice, ctx->stream)) !=
