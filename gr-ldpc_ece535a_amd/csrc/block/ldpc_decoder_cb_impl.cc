@@ -302,6 +302,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       const int k = std::min(pass_run(pol, pos, nin), (noutput - r.produced) / mo);
       if (k > 0) {
         if (exact) {
+          d_grid_frames += k;
           for (int i = 0; i < k; ++i)
             std::memcpy(out + r.produced + (size_t)i * mo,
                         &d_rpacked[(size_t)d_memo[pol][pos + i * N] * KB], (size_t)mo);
@@ -335,7 +336,8 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       guessed_out = !pass;
       // a frame in sync is also wanted at the other polarity when its result
       // decides a sync loss's "-tx" retry (:178-187)
-      if (pass && d_spec_both) want(pos, pol ^ 1, nin);
+      if (pass && (d_spec_both == 1 || (d_spec_both > 1 && 8 * d_grid_fails > d_grid_frames)))
+        want(pos, pol ^ 1, nin);
       if (!pass && r.state == STATE_OUT_OF_SYNC) d_forks.push_back(pos);
     }
     if (exact && pass && r.state != STATE_OUT_OF_SYNC) {
@@ -343,6 +345,14 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       // misaligned pair passes ~1e-4 of the time)
       if (d_last_pass == d_abs + pos - N) d_anchor = (int)((d_abs + pos) % N);
       d_last_pass = d_abs + pos;
+    }
+    if (exact && r.state != STATE_OUT_OF_SYNC) {  // the grid's failure rate, decayed
+      d_grid_frames += 1;
+      d_grid_fails += pass ? 0 : 1;
+      if (d_grid_frames > 4096) {
+        d_grid_frames *= 0.5;
+        d_grid_fails *= 0.5;
+      }
     }
     if (!pass) {
       if (n.state != STATE_OUT_OF_SYNC) {  // :169-176

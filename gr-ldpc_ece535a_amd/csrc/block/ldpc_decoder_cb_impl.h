@@ -40,8 +40,12 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   int64_t d_frames_decoded;
   int64_t d_launches = 0;
   bool d_debug = getenv("LDPC_BLOCK_DEBUG") != nullptr;  // one line per launch on stderr
-  // A/B knob: LDPC_BLOCK_SPEC_BOTH=0 speculates in-sync frames at one polarity
-  bool d_spec_both = !(getenv("LDPC_BLOCK_SPEC_BOTH") && getenv("LDPC_BLOCK_SPEC_BOTH")[0] == '0');
+  // In-sync frames guessed to pass are also wanted at the other polarity
+  // (LDPC_BLOCK_SPEC_BOTH):
+  // 0: never, 1: always, otherwise (default) when more than 1 in 8 frames on
+  // the grid fail (then sync losses, and their retries, are frequent)
+  int d_spec_both = getenv("LDPC_BLOCK_SPEC_BOTH") ? atoi(getenv("LDPC_BLOCK_SPEC_BOTH")) : 2;
+  double d_grid_frames = 0, d_grid_fails = 0;  // decayed counts of in-sync frames
   // A/B knob: LDPC_BLOCK_FORK=1 also decodes the branches where a search position syncs
   bool d_fork = getenv("LDPC_BLOCK_FORK") && getenv("LDPC_BLOCK_FORK")[0] == '1';
   // A/B knob: LDPC_BLOCK_ANCHOR=0 guesses every in-sync window passes
