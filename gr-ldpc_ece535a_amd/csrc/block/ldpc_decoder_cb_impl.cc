@@ -47,8 +47,10 @@
 #include <gnuradio/io_signature.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <iostream>
+#include <cstdio>
 #include <stdexcept>
 #include <string>
 
@@ -184,7 +186,20 @@ ldpc_decoder_cb_impl::ldpc_decoder_cb_impl(int method, int iterations, ldpc_bloc
   d_backend_user = user;
 }
 
-ldpc_decoder_cb_impl::~ldpc_decoder_cb_impl() { ldpc_destroy(d_ctx); }
+ldpc_decoder_cb_impl::~ldpc_decoder_cb_impl() {
+  if (d_profile)
+    fprintf(stderr,
+            "ldpc_decoder_cb profile: %lld launches; general_work %.3f ms = exact replay %.3f + "
+            "dry runs %.3f + decode launches %.3f (GPU round trips) + rest\n",
+            (long long)d_launches, 1e3 * d_prof[0], 1e3 * d_prof[1], 1e3 * d_prof[2],
+            1e3 * d_prof[3]);
+  ldpc_destroy(d_ctx);
+}
+
+double ldpc_decoder_cb_impl::now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
 
 void ldpc_decoder_cb_impl::forecast(int noutput_items, gr_vector_int &ninput_items_required) {
   ninput_items_required[0] = noutput_items * d_N;
@@ -413,6 +428,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
 int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_items,
                                        gr_vector_const_void_star &input_items,
                                        gr_vector_void_star &output_items) {
+  const double t_call = d_profile ? now_s() : 0.0;
   const float *in = (const float *)input_items[0];  // interleaved re/im
   unsigned char *out = (unsigned char *)output_items[0];
   const int N = (int)d_N;
@@ -435,7 +451,9 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   Replay r{d_state, d_errors, 0, 0};
   int out_budget = kSearchFirst;  // out-of-sync positions one launch may guess past
   bool first = true, last_out = false;
+  double t0 = d_profile ? now_s() : 0.0;
   while (replay(r, true, nin, noutput_items, out, 0, 0) == STALLED) {
+    if (d_profile) d_prof[1] += now_s() - t0;
     // the loop needs a window not decoded yet: dry-run ahead from here to
     // collect the windows it will probably need, and decode them at once
     const bool now_out = r.state == STATE_OUT_OF_SYNC;
@@ -447,6 +465,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
     d_want.clear();
     d_forks.clear();
     Replay dry = r;
+    if (d_profile) t0 = now_s();
     replay(dry, false, nin, noutput_items, nullptr, out_budget, (size_t)kMaxWindows);
     // then the branches where a search position passes, nearest first, while
     // the launch has room: windows up to about one per wave slot of the GPU
@@ -460,8 +479,22 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       std::cerr << "ldpc_decoder_cb: stall at " << r.consumed << " state " << r.state
                 << " errors " << r.errors << " grid " << d_anchor << ": launch " << d_want.size()
                 << " windows, dry run to " << dry.consumed << " state " << dry.state << std::endl;
+    if (d_profile) {
+      const double t1 = now_s();
+      d_prof[2] += t1 - t0;
+      t0 = t1;
+    }
     decode_wanted(in, nin, first);
+    if (d_profile) {
+      const double t1 = now_s();
+      d_prof[3] += t1 - t0;
+      t0 = t1;
+    }
     first = false;
+  }
+  if (d_profile) {
+    d_prof[1] += now_s() - t0;
+    d_prof[0] += now_s() - t_call;
   }
   d_state = r.state;
   d_errors = r.errors;

@@ -40,6 +40,10 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   int64_t d_frames_decoded;
   int64_t d_launches = 0;
   bool d_debug = getenv("LDPC_BLOCK_DEBUG") != nullptr;  // one line per launch on stderr
+  // LDPC_BLOCK_PROFILE: host time split of general_work, printed when destroyed
+  bool d_profile = getenv("LDPC_BLOCK_PROFILE") != nullptr;
+  double d_prof[4] = {0, 0, 0, 0};  // total, exact replay, dry runs, decode launches
+  static double now_s();
   // In-sync frames guessed to pass are also wanted at the other polarity
   // (LDPC_BLOCK_SPEC_BOTH):
   // 0: never, 1: always, otherwise (default) when more than 1 in 8 frames on

@@ -50,6 +50,9 @@ def main():
                   "%.2f windows per output frame" % (
                       db, name, made * 8 / dt / 1e6, dt / calls * 1e3, calls, launches / calls,
                       windows / max(1, made / 4)), flush=True)
+            del blk  # LDPC_BLOCK_PROFILE prints its split when the block is destroyed
+            import gc
+            gc.collect()
 
 
 if __name__ == "__main__":
