@@ -1263,9 +1263,9 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   if (!direct && (e = hipMemcpyAsync(h_out, d_pk, out_bytes, hipMemcpyDeviceToHost,
                                      ctx->stream)) != hipSuccess)
     return hip_err(ctx, e, "hipMemcpyAsync(out)");
-  // the block waits on one frame's latency per launch: poll rather than
-  // sleep on the completion (LDPC_WIN_SPIN=0: hipStreamSynchronize)
-  static const bool no_spin = getenv("LDPC_WIN_SPIN") && getenv("LDPC_WIN_SPIN")[0] == '0';
+  // wait for the launch; polling instead of hipStreamSynchronize
+  // (LDPC_WIN_SPIN=1) measured no faster (profiles/round2/block/window_latency.txt)
+  static const bool no_spin = !(getenv("LDPC_WIN_SPIN") && getenv("LDPC_WIN_SPIN")[0] == '1');
   if (no_spin) {
     if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
       return hip_err(ctx, e, "hipStreamSynchronize");
