@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--sizes", default="1,64,256,1024,4096")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--label", default="")
+    ap.add_argument("--iters", default="50", help="iteration caps, comma-separated")
     a = ap.parse_args()
     import torch  # noqa: F401
     import bench
@@ -29,17 +30,19 @@ def main():
     Bmax = max(int(v) for v in a.sizes.split(","))
     y, _ = bench.synth(dec.H, Bmax + 1, -3.0, 11)
     span = y.ravel().astype(np.float32)
-    for B in [int(v) for v in a.sizes.split(",")]:
-        rng = np.random.default_rng(B)
-        w = (rng.integers(0, span.size - 64, size=B).astype(np.int64) << 1) | rng.integers(0, 2, B)
-        dec.decode_windows(span, w)  # stage the span
-        ts = []
-        for _ in range(a.reps):
-            t0 = time.perf_counter()
-            dec.decode_windows(span, w, reuse_span=True)
-            ts.append(time.perf_counter() - t0)
-        print("%s B=%5d median %.1f us  min %.1f us" % (a.label, B, 1e6 * np.median(ts),
-                                                        1e6 * np.min(ts)), flush=True)
+    for it in [int(v) for v in a.iters.split(",")]:
+        for B in [int(v) for v in a.sizes.split(",")]:
+            rng = np.random.default_rng(B)
+            w = (rng.integers(0, span.size - 64, size=B).astype(np.int64) << 1) | \
+                rng.integers(0, 2, B)
+            dec.decode_windows(span, w, max_iters=it)  # stage the span
+            ts = []
+            for _ in range(a.reps):
+                t0 = time.perf_counter()
+                dec.decode_windows(span, w, max_iters=it, reuse_span=True)
+                ts.append(time.perf_counter() - t0)
+            print("%s iters=%2d B=%5d median %.1f us  min %.1f us" % (
+                a.label, it, B, 1e6 * np.median(ts), 1e6 * np.min(ts)), flush=True)
 
 
 if __name__ == "__main__":
