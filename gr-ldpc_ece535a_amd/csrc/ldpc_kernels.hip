@@ -347,14 +347,21 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
         for (int k = 0; k < DVN; ++k) ev[k] = lds_ld<Real>(ea[q][k]);
         // L = sum_j (E(j,i) + r(i)), ascending j; 1 iff L <= 0 (:519-532)
-        Real acc = Real(0);
 #pragma unroll
-        for (int k = 0; k < DVN; ++k) {
-          tv[q][k] = ev[k] + rc[q];
-          if constexpr (FIN)
-            acc = acc + tv[q][k];  // a missing edge's term is exactly +0.0
-          else
-            acc = ea[q][k] != eb_dummy ? acc + tv[q][k] : acc;
+        for (int k = 0; k < DVN; ++k) tv[q][k] = ev[k] + rc[q];
+        Real acc = Real(0);
+        if constexpr (FIN) {
+          // +0.0 + x == x for every x but -0.0, and no term is -0.0 here: a
+          // check message is never -0.0 (E = log(1) = +0.0 at T = +-0), so
+          // E + r is -0.0 only if both are, and a missing edge's term is
+          // exactly +0.0.  The sums start at their first term instead of the
+          // reference's 0.0 seed (the same value, one f64 add fewer).
+          acc = tv[q][0];
+#pragma unroll
+          for (int k = 1; k < DVN; ++k) acc = acc + tv[q][k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < DVN; ++k) acc = ea[q][k] != eb_dummy ? acc + tv[q][k] : acc;
         }
         post[q] = acc;
         hard[q] = __builtin_amdgcn_ballot_w64(acc <= Real(0)) & col_ok[q];
@@ -368,13 +375,15 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
         for (int k = 0; k < DVN; ++k) {
           Real m = Real(0);
+          bool first = true;  // FIN: seeded with the first term (see acc above)
 #pragma unroll
           for (int k2 = 0; k2 < DVN; ++k2) {
             if (k2 == k) continue;
             if constexpr (FIN)
-              m = m + tv[q][k2];
+              m = first ? tv[q][k2] : m + tv[q][k2];
             else
               m = ea[q][k2] != eb_dummy ? m + tv[q][k2] : m;
+            first = false;
           }
           mv[q][k] = m;
         }
