@@ -205,6 +205,33 @@ def reduce_results(dist, packed, counters, wall, device=None):
     return full, c, float(w.item())
 
 
+def gathered_parity(L, torch, orc, dec, args, dev, full, world, Hr, csr, threads, sample=256):
+    """Rank 0, N > 1: the all-gathered outputs (every rank's first batch, in
+    rank order) against the oracle.  Each rank's batch is made again here from
+    its seed (synth_device is deterministic) and the first `sample` frames of
+    every rank are decoded on the CPU."""
+    full = full.cpu().numpy()
+    pos, frames, bad = 0, 0, 0
+    for rk in range(world):
+        _, Br = plan_batch(args.batch, world, rk, args.strong)
+        y = synth_device(L, torch, dec, Br, args.ebn0, args.seed + 7919 * rk, dev)[0]
+        nb = min(Br, sample)
+        llr = y[:nb].cpu().numpy()
+        if csr is not None:
+            ref = orc.decode_batch_sparse(args.method, csr[2], csr[3], csr[0], csr[1], llr,
+                                          args.iters, nthreads=threads, want_bits=False)
+        else:
+            ref = orc.decode_batch(args.method, Hr, llr, args.iters, nthreads=threads,
+                                   et_period=args.et_period)
+        bad += int((ref["packed"] != full[pos:pos + nb]).any(axis=1).sum())
+        frames += nb
+        pos += Br
+    return {"ranks": world, "frames": frames, "gathered_frames": int(full.shape[0]),
+            "packed_mismatch_frames": bad,
+            "checker": "first %d frames of every rank's batch (made again from the rank's seed) "
+                       "vs the oracle, compared with the all-gathered outputs" % sample}
+
+
 def plan_batch(B, world, rank, strong):
     """Frames this rank decodes: (offset in the global batch, count).  Weak
     scaling: every rank its own B frames; strong: shard_range of one B."""
@@ -554,10 +581,20 @@ def main():
     import ldpc_ece535a as L
 
     dist = None
+    # LDPC_BENCH_SHARE_GPU=1: ranks share the visible GPUs (local % count) --
+    # a rehearsal of the N-rank path on a one-GPU box, with
+    # LDPC_BENCH_DIST_BACKEND=gloo (RCCL wants one GPU per rank).  The driver's
+    # runs set neither: one rank per GPU over RCCL.
+    if os.environ.get("LDPC_BENCH_SHARE_GPU") == "1":
+        local = local % max(1, torch.cuda.device_count())
+    backend = os.environ.get("LDPC_BENCH_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
         dist = tdist
     dev = torch.device("cuda", local)
     prec = 0 if args.precision == "f64" else 1
@@ -610,7 +647,9 @@ def main():
                 sum(steps_of[j] * B * dec.K for j in range(D)),
                 sum(steps_of[j] * int(iters_b[j].sum()) for j in range(D)),
                 sum(steps_of[j] * int((synd_b[j] > 0).sum()) for j in range(D))]
-    full, totals, wall_max = reduce_results(dist, r["outs"][0][0], counters, wall, dev)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
+    full, totals, wall_max = reduce_results(
+        dist, r["outs"][0][0].to(red_dev), counters, wall, red_dev)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -772,6 +811,9 @@ def main():
                                                et_period=args.et_period)
                 line["variants_1gpu"][name]["packed_mismatch_frames"] = int(
                     (refs[m]["packed"] != pk).any(axis=1).sum())
+        if world > 1:
+            line["parity_all_ranks"] = gathered_parity(L, torch, orc, dec, args, dev, full, world,
+                                                       Hr, csr, threads)
     if pre["config4_check"] is not None:
         pre["config4_check"]()
     print(json.dumps(line), flush=True)
