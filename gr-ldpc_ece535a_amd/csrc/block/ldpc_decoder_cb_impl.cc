@@ -2,8 +2,10 @@
 /*
  * LDPC decoder block implementation (MI355X edition).
  *
- * general_work reproduces lib/ldpc_decoder_cb_impl.cc:133-234 of
- * gr-ldpc_ece535a output for output, for any chunking of the input.  The
+ * general_work reproduces the control flow of lib/ldpc_decoder_cb_impl.cc:133-234
+ * of gr-ldpc_ece535a for any chunking of the input; its outputs equal the
+ * reference's as far as the window decodes do (parity measured, not proven:
+ * see the end of this comment and DESIGN.md section 3).  The
  * reference loop decodes one window per step -- the N samples at the
  * current position times +-1 -- and its state machine decides the next
  * position.  Here the loop is replayed exactly over a memo of decoded
