@@ -577,9 +577,13 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           bit = acc <= Real(0);
           post[q] = acc;
         } else {
-          // s = sum_i L(r_ji) (:380-385); L(Q) = Lci + s; 1 iff L(Q) < 0 (:395-402)
+          // s = sum_i L(r_ji) (:380-385); L(Q) = Lci + s; 1 iff L(Q) < 0 (:395-402).
+          // Seeded with the first term, not 0.0: an L(r) is never -0.0 (a zero
+          // |beta| sets the zero flag, which yields +0.0) and missing edges read
+          // +0.0, so 0.0 + x == x for every term.
+          acc = ev[0];
 #pragma unroll
-          for (int k = 0; k < DVN; ++k) acc = acc + ev[k];
+          for (int k = 1; k < DVN; ++k) acc = acc + ev[k];
           const Real LQ = rc + acc;
           sb[c] = LQ;
           bit = LQ < Real(0);
