@@ -78,7 +78,8 @@ def parse(argv=None):
     ap.add_argument("--method", type=int, default=None, help="default 1 (0 for dvbs2)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 variant")
     ap.add_argument("--no-block", action="store_true", help="skip the block-throughput variant")
-    ap.add_argument("--precision", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--precision", choices=["f64", "f64libm", "f32"], default="f64",
+                    help="f64: LDPC_PREC_F64 (default), f64libm: LDPC_PREC_F64_LIBM, f32")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--et-period", type=int, default=1)
     ap.add_argument("--ebn0", type=float, default=2.0)
@@ -166,7 +167,7 @@ def synth(Hr, B, ebn0, seed):
 
 
 def bytes_per_iter(E, N, prec):
-    return 32 * E + 10 * N if prec == 0 else 16 * E + 6 * N
+    return 16 * E + 6 * N if prec == 1 else 32 * E + 10 * N
 
 
 # --------------------------------------------------------------------------
@@ -597,7 +598,7 @@ def main():
             tdist.init_process_group(backend)
         dist = tdist
     dev = torch.device("cuda", local)
-    prec = 0 if args.precision == "f64" else 1
+    prec = {"f64": 0, "f32": 1, "f64libm": 2}[args.precision]
     dvb = args.code == "dvbs2"
     if args.method is None:
         args.method = 0 if dvb else 1
@@ -689,7 +690,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.strong and world > 1 else "weak",
         "vs_baseline": None,
-        "dtype": args.precision,
+        "dtype": "f64" if args.precision == "f64libm" else args.precision,
         "data": "synthetic, made on the GPU: Philox bits, GF(2) systematic encode "
                 "(ldpc_encode_device), BPSK, AWGN sigma=sqrt(10^(-EbN0/10))",
         "config": {
