@@ -82,3 +82,42 @@ def test_plan_batch():
     parts = [bench.plan_batch(4097, 8, r, True) for r in range(8)]
     assert sum(n for _, n in parts) == 4097 and parts[0][0] == 0
     assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(7))
+
+
+@pytest.mark.parametrize("strong", [False, True])
+def test_gathered_parity(monkeypatch, strong):
+    """bench.gathered_parity (rank 0, N > 1): every rank's batch is made again
+    from its seed and checked against the all-gathered outputs.  The device
+    synthesis is replaced by fixture frames chosen by the rank the seed
+    encodes; one corrupted frame of rank 1 must be counted."""
+    import sys
+    import types
+    import torch
+    sys.path[:0] = [REPO, os.path.join(REPO, "gr-ldpc_ece535a_amd")]
+    import bench
+    from oracle import oracle as orc
+    fd = np.load(os.path.join(REPO, "tests", "golden", "frames_default.npz"))
+    Hr = fd["H_reordered"]
+    allframes = np.concatenate([fd["db2_llr"], fd["db0_llr"], fd["db4_llr"]])
+    world, B = 2, 48
+    args = types.SimpleNamespace(batch=B, strong=strong, ebn0=2.0, seed=2024, method=1,
+                                 iters=50, et_period=1)
+
+    def fake_synth(L, torch_, dec, Br, ebn0, seed, dev):
+        rk = (seed - args.seed) // 7919
+        off, n = bench.plan_batch(B, world, rk, strong)
+        assert n == Br
+        return torch.from_numpy(allframes[off:off + n].copy()), None
+
+    monkeypatch.setattr(bench, "synth_device", fake_synth)
+    total = B if strong else world * B
+    full = torch.from_numpy(orc.decode_batch(1, Hr, allframes[:total], 50)["packed"])
+    r = bench.gathered_parity(None, torch, orc, None, args, None, full, world, Hr, None, 2,
+                              sample=16)
+    assert r["ranks"] == world and r["frames"] == 2 * 16 and r["gathered_frames"] == total
+    assert r["packed_mismatch_frames"] == 0
+    _, n0 = bench.plan_batch(B, world, 0, strong)
+    full[n0 + 3] ^= 1  # rank 1's fourth frame
+    r = bench.gathered_parity(None, torch, orc, None, args, None, full, world, Hr, None, 2,
+                              sample=16)
+    assert r["packed_mismatch_frames"] == 1
