@@ -597,7 +597,13 @@ LDPC_HD double log_ratio_tab(double T, const LogTabEntry *tab) {
   const uint32_t hx = (uint32_t)(ix >> 32);
   const uint32_t th = hx - 0x3FE60000u;
   // byte offset of bucket (th >> (20 - kLogTabBits)) % 2^kLogTabBits in one shift and one mask
+#if defined(LDPC_PROBE_LOGTAB_LANE) && defined(__HIP_DEVICE_COMPILE__)
+  // diagnostic build only (wrong results): every lane reads its own entry,
+  // so the table reads are conflict-free (tools/probe_logtab.sh)
+  const uint32_t off = (__builtin_amdgcn_workitem_id_x() & 63u) << 4;
+#else
   const uint32_t off = (th >> (20 - kLogTabBits - 4)) & (((1u << kLogTabBits) - 1) << 4);
+#endif
   const int k = (int)th >> 20;
   const uint64_t iz = ((uint64_t)(hx - (th & 0xFFF00000u)) << 32) | (ix & 0xFFFFFFFFull);
   double z;
@@ -631,7 +637,13 @@ LDPC_HD double log_q_tab_open(double q, const LogTabEntry *tab) {
   __builtin_memcpy(&ix, &q, 8);
   const uint32_t hx = (uint32_t)(ix >> 32);
   const uint32_t th = hx - 0x3FE60000u;
+#if defined(LDPC_PROBE_LOGTAB_LANE) && defined(__HIP_DEVICE_COMPILE__)
+  // diagnostic build only (wrong results): every lane reads its own entry,
+  // so the table reads are conflict-free (tools/probe_logtab.sh)
+  const uint32_t off = (__builtin_amdgcn_workitem_id_x() & 63u) << 4;
+#else
   const uint32_t off = (th >> (20 - kLogTabBits - 4)) & (((1u << kLogTabBits) - 1) << 4);
+#endif
   const int k = (int)th >> 20;
   const uint64_t iz = ((uint64_t)(hx - (th & 0xFFF00000u)) << 32) | (ix & 0xFFFFFFFFull);
   double z;
