@@ -78,8 +78,10 @@ def parse(argv=None):
     ap.add_argument("--method", type=int, default=None, help="default 1 (0 for dvbs2)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 variant")
     ap.add_argument("--no-block", action="store_true", help="skip the block-throughput variant")
-    ap.add_argument("--precision", choices=["f64", "f64libm", "f32"], default="f64",
-                    help="f64: LDPC_PREC_F64 (default), f64libm: LDPC_PREC_F64_LIBM, f32")
+    ap.add_argument("--precision", choices=["f64", "f64libm", "f64fast", "f32"], default="f64",
+                    help="f64: LDPC_PREC_F64 (default, bit-exact), f64libm: LDPC_PREC_F64_LIBM "
+                         "(exact, unbatched divisions), f64fast: LDPC_PREC_F64_FAST (compact "
+                         "tanh/log, not exact), f32")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--et-period", type=int, default=1)
     ap.add_argument("--ebn0", type=float, default=2.0)
@@ -501,6 +503,7 @@ def gpu_variants(L, torch, dec, args, dev, inputs, B, D, prec, dvb, world, rank)
                          "latency_ms_per_batch": round(r1["per_launch_ms"], 5)}
     if not dvb:
         for name, (m, p) in {"sum-product f32": (1, 1), "sum-product f64": (1, 0),
+                             "sum-product f64fast (compact tanh/log, not exact)": (1, 3),
                              "min-sum f64": (0, 0), "min-sum f32": (0, 1)}.items():
             if (m, p) == (args.method, prec):
                 continue
@@ -598,7 +601,7 @@ def main():
             tdist.init_process_group(backend)
         dist = tdist
     dev = torch.device("cuda", local)
-    prec = {"f64": 0, "f32": 1, "f64libm": 2}[args.precision]
+    prec = {"f64": 0, "f32": 1, "f64libm": 2, "f64fast": 3}[args.precision]
     dvb = args.code == "dvbs2"
     if args.method is None:
         args.method = 0 if dvb else 1
@@ -690,7 +693,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.strong and world > 1 else "weak",
         "vs_baseline": None,
-        "dtype": "f64" if args.precision == "f64libm" else args.precision,
+        "dtype": "f32" if args.precision == "f32" else "f64",
         "data": "synthetic, made on the GPU: Philox bits, GF(2) systematic encode "
                 "(ldpc_encode_device), BPSK, AWGN sigma=sqrt(10^(-EbN0/10))",
         "config": {

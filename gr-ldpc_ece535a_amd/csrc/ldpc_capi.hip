@@ -316,7 +316,8 @@ int check_decode_args(ldpc_ctx *ctx, int &method, int max_iters, int et_period, 
     return set_err(ctx, LDPC_EINVAL, "max_iters must be >= 1 for min-sum / sum-product");
   if (method == 2 && max_iters < 0) return set_err(ctx, LDPC_EINVAL, "max_iters < 0");
   if (et_period < 1) return set_err(ctx, LDPC_EINVAL, "et_period must be >= 1");
-  if (precision != LDPC_PREC_F64 && precision != LDPC_PREC_F32 && precision != LDPC_PREC_F64_LIBM)
+  if (precision != LDPC_PREC_F64 && precision != LDPC_PREC_F32 &&
+      precision != LDPC_PREC_F64_LIBM && precision != LDPC_PREC_F64_FAST)
     return set_err(ctx, LDPC_EINVAL, "precision must be one of LDPC_PREC_*");
   if (elem_stride < 1 || cw_stride < 0) return set_err(ctx, LDPC_EINVAL, "bad strides");
   return LDPC_OK;

@@ -8,61 +8,143 @@
 #include <float.h>
 #include <math.h>
 
+#include "ldpc_exact.hpp"
 #include "ldpc_math.hpp"
 
 namespace ldpc {
 
 // Arithmetic per precision mode (include/ldpc_hip.h LDPC_PREC_*):
-//   0 F64       double, compact two-range tanh (glibc's double near 1, <= 3 ulp
-//               elsewhere) and table-driven
-//               log (<= 1 ulp) of ldpc_math.hpp, reciprocal-based divisions
+//   0 F64       double, glibc's tanh(m/2) and log((1+T)/(1-T)) bit for bit
+//               (ldpc_exact.hpp), n quotients per shared reciprocal with
+//               correctly rounded results -- the reference's arithmetic
+//   2 F64_LIBM  the same functions one value at a time (no shared
+//               reciprocal): an independent evaluation of mode 0
+//   3 F64_FAST  double, compact approximations (ldpc_math.hpp): tanh within
+//               3 ulp of glibc, table log within 1 ulp -- faster, not exact
 //   1 F32       float, ROCm libm
-//   2 F64_LIBM  double, fdlibm tanh bit-identical to glibc's, fdlibm log
+// tanh_half(m) = tanh(m / 2) (:509); check_msg(T, tab) = log((1+T)/(1-T))
+// (:513); the _n forms take n independent operands (a lane's edge slots /
+// column entries) so their divisions can share one reciprocal.  `Tab` is
+// the log table the kernels stage in LDS (stage_tab) and pass back in.
 template <int PREC>
 struct Math;
-// The 512-entry log table of LDPC_PREC_F64's check message (ldpc_logtab.hpp);
-// kernels stage it in LDS (stage_logtab) and pass that copy to check_msg.
+
+__device__ const ex::GlLogEntry kGlLogTab[1 << ex::kGlTabBits] = {LDPC_GLIBC_LOG_TAB};
+// The 512-entry table of LDPC_PREC_F64_FAST's log (ldpc_logtab.hpp).
 __device__ const fm::LogTabEntry kLogTab[1 << fm::kLogTabBits] = {LDPC_LOGTAB_ENTRIES};
 
-// Every thread of the block takes part; one __syncthreads.
-__device__ __forceinline__ void stage_logtab(fm::LogTabEntry *lds) {
-  for (int i = threadIdx.x; i < (1 << fm::kLogTabBits); i += blockDim.x) lds[i] = kLogTab[i];
-  __syncthreads();
-}
-
-// tanh_half(m) = tanh(m / 2) (:509); check_msg(T, tab) = log((1+T)/(1-T))
-// (:513), tab = the LDS copy of kLogTab (used by LDPC_PREC_F64 only).
 template <>
 struct Math<0> {
   typedef double Real;
-#ifdef LDPC_TANH_SINGLE_RANGE  // A/B only: loses parity on large-amplitude frames
-  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_fast(m); }
-#else
-  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_acc(m); }
-#endif
-  static __device__ __forceinline__ double check_msg(double T, const fm::LogTabEntry *tab) {
-    return fm::log_ratio_tab(T, tab);
+  typedef ex::GlLogEntry Tab;
+  static constexpr int kTabN = 1 << ex::kGlTabBits;
+  static __device__ __forceinline__ const Tab *tab_src() { return kGlLogTab; }
+  template <int n>
+  static __device__ __forceinline__ void tanh_half_n(const double (&m)[n], double (&z)[n]) {
+    ex::tanh_half_n<n>(m, z);
+  }
+  template <int n>
+  static __device__ __forceinline__ void check_msg_n(const double (&T)[n], const Tab *tab,
+                                                     double (&E)[n]) {
+    ex::log_ratio_n<n>(T, tab, E);
+  }
+  static __device__ __forceinline__ double tanh_half(double m) {
+    const double v[1] = {m};
+    double z[1];
+    ex::tanh_half_n<1>(v, z);
+    return z[0];
+  }
+  static __device__ __forceinline__ double check_msg(double T, const Tab *tab) {
+    const double v[1] = {T};
+    double e[1];
+    ex::log_ratio_n<1>(v, tab, e);
+    return e[0];
   }
   static __device__ __forceinline__ double abs_(double x) { return ::fabs(x); }
   static __device__ __forceinline__ double max_() { return DBL_MAX; }
 };
 template <>
 struct Math<2> : Math<0> {
-  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_f64_bf(m / 2.0); }
-  static __device__ __forceinline__ double check_msg(double T, const fm::LogTabEntry *) {
-    return fm::log_f64_bf((1.0 + T) / (1.0 - T));  // IEEE division
+  template <int n>
+  static __device__ __forceinline__ void tanh_half_n(const double (&m)[n], double (&z)[n]) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) z[i] = Math<0>::tanh_half(m[i]);
   }
+  template <int n>
+  static __device__ __forceinline__ void check_msg_n(const double (&T)[n], const Tab *tab,
+                                                     double (&E)[n]) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) E[i] = Math<0>::check_msg(T[i], tab);
+  }
+};
+template <>
+struct Math<3> {
+  typedef double Real;
+  typedef fm::LogTabEntry Tab;
+  static constexpr int kTabN = 1 << fm::kLogTabBits;
+  static __device__ __forceinline__ const Tab *tab_src() { return kLogTab; }
+#ifdef LDPC_TANH_SINGLE_RANGE  // A/B only: loses accuracy on large-amplitude frames
+  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_fast(m); }
+#else
+  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_acc(m); }
+#endif
+  static __device__ __forceinline__ double check_msg(double T, const Tab *tab) {
+    return fm::log_ratio_tab(T, tab);
+  }
+  template <int n>
+  static __device__ __forceinline__ void tanh_half_n(const double (&m)[n], double (&z)[n]) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) z[i] = tanh_half(m[i]);
+  }
+  template <int n>
+  static __device__ __forceinline__ void check_msg_n(const double (&T)[n], const Tab *tab,
+                                                     double (&E)[n]) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) E[i] = check_msg(T[i], tab);
+  }
+  static __device__ __forceinline__ double abs_(double x) { return ::fabs(x); }
+  static __device__ __forceinline__ double max_() { return DBL_MAX; }
 };
 template <>
 struct Math<1> {
   typedef float Real;
+  typedef float Tab;  // no table
+  static constexpr int kTabN = 0;
+  static __device__ __forceinline__ const Tab *tab_src() { return nullptr; }
   static __device__ __forceinline__ float tanh_half(float m) { return ::tanhf(m / 2.0f); }
-  static __device__ __forceinline__ float check_msg(float T, const fm::LogTabEntry *) {
+  static __device__ __forceinline__ float check_msg(float T, const Tab *) {
     return ::logf((1.0f + T) / (1.0f - T));
+  }
+  template <int n>
+  static __device__ __forceinline__ void tanh_half_n(const float (&m)[n], float (&z)[n]) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) z[i] = tanh_half(m[i]);
+  }
+  template <int n>
+  static __device__ __forceinline__ void check_msg_n(const float (&T)[n], const Tab *tab,
+                                                     float (&E)[n]) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) E[i] = check_msg(T[i], tab);
   }
   static __device__ __forceinline__ float abs_(float x) { return ::fabsf(x); }
   static __device__ __forceinline__ float max_() { return FLT_MAX; }
 };
+
+// LDS copy of mode PREC's log table (sized 1 for modes without one); every
+// thread of the block takes part, one __syncthreads.
+template <int PREC>
+struct TabLds {
+  typedef typename Math<PREC>::Tab Tab;
+  static constexpr int kN = Math<PREC>::kTabN > 0 ? Math<PREC>::kTabN : 1;
+};
+template <int PREC>
+__device__ __forceinline__ void stage_tab(typename Math<PREC>::Tab *lds) {
+  if constexpr (Math<PREC>::kTabN > 0) {
+    const typename Math<PREC>::Tab *src = Math<PREC>::tab_src();
+    for (int i = threadIdx.x; i < Math<PREC>::kTabN; i += blockDim.x) lds[i] = src[i];
+    __syncthreads();
+  }
+}
 
 // sign(), lib/ldpc_decoder_cb_impl.cc:574-578 (sign(0) == 0).
 template <typename Real>

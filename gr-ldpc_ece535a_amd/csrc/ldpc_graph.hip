@@ -162,10 +162,10 @@ __global__ void __launch_bounds__(256) g_check(GraphView g, GraphWork w_, int h)
   const GraphWork w = live(w_);
   typedef typename Math<PREC>::Real Real;
   const int k = blockIdx.y;
-  __shared__ fm::LogTabEntry logtab[1 << fm::kLogTabBits];
-  if constexpr (METHOD == 1 && PREC == 0) {
+  __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
+  if constexpr (METHOD == 1 && Math<PREC>::kTabN > 0) {
     if (w.chunk_done[k]) return;  // uniform per block: no thread misses the barrier
-    stage_logtab(logtab);
+    stage_tab<PREC>(logtab);
   }
   if (w.chunk_done[k]) return;
   const int lane = threadIdx.x & 63;
@@ -774,6 +774,8 @@ int launch_graph_decode(const GraphView &g, const GraphWork &w, const DecodeArgs
       run_soft<1, 1>(g, w, a, rgrid, cgrid, st);
     else if (prec == 2)
       run_soft<2, 1>(g, w, a, rgrid, cgrid, st);
+    else if (prec == 3)
+      run_soft<3, 1>(g, w, a, rgrid, cgrid, st);
     else
       run_soft<0, 1>(g, w, a, rgrid, cgrid, st);
   } else if (method == 2) {

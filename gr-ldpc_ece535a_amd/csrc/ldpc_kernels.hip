@@ -175,7 +175,8 @@ template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = k
 __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeArgs &a,
                                              const int64_t b, WaveTables<S, NW> &wt,
                                              Real *tb, Real *eb, Real *rb, Real *sb,
-                                             const int lane, const fm::LogTabEntry *logtab,
+                                             const int lane,
+                                             const typename Math<PREC>::Tab *logtab,
                                              const float (&xin)[NW], const int (&colq)[NW],
                                              const uint32_t (&ppos)[2]) {
   const int M = code.M, N = code.N;
@@ -251,9 +252,10 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         ea[q][k] = (FIN && e == eb_dummy) ? lds_addr(nr + lane + 64 * q) : e;
       }
     Real rc[NW];
-    // every check operand in tb is a tanh(m/2) with |m| <= LDPC_TANH_SPLIT
-    // (so |T| < 1 and finite): the check messages need no saturation select
-    bool open = FIN && PREC == 0 && LDPC_TANH_SPLIT > 0;
+    // F64_FAST only: every check operand in tb is a tanh(m/2) with
+    // |m| <= LDPC_TANH_SPLIT (so |T| < 1 and finite): the check messages need
+    // no saturation select
+    bool open = FIN && PREC == 3 && LDPC_TANH_SPLIT > 0;
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
       rc[q] = rb[lane + 64 * q];  // written by this lane above
@@ -292,7 +294,14 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
         for (int k = 0; k < DCN; ++k) T = T * nb[s][k];
         Ts[s] = T;
       }
-      if constexpr (FIN && PREC == 0 && LDPC_TANH_SPLIT > 0) {
+      if constexpr (PREC != 3) {
+        // the S check messages; modes 0 / 2: glibc's log((1+T)/(1-T)) bit for
+        // bit, mode 0 with the S quotients from one reciprocal
+        Real Es[S];
+        Math<PREC>::template check_msg_n<S>(Ts, logtab, Es);
+#pragma unroll
+        for (int s = 0; s < S; ++s) eb[lane + 64 * s] = Es[s];
+      } else if constexpr (FIN && LDPC_TANH_SPLIT > 0) {
         if (open) {
 #ifdef LDPC_NO_BATCH_DIV
 #pragma unroll
@@ -387,8 +396,18 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           }
           mv[q][k] = m;
         }
-      if constexpr (PREC == 0 && LDPC_TANH_SPLIT > 0) {
-        // tanh(m/2), :509.  While every |m| of the frame is below the split,
+      if constexpr (PREC != 3) {
+        // tanh(m/2), :509: glibc's, bit for bit; mode 0 forms the column's
+        // DVN quotients from one reciprocal
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          Real th[DVN];
+          Math<PREC>::template tanh_half_n<DVN>(mv[q], th);
+#pragma unroll
+          for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], th[k]);
+        }
+      } else if constexpr (LDPC_TANH_SPLIT > 0) {
+        // F64_FAST: tanh(m/2), :509.  While every |m| of the frame is below the split,
         // the single-range form (no cap, no range selects) is used: its 1-3 ulp
         // near 1 stay below ~1e-9 in the check messages there.  Otherwise the
         // two-range form, glibc's double near 1 (Math<0>::tanh_half).
@@ -489,12 +508,14 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 
     for (int h = 0; h < a.max_iters; ++h) {
       // ---- check-pass operand of every edge -> LDS ----------------------
+      if constexpr (METHOD == 1) {
+        Real th[S];
+        Math<PREC>::template tanh_half_n<S>(msg, th);  // :509
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if constexpr (METHOD == 1)
-          tb[lane + 64 * s] = Math<PREC>::tanh_half(msg[s]);  // :509
-        else
-          tb[lane + 64 * s] = msg[s];
+        for (int s = 0; s < S; ++s) tb[lane + 64 * s] = th[s];
+      } else {
+#pragma unroll
+        for (int s = 0; s < S; ++s) tb[lane + 64 * s] = msg[s];
       }
       wave_lds_sync();
       // gather the row neighbours of every slot (unconditional loads)
@@ -508,16 +529,24 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       for (int s = 0; s < S; ++s)
 #pragma unroll
         for (int k = 0; k < DCN; ++k) asm volatile("" ::"v"(nb[s][k]));
+      if constexpr (METHOD == 1) {
+        // T = prod_{k != i} tanh(M(j,k)/2), ascending k; E = log((1+T)/(1-T))
+        // (:506-513).  Padding neighbours read the 1.0 dummy: exact no-op.
+        Real Ts[S], Es[S];
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if constexpr (METHOD == 1) {
-          // T = prod_{k != i} tanh(M(j,k)/2), ascending k; E = log((1+T)/(1-T))
-          // (:506-513).  Padding neighbours read the 1.0 dummy: exact no-op.
+        for (int s = 0; s < S; ++s) {
           Real T = Real(1);
 #pragma unroll
           for (int k = 0; k < DCN; ++k) T = T * nb[s][k];
-          eb[lane + 64 * s] = Math<PREC>::check_msg(T, logtab);
-        } else {
+          Ts[s] = T;
+        }
+        Math<PREC>::template check_msg_n<S>(Ts, logtab, Es);
+#pragma unroll
+        for (int s = 0; s < S; ++s) eb[lane + 64 * s] = Es[s];
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if constexpr (METHOD == 0) {
           // min-sum horizontal step (:350-376): L(r) = p * alpha_self * min,
           // p = prod of every alpha of the row (self included), so
           // p * alpha_self = alpha_self^2 * prod_{others} alpha: 0 when any
@@ -753,8 +782,8 @@ __global__ void __launch_bounds__(kThreads, MINB)
   const int M = code.M;
   typedef Layout<Real, METHOD, S, NW, DVN> LW;
   constexpr SliceLayout L = LW::L;
-  __shared__ fm::LogTabEntry logtab[1 << fm::kLogTabBits];
-  if constexpr (METHOD == 1 && PREC == 0) stage_logtab(logtab);
+  __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
+  if constexpr (METHOD == 1) stage_tab<PREC>(logtab);
 
   int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave;
   if (b >= a.waves || b >= a.B) return;
@@ -926,8 +955,8 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
   Real *rb = reinterpret_cast<Real *>(smem + L.waves + (size_t)wave * L.per_wave);
   Real *sb = rb + 64 * NW;
   int *fslot = reinterpret_cast<int *>(smem + L.fslot);
-  __shared__ fm::LogTabEntry logtab[1 << fm::kLogTabBits];
-  if constexpr (METHOD == 1 && PREC == 0) stage_logtab(logtab);
+  __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
+  if constexpr (METHOD == 1) stage_tab<PREC>(logtab);
   if (tid == 0) tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
 
   // this lane's edge, and (every wave) the columns lane + 64 q
@@ -1158,7 +1187,7 @@ static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots, hi
   if constexpr (NW == 1 && METHOD <= 1) {
     if (code.dc_max <= 6 && code.dv_max <= 3) {
       // throughput mode (no issue-priority management): the 4-waves-per-SIMD build
-      if constexpr (PREC == 0 && METHOD == 1)
+      if constexpr ((PREC == 0 || PREC == 3) && METHOD == 1)
         if (a.fair_cycles == 0) switch (slots) {
             case 3: return launch_one<PREC, METHOD, 3, NW, 5, 3, 4>(code, a, st);
             case 4: return launch_one<PREC, METHOD, 4, NW, 5, 3, 4>(code, a, st);
@@ -1192,6 +1221,7 @@ static int launch_nw(const CodeView &code, const DecodeArgs &a, int method, int 
   if (mw && method == 1) {
     if (prec == 1) return launch_mw_slots<1, 1, NW>(code, a, slots, st);
     if (prec == 2) return launch_mw_slots<2, 1, NW>(code, a, slots, st);
+    if (prec == 3) return launch_mw_slots<3, 1, NW>(code, a, slots, st);
     return launch_mw_slots<0, 1, NW>(code, a, slots, st);
   }
   if (mw && method == 0)
@@ -1202,6 +1232,7 @@ static int launch_nw(const CodeView &code, const DecodeArgs &a, int method, int 
   if (method == 1) {
     if (prec == 1) return launch_slots<1, 1, NW>(code, a, slots, st);
     if (prec == 2) return launch_slots<2, 1, NW>(code, a, slots, st);
+    if (prec == 3) return launch_slots<3, 1, NW>(code, a, slots, st);
     return launch_slots<0, 1, NW>(code, a, slots, st);
   }
   // min-sum has no transcendentals: both f64 modes are the same kernel

@@ -12,7 +12,7 @@ lib/libldpc_hip.so; there is no CPU fallback.
 """
 from ._capi import (  # noqa: F401
     FLAG_NO_REORDER, METHOD_BITFLIP, METHOD_HARD, METHOD_LOGDOMAIN, METHOD_SUMPRODUCT,
-    PREC_F32, PREC_F64, PREC_F64_LIBM, Decoder, LdpcError, bpsk_awgn, check_frame, count_bit_errors,
+    PREC_F32, PREC_F64, PREC_F64_FAST, PREC_F64_LIBM, Decoder, LdpcError, bpsk_awgn, check_frame, count_bit_errors,
     default_h, encode, plan_layout, random_bits, reorder_h,
 )
 from .blocks import (  # noqa: F401,E402

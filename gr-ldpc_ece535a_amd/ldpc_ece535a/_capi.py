@@ -15,7 +15,7 @@ LIB_DIR = os.path.join(PKG_ROOT, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libldpc_hip.so")
 
 METHOD_LOGDOMAIN, METHOD_SUMPRODUCT, METHOD_BITFLIP, METHOD_HARD = 0, 1, 2, 3
-PREC_F64, PREC_F32, PREC_F64_LIBM = 0, 1, 2
+PREC_F64, PREC_F32, PREC_F64_LIBM, PREC_F64_FAST = 0, 1, 2, 3
 FLAG_NO_REORDER = 1
 FLAG_GRAPH = 2
 FLAG_PLAIN_LAYOUT = 4

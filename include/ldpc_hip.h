@@ -54,15 +54,22 @@ extern "C" {
 #define LDPC_METHOD_BITFLIP 2    /* decodeBitFlipping */
 #define LDPC_METHOD_HARD 3       /* decodeHard */
 
-/* arithmetic for methods 0/1.  The F64 modes repeat the reference's double
- * operations in the reference's order (parity modes): F64 (default) with
- * compact tanh/log within 3 ulp of glibc's, F64_LIBM with fdlibm tanh
- * bit-identical to glibc's (and fdlibm log); min-sum has no transcendentals
- * and is exact in both.  F32 is the fast mode: its hard decisions are
- * measured against the oracle, not guaranteed. */
+/* arithmetic for methods 0/1.
+ *   F64 (default)  the reference's double arithmetic bit for bit: its
+ *                  operations in its order, glibc's tanh(m/2) and
+ *                  log((1+T)/(1-T)) reproduced exactly, correctly rounded
+ *                  divisions -- hard decisions, posteriors and iteration
+ *                  counts identical to the reference CPU decoder's
+ *   F64_LIBM       the same results, each tanh / log / division evaluated on
+ *                  its own (no shared reciprocal): a second evaluation of F64
+ *   F64_FAST       double with compact tanh/log (within 3 / 1 ulp of glibc):
+ *                  faster, decisions not guaranteed identical (measured)
+ *   F32            float, ROCm libm: fast mode, decisions measured only
+ * min-sum has no transcendentals: every double mode is the same exact kernel. */
 #define LDPC_PREC_F64 0
 #define LDPC_PREC_F32 1
 #define LDPC_PREC_F64_LIBM 2
+#define LDPC_PREC_F64_FAST 3
 
 /* ldpc_create flags */
 #define LDPC_FLAG_NO_REORDER 1 /* use H as given (skip reorderHMatrix) */

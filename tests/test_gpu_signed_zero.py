@@ -36,9 +36,17 @@ def _frames(golden):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("prec", [0, 2])
+@pytest.mark.parametrize("prec", [0, 2, 3])
 @pytest.mark.parametrize("method", [0, 1])
 def test_signed_zero_samples(golden, method, prec, mode):
+    """Modes 0 (default) and 2 are the reference's arithmetic bit for bit:
+    bytes, iterations, syndromes and the posteriors' bits (sign of zero too)
+    equal the oracle's on every frame.  Mode 3 (F64_FAST, compact tanh/log
+    within 3 ulp of glibc) is not exact: on these frames -- a quarter of
+    their samples exactly 0, posteriors near 0 for 50 iterations -- its last
+    bits grow into decisions on 2 of 576 frames (126 and 376) at 50
+    iterations (profiles/round2/signed_zero_probe.txt); pinned here so a
+    change in either mode shows."""
     import ldpc_ece535a
     sys.path.insert(0, REPO)
     from oracle import oracle as orc
@@ -48,21 +56,14 @@ def test_signed_zero_samples(golden, method, prec, mode):
     for iters in (5, 50):
         out = dec.decode(y, method=method, max_iters=iters, precision=prec, want_llr=True)
         ref = orc.decode_batch(method, dec.H, y, iters, nthreads=8, want_post=True)
-        if method == 1 and prec == 0:
-            # The default f64 mode's compact tanh/log (<= 3 ulp of glibc, DESIGN
-            # section 3) is not bit-identical, and these frames -- a quarter of
-            # their samples exactly 0, posteriors near 0 for 50 iterations --
-            # are where ulps grow into decisions: 2 of 576 frames (126, 376)
-            # differ at 50 iterations, identically before and after the zero
-            # seed (profiles/round2/signed_zero_probe.txt).  The libm mode
-            # (prec 2) is exact on all of them.
-            bad = int((out["packed"] != ref["packed"]).any(axis=1).sum())
-            assert bad <= (0 if iters == 5 else 4), bad
+        if method == 1 and prec == 3:
+            bad = np.flatnonzero((out["packed"] != ref["packed"]).any(axis=1))
+            assert len(bad) <= (0 if iters == 5 else 4), bad
             continue
         np.testing.assert_array_equal(out["packed"], ref["packed"])
         np.testing.assert_array_equal(out["iters"], ref["iters"])
         np.testing.assert_array_equal(out["synd"], ref["synd"])
-        if method == 0:
-            # min-sum posteriors are exact: compare bit patterns (sign of zero too)
-            np.testing.assert_array_equal(out["llr"].view(np.uint32),
-                                          ref["post"].view(np.uint32))
+        # posteriors (float of the f64 sums): bit patterns, NaN == NaN
+        a, b = out["llr"], ref["post"]
+        same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+        assert same.all(), np.argwhere(~same)[:5]
