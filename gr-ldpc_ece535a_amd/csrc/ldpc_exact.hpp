@@ -186,12 +186,15 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n]) {
   int k[n];
 #pragma unroll
   for (int i = 0; i < n; ++i) {
-    const uint32_t hx = hiw(u[i]) & 0x7fffffffu;
-    const bool neg = u[i] < 0.0;
-    // (int)(invln2 * u + (u > 0 ? 0.5 : -0.5)): truncation toward zero
-    const double kg = __builtin_trunc(invln2 * u[i] + (neg ? -0.5 : 0.5));
-    double tk = hx < 0x3FF0A2B2u ? (neg ? -1.0 : 1.0) : kg;
-    tk = hx > 0x3fd62e42u ? tk : 0.0;
+    const uint32_t hw = hiw(u[i]);
+    const uint32_t hx = hw & 0x7fffffffu, sgn = hw & 0x80000000u;
+    // k = (int)(invln2 * u + (u > 0 ? 0.5 : -0.5)), truncation toward zero;
+    // |k| <= 63 here, so the integral double has a zero low word and the
+    // three-way choice of k is made on high words
+    const double kg = __builtin_trunc(invln2 * u[i] + from_hi(0x3fe00000u | sgn));
+    uint32_t th = hx < 0x3FF0A2B2u ? (0x3ff00000u | sgn) : hiw(kg);  // +-1 below 1.5 ln2
+    th = hx > 0x3fd62e42u ? th : 0u;                                  // 0 up to 0.5 ln2
+    const double tk = from_hi(th);
     k[i] = (int)tk;
     const double hi = fma_(-tk, ln2_hi, u[i]);  // tk * ln2_hi is exact (|k| <= 64)
     const double lo = tk * ln2_lo;
@@ -218,17 +221,13 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n]) {
     const double d = ep[i] - x[i];
     const int kk = k[i];
     // per-lane constants (high words; every low word is zero)
-    const uint32_t sh = (uint32_t)(0x3ff + kk) << 20;  // 2^k
-    const int kc = kk < 1 ? 1 : (kk > 19 ? 19 : kk);
-    uint32_t ah = 0x3ff00000u - (0x200000u >> kc);     // 1 - 2^-k
-    ah = kk > 19 ? 0x3ff00000u : ah;                   // k > 56 (the 20..56 lanes redo below)
-    ah = kk <= -2 ? 0x3ff00000u : ah;                  // 1
-    ah = (kk == 0 || kk == -1) ? 0u : ah;              // 0
-    uint32_t bh = kk <= -2 ? 0xbff00000u : 0x80000000u;  // -1 / -0
-    bh = kk > 56 ? 0xbff00000u : bh;
-    bh = kk == -1 ? 0xbfe00000u : bh;                  // -0.5
+    const uint32_t sh = (uint32_t)(0x3ff + kk) << 20;                  // 2^k
+    uint32_t ah = 0x3ff00000u - (0x200000u >> (kk & 31));              // 1 - 2^-k (k = 2..19),
+    ah = (uint32_t)(kk + 1) <= 1u ? 0u : ah;                           // 1 (k <= -2, 22..63), 0 (k = 0, -1)
+    uint32_t bh = (uint32_t)kk <= 56u ? 0x80000000u : 0xbff00000u;   // -0 (k = 0..56) / -1
+    bh = kk == -1 ? 0xbfe00000u : bh;                                  // -0.5
     t[i] = fma_(from_hi(ah) - d, from_hi(sh), from_hi(bh));
-    any_mid |= kk >= 20 && kk <= 56;
+    any_mid |= (uint32_t)(kk - 20) <= 36u;
   }
   if (LDPC_EX_ANY(any_mid)) {
 #pragma unroll
@@ -238,7 +237,7 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n]) {
       const double tm = from_hi((uint32_t)(0x3ff - km) << 20);  // 2^-k
       const double y = (x[i] - (ep[i] + tm)) + 1.0;
       const double v = y * from_hi((uint32_t)(0x3ff + km) << 20);
-      t[i] = (kk >= 20 && kk <= 56) ? v : t[i];
+      t[i] = (uint32_t)(kk - 20) <= 36u ? v : t[i];
     }
   }
 }
@@ -255,33 +254,45 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n]) {
 // ---------------------------------------------------------------------------
 template <int n>
 LDPC_HD void tanh_half_n(const double (&m)[n], double (&z)[n]) {
+  static_assert(n <= 8, "the tanh divisors (up to 2^63 each) share one prefix product");
   double u[n], t[n], num[n], den[n], q[n], x[n];
-  uint32_t ix[n];
+  uint32_t hx[n];
+  bool special = false;
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     x[i] = m[i] * 0.5;
-    ix[i] = hiw(x[i]) & 0x7fffffffu;
-    const double a = __builtin_fabs(x[i]);
-    const bool ok = ix[i] < 0x40360000u && ix[i] >= 0x3c800000u;
-    const bool big = ix[i] >= 0x3ff00000u;
-    u[i] = ok ? (big ? 2.0 * a : -2.0 * a) : -1.0;
+    hx[i] = hiw(x[i]);
+    const uint32_t ix = hx[i] & 0x7fffffffu;
+    // |x| clamped into [2^-55, 21.5] (NaN -> 2^-55): lanes outside glibc's
+    // expm1 range are replaced below, and any |x| >= 19.1 gives exactly 1,
+    // as glibc's 1 - tiny for |x| >= 22 (2 / (expm1(2|x|) + 2) < 2^-54)
+    const double ac = __builtin_fmin(__builtin_fmax(__builtin_fabs(x[i]), 0x1p-55), 21.5);
+    // u = 2|x| for |x| >= 1, else -2|x|: the sign bit of ix - 0x3ff00000
+    u[i] = dbl(bits(2.0 * ac) ^ ((uint64_t)((ix - 0x3ff00000u) & 0x80000000u) << 32));
+    special |= ix - 0x3c800000u >= 0x7ff00000u - 0x3c800000u;  // |x| < 2^-55, inf, NaN
   }
   expm1_n<n>(u, t);
 #pragma unroll
   for (int i = 0; i < n; ++i) {
-    const bool big = ix[i] >= 0x3ff00000u;
+    const bool big = (hx[i] & 0x7fffffffu) >= 0x3ff00000u;
     num[i] = big ? 2.0 : -t[i];
     den[i] = t[i] + 2.0;
   }
   div_n<n>(num, den, q);
 #pragma unroll
   for (int i = 0; i < n; ++i) {
-    const bool big = ix[i] >= 0x3ff00000u;
-    double r = big ? 1.0 - q[i] : q[i];
-    r = ix[i] < 0x40360000u ? r : 1.0;
-    r = (int32_t)hiw(x[i]) >= 0 ? r : -r;
-    r = ix[i] < 0x3c800000u ? x[i] * (1.0 + x[i]) : r;
-    z[i] = x[i] != x[i] ? x[i] + x[i] : r;
+    const bool big = (hx[i] & 0x7fffffffu) >= 0x3ff00000u;
+    const double r = big ? 1.0 - q[i] : q[i];  // >= 0: the sign is x's
+    z[i] = dbl(bits(r) | ((uint64_t)(hx[i] & 0x80000000u) << 32));
+  }
+  if (LDPC_EX_ANY(special)) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const uint32_t ix = hx[i] & 0x7fffffffu;
+      // glibc: x (1 + x) below 2^-55 (x itself at +-0); 1/x +- 1 for NaN
+      // (NaN) and +-inf (+-1, as computed above)
+      z[i] = ix < 0x3c800000u ? x[i] * (1.0 + x[i]) : (x[i] != x[i] ? x[i] + x[i] : z[i]);
+    }
   }
 }
 
@@ -336,20 +347,16 @@ LDPC_HD double log_near1(double q) {
   return fma_(poly, r3, lo2) + hi;
 }
 
-LDPC_HD bool log_is_near1(double q) {
-  return bits(q) - 0x3fee000000000000ull < 0x3ff1090000000000ull - 0x3fee000000000000ull;
-}
+// bits(q) - bits(1 - 2^-4) < bits(1 + 0x1.09p-4) - bits(1 - 2^-4): both bounds
+// have zero low words, so the high word decides
+LDPC_HD bool log_is_near1(double q) { return hiw(q) - 0x3fee0000u < 0x3ff10900u - 0x3fee0000u; }
 
-// log(q) on the decoder's domain (see above)
+// log(q) for q normal in [2^-60, 2^60] (the decoder's open ratios)
 LDPC_HD double log_q(double q, const GlLogEntry *tab) {
   double y = log_main(q, tab);
   const bool near = log_is_near1(q);
   if (LDPC_EX_ANY(near)) y = near ? log_near1(q) : y;
-  // +0 -> -inf, +inf -> +inf, NaN -> NaN (the main path's lanes for these
-  // read some table entry and are replaced)
-  const uint32_t top = hiw(q);
-  y = top >= 0x7ff00000u ? q : y;
-  return q == 0.0 ? -__builtin_inf() : y;
+  return y;
 }
 
 // glibc's log on every double (host reference for the tests)
@@ -374,20 +381,26 @@ inline double log_glibc(double x, const GlLogEntry *tab) {
 // ---------------------------------------------------------------------------
 template <int n>
 LDPC_HD void log_ratio_n(const double (&T)[n], const GlLogEntry *tab, double (&E)[n]) {
+  static_assert(n <= 16, "the divisors (>= 2^-53 each) share one prefix product");
   double num[n], den[n], q[n];
-  bool open[n];
+  bool special = false;
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     num[i] = 1.0 + T[i];
-    const double d = 1.0 - T[i];
-    open[i] = d > 0.0;  // false: T == 1 (2/0 = +inf) or NaN
-    den[i] = open[i] ? d : 1.0;
+    // 1 - T >= 2^-53 unless T = 1 or NaN: those divide by 2^-60 here (a
+    // finite quotient in the shared product) and are replaced below
+    den[i] = __builtin_fmax(1.0 - T[i], 0x1p-60);
+    special |= !(__builtin_fabs(T[i]) < 1.0);  // T = +-1 (2/0, 0/2) or NaN
   }
   div_n<n>(num, den, q);
 #pragma unroll
-  for (int i = 0; i < n; ++i) {
-    const double qq = open[i] ? q[i] : (T[i] != T[i] ? T[i] : __builtin_inf());
-    E[i] = log_q(qq, tab);
+  for (int i = 0; i < n; ++i) E[i] = log_q(q[i], tab);
+  if (LDPC_EX_ANY(special)) {
+#pragma unroll
+    for (int i = 0; i < n; ++i)  // log(2/0) = +inf, log(0/2) = -inf, NaN -> NaN
+      E[i] = __builtin_fabs(T[i]) < 1.0 ? E[i]
+                                         : (T[i] != T[i] ? T[i] + T[i]
+                                                         : __builtin_copysign(__builtin_inf(), T[i]));
   }
 }
 

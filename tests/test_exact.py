@@ -83,9 +83,10 @@ def test_log_bit_identical(ec):
     for x in sets:
         mism, maxu = _call(ec.check_log, x, mode=0)
         assert mism == 0, (mism, maxu)
-    # the decoder's form on its own domain: {0} U normal [2^-60, 2^60] U {inf, NaN}
-    for x in sets[:4] + [np.array([0.0, np.inf, np.nan, 2.0 ** -60, 2.0 ** 60])]:
-        x = x[(x == 0) | (x != x) | (x == np.inf) | ((x >= 2.0 ** -60) & (x <= 2.0 ** 60))]
+    # the decoder's form on its own domain: normal [2^-60, 2^60] (log_ratio_n
+    # handles T = +-1 / NaN, i.e. ratios 0 / inf / NaN, itself)
+    for x in sets[:4] + [np.array([2.0 ** -60, 2.0 ** 60, 1.0])]:
+        x = x[(x >= 2.0 ** -60) & (x <= 2.0 ** 60)]
         assert _call(ec.check_log, x, mode=1)[0] == 0
 
 
@@ -134,8 +135,8 @@ def test_log_ratio_bit_identical(ec):
 @pytest.mark.parametrize("perturb", [0, 1, -1, 3, -3, 8, -8, 1 << 20, -(1 << 22)])
 def test_batched_division_is_ieee(ec, perturb):
     """div_n<k> for k = 1..3 equals a / b with the shared reciprocal seed off
-    by `perturb` ulp: the per-quotient Newton step and residual correction
-    make the result independent of the seed's last bits.  Operands: the
+    by `perturb` ulp (up to 2^22): the residual correction and the exact
+    residual test make the result independent of the seed's last bits.  Operands: the
     three divisions of the sum-product pass (expm1's (r1 - t) / (6 - x t) ~
     O(1), tanh's -t/(t+2) or 2/(t+2), (1+T)/(1-T) down to 2^-53) and
     significands with long runs of ones / zeros (the hard cases of division)."""
