@@ -102,8 +102,9 @@ LDPC_HD double rcp_seed(double p) {
 //     except below a power of two, where the gap halves.  The common path
 //     tests |r1| against the smaller of the two (the gap below q1:
 //     bits(q1) - 1's exponent): exact for every q1 but a power of two, where
-//     it can only over-report; any lane it flags is settled with the right h
-//     in a branch the wave takes only then, and moves one ulp.
+//     it can only over-report (so can the high-word shortcut for it, on
+//     q1 within 2^-20 of a power of two); any lane it flags is settled with
+//     the right h in a branch the wave takes only then, and moves one ulp.
 // Domain: a, b normal (or a = +-0), a / b normal, all far from
 // over/underflow (|exponents| < 900).
 LDPC_HD double div_core(double a, double b, double y) {
@@ -111,13 +112,16 @@ LDPC_HD double div_core(double a, double b, double y) {
   const double r = fma_(-b, q0, a);
   double q1 = fma_(r, y, q0);
   const double r1 = fma_(-b, q1, a);  // exact
-  const uint32_t hb = (uint32_t)((bits(q1) - 1) >> 32) & 0x7ff00000u;
-  const double h_lo = from_hi(hb - (53u << 20));  // half the gap below q1
+  // half the gap below q1, or half of that when q1's high-word significand
+  // is zero (a power of two, or within 2^-20 of one: those may be flagged
+  // needlessly, never missed)
+  const double h_lo = from_hi(((hiw(q1) - 1u) & 0x7ff00000u) - (53u << 20));
   const bool flag = fma_(-__builtin_fabs(b), h_lo, __builtin_fabs(r1)) > 0.0;
   if (LDPC_EX_ANY(flag)) {
     // a/b is on q1's zero side iff r1 / b and q1 differ in sign
     const bool down = ((hiw(r1) ^ hiw(b) ^ hiw(q1)) & 0x80000000u) != 0;
-    const double h = down ? h_lo : from_hi((hiw(q1) & 0x7ff00000u) - (53u << 20));
+    const uint32_t e = down ? (uint32_t)((bits(q1) - 1) >> 32) : hiw(q1);  // exact gap side
+    const double h = from_hi((e & 0x7ff00000u) - (53u << 20));
     const bool wrong = fma_(-__builtin_fabs(b), h, __builtin_fabs(r1)) > 0.0;
     q1 = wrong ? dbl(bits(q1) + (down ? ~0ull : 1ull)) : q1;
   }
@@ -313,7 +317,8 @@ LDPC_HD double log_main(double q, const GlLogEntry *tab) {
   const uint32_t th = (uint32_t)(ix >> 32) - 0x3fe60000u;  // high word of ix - OFF
   const uint32_t i = (th >> (20 - kGlTabBits)) & ((1u << kGlTabBits) - 1);
   const int k = (int32_t)th >> 20;
-  const uint64_t iz = ix - ((uint64_t)(th & 0xfff00000u) << 32);
+  // iz = ix - (tmp & 0xfff << 52): only the high word changes
+  const uint64_t iz = ((uint64_t)((uint32_t)(ix >> 32) - (th & 0xfff00000u)) << 32) | (uint32_t)ix;
   const GlLogEntry e = tab[i];
   const double z = dbl(iz);
   const double r = fma_(z, e.invc, -1.0);

@@ -1180,6 +1180,9 @@ static int launch_mw_slots(const CodeView &code, const DecodeArgs &a, int slots,
   }
 }
 
+#ifndef LDPC_TP_MINB
+#define LDPC_TP_MINB 4  // throughput build: waves per SIMD the register budget allows
+#endif
 template <int PREC, int METHOD, int NW>
 static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots, hipStream_t st) {
   // low-degree codes (dc <= 6, dv <= 3: the reference's H) with one column
@@ -1189,8 +1192,8 @@ static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots, hi
       // throughput mode (no issue-priority management): the 4-waves-per-SIMD build
       if constexpr ((PREC == 0 || PREC == 3) && METHOD == 1)
         if (a.fair_cycles == 0) switch (slots) {
-            case 3: return launch_one<PREC, METHOD, 3, NW, 5, 3, 4>(code, a, st);
-            case 4: return launch_one<PREC, METHOD, 4, NW, 5, 3, 4>(code, a, st);
+            case 3: return launch_one<PREC, METHOD, 3, NW, 5, 3, LDPC_TP_MINB>(code, a, st);
+            case 4: return launch_one<PREC, METHOD, 4, NW, 5, 3, LDPC_TP_MINB>(code, a, st);
             default: break;
           }
       switch (slots) {

@@ -20,9 +20,12 @@ for defs in "$@"; do
     make -s -j8 -C "$src" hip OUT="$root/ab/V$i/lib"
     git -C "$root" worktree remove --force /tmp/ab_wt
   else
+    # "<defines>|<make variables>", e.g. "-DLDPC_TP_MINB=3" or "|SMALL_SCHED="
+    mvars=""
+    if [[ "$defs" == *"|"* ]]; then mvars=${defs#*|}; fi
     cp -r "$src/ldpc_ece535a" "$root/ab/V$i/"
-    make -s -j8 -C "$src" hip OUT="$root/ab/V$i/lib" \
-      HIPFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wall $defs"
+    make -s -j8 -C "$src" hip OUT="$root/ab/V$i/lib" $mvars \
+      HIPFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wall ${defs%%|*}"
   fi
   echo "V$i: $defs" >> "$root/ab/variants.txt"
 done
