@@ -29,29 +29,31 @@ namespace ldpc {
 template <int PREC>
 struct Math;
 
-__device__ const ex::GlLogEntry kGlLogTab[1 << ex::kGlTabBits] = {LDPC_GLIBC_LOG_TAB};
+// glibc's log table and expm1's per-k constants (ldpc_exact.hpp)
+__device__ const ex::ExTab kExTab = ex::make_ex_tab();
 // The 512-entry table of LDPC_PREC_F64_FAST's log (ldpc_logtab.hpp).
 __device__ const fm::LogTabEntry kLogTab[1 << fm::kLogTabBits] = {LDPC_LOGTAB_ENTRIES};
 
 template <>
 struct Math<0> {
   typedef double Real;
-  typedef ex::GlLogEntry Tab;
-  static constexpr int kTabN = 1 << ex::kGlTabBits;
-  static __device__ __forceinline__ const Tab *tab_src() { return kGlLogTab; }
+  typedef ex::ExTab Tab;
+  static constexpr int kTabN = 1;
+  static __device__ __forceinline__ const Tab *tab_src() { return &kExTab; }
   template <int n>
-  static __device__ __forceinline__ void tanh_half_n(const double (&m)[n], double (&z)[n]) {
-    ex::tanh_half_n<n>(m, z);
+  static __device__ __forceinline__ void tanh_half_n(const double (&m)[n], double (&z)[n],
+                                                     const Tab *tab) {
+    ex::tanh_half_n<n>(m, z, tab);
   }
   template <int n>
   static __device__ __forceinline__ void check_msg_n(const double (&T)[n], const Tab *tab,
                                                      double (&E)[n]) {
     ex::log_ratio_n<n>(T, tab, E);
   }
-  static __device__ __forceinline__ double tanh_half(double m) {
+  static __device__ __forceinline__ double tanh_half(double m, const Tab *tab) {
     const double v[1] = {m};
     double z[1];
-    ex::tanh_half_n<1>(v, z);
+    ex::tanh_half_n<1>(v, z, tab);
     return z[0];
   }
   static __device__ __forceinline__ double check_msg(double T, const Tab *tab) {
@@ -66,9 +68,10 @@ struct Math<0> {
 template <>
 struct Math<2> : Math<0> {
   template <int n>
-  static __device__ __forceinline__ void tanh_half_n(const double (&m)[n], double (&z)[n]) {
+  static __device__ __forceinline__ void tanh_half_n(const double (&m)[n], double (&z)[n],
+                                                     const Tab *tab) {
 #pragma unroll
-    for (int i = 0; i < n; ++i) z[i] = Math<0>::tanh_half(m[i]);
+    for (int i = 0; i < n; ++i) z[i] = Math<0>::tanh_half(m[i], tab);
   }
   template <int n>
   static __device__ __forceinline__ void check_msg_n(const double (&T)[n], const Tab *tab,
@@ -84,15 +87,20 @@ struct Math<3> {
   static constexpr int kTabN = 1 << fm::kLogTabBits;
   static __device__ __forceinline__ const Tab *tab_src() { return kLogTab; }
 #ifdef LDPC_TANH_SINGLE_RANGE  // A/B only: loses accuracy on large-amplitude frames
-  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_fast(m); }
+  static __device__ __forceinline__ double tanh_half(double m, const Tab * = nullptr) {
+    return fm::tanh_half_fast(m);
+  }
 #else
-  static __device__ __forceinline__ double tanh_half(double m) { return fm::tanh_half_acc(m); }
+  static __device__ __forceinline__ double tanh_half(double m, const Tab * = nullptr) {
+    return fm::tanh_half_acc(m);
+  }
 #endif
   static __device__ __forceinline__ double check_msg(double T, const Tab *tab) {
     return fm::log_ratio_tab(T, tab);
   }
   template <int n>
-  static __device__ __forceinline__ void tanh_half_n(const double (&m)[n], double (&z)[n]) {
+  static __device__ __forceinline__ void tanh_half_n(const double (&m)[n], double (&z)[n],
+                                                     const Tab *) {
 #pragma unroll
     for (int i = 0; i < n; ++i) z[i] = tanh_half(m[i]);
   }
@@ -111,12 +119,15 @@ struct Math<1> {
   typedef float Tab;  // no table
   static constexpr int kTabN = 0;
   static __device__ __forceinline__ const Tab *tab_src() { return nullptr; }
-  static __device__ __forceinline__ float tanh_half(float m) { return ::tanhf(m / 2.0f); }
+  static __device__ __forceinline__ float tanh_half(float m, const Tab * = nullptr) {
+    return ::tanhf(m / 2.0f);
+  }
   static __device__ __forceinline__ float check_msg(float T, const Tab *) {
     return ::logf((1.0f + T) / (1.0f - T));
   }
   template <int n>
-  static __device__ __forceinline__ void tanh_half_n(const float (&m)[n], float (&z)[n]) {
+  static __device__ __forceinline__ void tanh_half_n(const float (&m)[n], float (&z)[n],
+                                                     const Tab *) {
 #pragma unroll
     for (int i = 0; i < n; ++i) z[i] = tanh_half(m[i]);
   }
@@ -130,6 +141,54 @@ struct Math<1> {
   static __device__ __forceinline__ float max_() { return FLT_MAX; }
 };
 
+// log_ratio_n with glibc's |q - 1| < 1/16 path evaluated once per 64 such
+// ratios of the wave instead of once per slot that has any: about a fifth of
+// the check messages take that path in steady state, so with per-slot
+// branches every slot would run both paths.  The near-1 ratios are packed
+// (ballot + mbcnt prefix) into `scratch` -- this wave's LDS, >= 64 n
+// doubles, free for the duration of the call --, evaluated densely, and read
+// back by their lanes.  Same functions, same results as ex::log_ratio_n.
+// A wave's LDS accesses execute in issue order, so only the compiler must be
+// kept from reordering them (the empty asm with a memory clobber).
+template <int n>
+__device__ __forceinline__ void log_ratio_n_packed(const double (&T)[n],
+                                                   const ex::ExTab *tab, double (&E)[n],
+                                                   double *scratch, int lane) {
+  double q[n];
+  const bool special = ex::ratio_n<n>(T, q);
+  uint32_t pos[n];
+  bool near[n];
+  uint32_t base = 0;  // wave-uniform
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    E[i] = ex::log_main(q[i], tab->log);
+    near[i] = ex::log_is_near1(q[i]);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(near[i]);
+    pos[i] = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    base += (uint32_t)__builtin_popcountll(m);
+  }
+  if (base != 0) {
+#pragma unroll
+    for (int i = 0; i < n; ++i)
+      if (near[i]) scratch[pos[i]] = q[i];
+    asm volatile("" ::: "memory");
+    for (uint32_t p = 0; p < base; p += 64) {
+      const uint32_t idx = p + (uint32_t)lane;
+      if (idx < base) scratch[idx] = ex::log_near1(scratch[idx]);
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < n; ++i)
+      if (near[i]) E[i] = scratch[pos[i]];
+    asm volatile("" ::: "memory");
+  }
+  if (__builtin_amdgcn_ballot_w64(special) != 0) {
+    LDPC_EX_COLD();
+    ex::ratio_fix_n<n>(T, E);
+  }
+}
+
 // LDS copy of mode PREC's log table (sized 1 for modes without one); every
 // thread of the block takes part, one __syncthreads.
 template <int PREC>
@@ -140,8 +199,12 @@ struct TabLds {
 template <int PREC>
 __device__ __forceinline__ void stage_tab(typename Math<PREC>::Tab *lds) {
   if constexpr (Math<PREC>::kTabN > 0) {
-    const typename Math<PREC>::Tab *src = Math<PREC>::tab_src();
-    for (int i = threadIdx.x; i < Math<PREC>::kTabN; i += blockDim.x) lds[i] = src[i];
+    typedef typename Math<PREC>::Tab Tab;
+    static_assert(sizeof(Tab) % 4 == 0, "tables are copied in 32-bit words");
+    constexpr int words = (int)(sizeof(Tab) / 4) * Math<PREC>::kTabN;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(Math<PREC>::tab_src());
+    uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
+    for (int i = threadIdx.x; i < words; i += blockDim.x) dst[i] = src[i];
     __syncthreads();
   }
 }

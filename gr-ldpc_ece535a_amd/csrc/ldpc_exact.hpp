@@ -51,8 +51,13 @@
 #if defined(__HIP_DEVICE_COMPILE__)
 // wave-uniform "does any lane need this": the region is skipped otherwise
 #define LDPC_EX_ANY(c) (__builtin_amdgcn_ballot_w64(c) != 0)
+// first statement of such a rare region: an empty volatile asm cannot be
+// speculated, so the compiler keeps the branch instead of if-converting it
+// into selects evaluated on every iteration
+#define LDPC_EX_COLD() asm volatile(";ldpc_cold")
 #else
 #define LDPC_EX_ANY(c) (c)
+#define LDPC_EX_COLD() ((void)0)
 #endif
 
 namespace ldpc {
@@ -88,7 +93,7 @@ LDPC_HD double rcp_seed(double p) {
 #endif
 }
 
-// a / b, correctly rounded, from y ~ 1/b (relative error << 2^-30).
+// a / b, correctly rounded, from y ~ 1/b (relative error < 2^-45).
 //  1. q0 = a y; r = fma(-b, q0, a); q1 = fma(r, y, q0).  q1 - a/b =
 //     (a/b - q0)(b y - 1) + rounding: q1 is within 1/2 ulp + 2^-40 ulp of
 //     a/b, i.e. faithful -- and RN(a/b) unless a/b lies within 2^-40 ulp of
@@ -96,31 +101,33 @@ LDPC_HD double rcp_seed(double p) {
 //     a = 1, b = 1 - 2^-53 with y = 1 gives 1 instead of 1 + 2^-52).
 //  2. The decision is then made exactly.  For faithful q1 the residual
 //     r1 = a - b q1 is a double, so fma(-b, q1, a) is exact, and
-//     a/b - q1 = r1 / b.  RN(a/b) = q1 iff |r1| < |b| h, h = half the gap to
-//     q1's neighbour on a/b's side (a quotient of two doubles is never a
-//     midpoint, so there are no ties).  h = 2^(e-53) for q1 in [2^e, 2^e+1),
-//     except below a power of two, where the gap halves.  The common path
-//     tests |r1| against the smaller of the two (the gap below q1:
-//     bits(q1) - 1's exponent): exact for every q1 but a power of two, where
-//     it can only over-report (so can the high-word shortcut for it, on
-//     q1 within 2^-20 of a power of two); any lane it flags is settled with
-//     the right h in a branch the wave takes only then, and moves one ulp.
+//     a/b - q1 = r1 / b.  RN(a/b) = q1 iff |r1 / b| is below half the gap
+//     to q1's neighbour on a/b's side (a quotient of two doubles is never a
+//     midpoint, so there are no ties).  The common path tests that with one
+//     fma, q1 + r1 y (1 + 2^-40) rounding back to q1 (see below): a sure
+//     pass, or a flag raised only within 2^-39 of a midpoint; a flagged lane
+//     is settled from the exact gap, h = 2^(e-53) for q1 in [2^e, 2^e+1)
+//     (halved below a power of two), in a branch the wave takes only then.
 // Domain: a, b normal (or a = +-0), a / b normal, all far from
 // over/underflow (|exponents| < 900).
 LDPC_HD double div_core(double a, double b, double y) {
   const double q0 = a * y;
   const double r = fma_(-b, q0, a);
   double q1 = fma_(r, y, q0);
-  const double r1 = fma_(-b, q1, a);  // exact
-  // half the gap below q1, or half of that when q1's high-word significand
-  // is zero (a power of two, or within 2^-20 of one: those may be flagged
-  // needlessly, never missed)
-  const double h_lo = from_hi(((hiw(q1) - 1u) & 0x7ff00000u) - (53u << 20));
-  const bool flag = fma_(-__builtin_fabs(b), h_lo, __builtin_fabs(r1)) > 0.0;
+  const double r1 = fma_(-b, q1, a);  // exact: a/b = q1 + r1/b
+  // t' = r1 yk with yk = y (1 + 2^-40), |b yk| in (1 + 2^-41, 1 + 2^-39)
+  // (y's relative error is below 2^-45): t' has r1/b's sign and a larger
+  // magnitude, so RN(q1 + t') == q1 implies |r1/b| < |t'| <= half the gap
+  // on that side (the addition itself takes the smaller gap below a power
+  // of two), i.e. RN(a/b) == q1.  Anything else is flagged.
+  const double yk = y * (1.0 + 0x1p-40);
+  const bool flag = fma_(r1, yk, q1) != q1;
   if (LDPC_EX_ANY(flag)) {
-    // a/b is on q1's zero side iff r1 / b and q1 differ in sign
+    LDPC_EX_COLD();
+    // exact decision: a/b is on q1's zero side iff r1 / b and q1 differ in
+    // sign; h = half the gap on that side (below a power of two it halves)
     const bool down = ((hiw(r1) ^ hiw(b) ^ hiw(q1)) & 0x80000000u) != 0;
-    const uint32_t e = down ? (uint32_t)((bits(q1) - 1) >> 32) : hiw(q1);  // exact gap side
+    const uint32_t e = down ? (uint32_t)((bits(q1) - 1) >> 32) : hiw(q1);
     const double h = from_hi((e & 0x7ff00000u) - (53u << 20));
     const bool wrong = fma_(-__builtin_fabs(b), h, __builtin_fabs(r1)) > 0.0;
     q1 = wrong ? dbl(bits(q1) + (down ? ~0ull : 1ull)) : q1;
@@ -147,6 +154,31 @@ LDPC_HD void div_n(const double (&a)[n], const double (&b)[n], double (&q)[n]) {
     q[i] = div_core(a[i], b[i], inv);
   }
   q[0] = div_core(a[0], b[0], y);
+}
+
+// Per-k constants of expm1's result formula (below): high words of A and B
+// (their low words are zero), for k in [kTailLo, kTailLo + kTailN).
+struct TailEntry {
+  uint32_t a_hi, b_hi;
+};
+constexpr int kTailLo = -3, kTailN = 68;  // k = -3 .. 64
+constexpr TailEntry tail_entry(int k) {
+  return TailEntry{(k == 0 || k == -1) ? 0u                                            // A = 0
+                   : (k >= 2 && k <= 19) ? 0x3ff00000u - (0x200000u >> k)              // 1 - 2^-k
+                                         : 0x3ff00000u,                                // 1
+                   k == -1 ? 0xbfe00000u                                               // B = -0.5
+                   : (k >= 0 && k <= 56) ? 0x80000000u                                 // -0
+                                         : 0xbff00000u};                               // -1
+}
+// Everything the exact functions look up: glibc's log table and the tails.
+struct ExTab {
+  GlLogEntry log[1 << kGlTabBits];
+  TailEntry tail[kTailN];
+};
+constexpr ExTab make_ex_tab() {
+  ExTab t{{LDPC_GLIBC_LOG_TAB}, {}};
+  for (int k = kTailLo; k < kTailLo + kTailN; ++k) t.tail[k - kTailLo] = tail_entry(k);
+  return t;
 }
 
 // ---------------------------------------------------------------------------
@@ -177,7 +209,7 @@ LDPC_HD void div_n(const double (&a)[n], const double (&b)[n], double (&q)[n]) {
 // Everything else is glibc's operation sequence, unchanged.
 // ---------------------------------------------------------------------------
 template <int n>
-LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n]) {
+LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n], const TailEntry *tail) {
   constexpr double ln2_hi = 6.93147180369123816490e-01;
   constexpr double ln2_lo = 1.90821492927058770002e-10;
   constexpr double invln2 = 1.44269504088896338700e+00;
@@ -224,16 +256,15 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n]) {
     ep[i] = (x[i] * (e - c[i]) - c[i]) - hxs[i];
     const double d = ep[i] - x[i];
     const int kk = k[i];
-    // per-lane constants (high words; every low word is zero)
-    const uint32_t sh = (uint32_t)(0x3ff + kk) << 20;                  // 2^k
-    uint32_t ah = 0x3ff00000u - (0x200000u >> (kk & 31));              // 1 - 2^-k (k = 2..19),
-    ah = (uint32_t)(kk + 1) <= 1u ? 0u : ah;                           // 1 (k <= -2, 22..63), 0 (k = 0, -1)
-    uint32_t bh = (uint32_t)kk <= 56u ? 0x80000000u : 0xbff00000u;   // -0 (k = 0..56) / -1
-    bh = kk == -1 ? 0xbfe00000u : bh;                                  // -0.5
-    t[i] = fma_(from_hi(ah) - d, from_hi(sh), from_hi(bh));
+    // per-lane constants (high words; every low word is zero): 2^k, and A, B
+    // from the table (tail_entry)
+    const uint32_t sh = (uint32_t)(0x3ff + kk) << 20;
+    const TailEntry te = tail[kk - kTailLo];
+    t[i] = fma_(from_hi(te.a_hi) - d, from_hi(sh), from_hi(te.b_hi));
     any_mid |= (uint32_t)(kk - 20) <= 36u;
   }
   if (LDPC_EX_ANY(any_mid)) {
+    LDPC_EX_COLD();
 #pragma unroll
     for (int i = 0; i < n; ++i) {
       const int kk = k[i];
@@ -257,45 +288,49 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n]) {
 // range feed it a dummy argument and are selected away.
 // ---------------------------------------------------------------------------
 template <int n>
-LDPC_HD void tanh_half_n(const double (&m)[n], double (&z)[n]) {
+LDPC_HD void tanh_half_n(const double (&m)[n], double (&z)[n], const ExTab *tab) {
   static_assert(n <= 8, "the tanh divisors (up to 2^63 each) share one prefix product");
-  double u[n], t[n], num[n], den[n], q[n], x[n];
-  uint32_t hx[n];
+  double u[n], t[n], num[n], den[n], q[n];
+  uint32_t hm[n];
   bool special = false;
 #pragma unroll
   for (int i = 0; i < n; ++i) {
-    x[i] = m[i] * 0.5;
-    hx[i] = hiw(x[i]);
-    const uint32_t ix = hx[i] & 0x7fffffffu;
-    // |x| clamped into [2^-55, 21.5] (NaN -> 2^-55): lanes outside glibc's
-    // expm1 range are replaced below, and any |x| >= 19.1 gives exactly 1,
-    // as glibc's 1 - tiny for |x| >= 22 (2 / (expm1(2|x|) + 2) < 2^-54)
-    const double ac = __builtin_fmin(__builtin_fmax(__builtin_fabs(x[i]), 0x1p-55), 21.5);
-    // u = 2|x| for |x| >= 1, else -2|x|: the sign bit of ix - 0x3ff00000
-    u[i] = dbl(bits(2.0 * ac) ^ ((uint64_t)((ix - 0x3ff00000u) & 0x80000000u) << 32));
-    special |= ix - 0x3c800000u >= 0x7ff00000u - 0x3c800000u;  // |x| < 2^-55, inf, NaN
+    // x = m / 2 and glibc's expm1 argument +-2|x| = +-|m| (exact: m / 2 is
+    // exact for |m| >= 2^-1021; smaller m are special below), so the
+    // thresholds on |x| are thresholds on |m| one binade up
+    hm[i] = hiw(m[i]);
+    const uint32_t im = hm[i] & 0x7fffffffu;
+    // |m| clamped into [2^-54, 43] (NaN -> 2^-54): lanes outside glibc's
+    // expm1 range are replaced below, and any |m| >= 38.2 gives exactly 1,
+    // as glibc's 1 - tiny for |x| >= 22 (2 / (expm1(|m|) + 2) < 2^-54)
+    const double ac = __builtin_fmin(__builtin_fmax(__builtin_fabs(m[i]), 0x1p-54), 43.0);
+    // u = |m| for |x| >= 1, else -|m|: the sign bit of im - bits(2.0)
+    u[i] = dbl(bits(ac) ^ ((uint64_t)((im - 0x40000000u) & 0x80000000u) << 32));
+    special |= im - 0x3c900000u >= 0x7ff00000u - 0x3c900000u;  // |x| < 2^-55, inf, NaN
   }
-  expm1_n<n>(u, t);
+  expm1_n<n>(u, t, tab->tail);
 #pragma unroll
   for (int i = 0; i < n; ++i) {
-    const bool big = (hx[i] & 0x7fffffffu) >= 0x3ff00000u;
+    const bool big = (hm[i] & 0x7fffffffu) >= 0x40000000u;  // |x| >= 1
     num[i] = big ? 2.0 : -t[i];
     den[i] = t[i] + 2.0;
   }
   div_n<n>(num, den, q);
 #pragma unroll
   for (int i = 0; i < n; ++i) {
-    const bool big = (hx[i] & 0x7fffffffu) >= 0x3ff00000u;
-    const double r = big ? 1.0 - q[i] : q[i];  // >= 0: the sign is x's
-    z[i] = dbl(bits(r) | ((uint64_t)(hx[i] & 0x80000000u) << 32));
+    const bool big = (hm[i] & 0x7fffffffu) >= 0x40000000u;
+    const double r = big ? 1.0 - q[i] : q[i];  // >= 0: the sign is x's (m's)
+    z[i] = dbl(bits(r) | ((uint64_t)(hm[i] & 0x80000000u) << 32));
   }
   if (LDPC_EX_ANY(special)) {
+    LDPC_EX_COLD();
 #pragma unroll
     for (int i = 0; i < n; ++i) {
-      const uint32_t ix = hx[i] & 0x7fffffffu;
+      const double x = m[i] * 0.5;
+      const uint32_t ix = hiw(x) & 0x7fffffffu;
       // glibc: x (1 + x) below 2^-55 (x itself at +-0); 1/x +- 1 for NaN
       // (NaN) and +-inf (+-1, as computed above)
-      z[i] = ix < 0x3c800000u ? x[i] * (1.0 + x[i]) : (x[i] != x[i] ? x[i] + x[i] : z[i]);
+      z[i] = ix < 0x3c800000u ? x * (1.0 + x) : (x != x ? x + x : z[i]);
     }
   }
 }
@@ -360,7 +395,10 @@ LDPC_HD bool log_is_near1(double q) { return hiw(q) - 0x3fee0000u < 0x3ff10900u 
 LDPC_HD double log_q(double q, const GlLogEntry *tab) {
   double y = log_main(q, tab);
   const bool near = log_is_near1(q);
-  if (LDPC_EX_ANY(near)) y = near ? log_near1(q) : y;
+  if (LDPC_EX_ANY(near)) {
+    LDPC_EX_COLD();
+    y = near ? log_near1(q) : y;
+  }
   return y;
 }
 
@@ -384,28 +422,44 @@ inline double log_glibc(double x, const GlLogEntry *tab) {
 // otherwise in [2^-54, 2^54] (1 -+ T >= 2^-53), so div_n's domain holds for
 // every lane once T = 1 / NaN lanes divide by 1 and are selected away.
 // ---------------------------------------------------------------------------
+// the quotients (1 + T) / (1 - T) of log_ratio_n; returns whether a lane
+// holds a T of +-1 or NaN (its q is then a placeholder: see ratio_fix_n)
 template <int n>
-LDPC_HD void log_ratio_n(const double (&T)[n], const GlLogEntry *tab, double (&E)[n]) {
+LDPC_HD bool ratio_n(const double (&T)[n], double (&q)[n]) {
   static_assert(n <= 16, "the divisors (>= 2^-53 each) share one prefix product");
-  double num[n], den[n], q[n];
+  double num[n], den[n];
   bool special = false;
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     num[i] = 1.0 + T[i];
     // 1 - T >= 2^-53 unless T = 1 or NaN: those divide by 2^-60 here (a
-    // finite quotient in the shared product) and are replaced below
+    // finite quotient in the shared product) and are replaced by ratio_fix_n
     den[i] = __builtin_fmax(1.0 - T[i], 0x1p-60);
     special |= !(__builtin_fabs(T[i]) < 1.0);  // T = +-1 (2/0, 0/2) or NaN
   }
   div_n<n>(num, den, q);
+  return special;
+}
+
+// E for the T = +-1 / NaN lanes: log(2/0) = +inf, log(0/2) = -inf, NaN
+template <int n>
+LDPC_HD void ratio_fix_n(const double (&T)[n], double (&E)[n]) {
 #pragma unroll
-  for (int i = 0; i < n; ++i) E[i] = log_q(q[i], tab);
+  for (int i = 0; i < n; ++i)
+    E[i] = __builtin_fabs(T[i]) < 1.0
+               ? E[i]
+               : (T[i] != T[i] ? T[i] + T[i] : __builtin_copysign(__builtin_inf(), T[i]));
+}
+
+template <int n>
+LDPC_HD void log_ratio_n(const double (&T)[n], const ExTab *tab, double (&E)[n]) {
+  double q[n];
+  const bool special = ratio_n<n>(T, q);
+#pragma unroll
+  for (int i = 0; i < n; ++i) E[i] = log_q(q[i], tab->log);
   if (LDPC_EX_ANY(special)) {
-#pragma unroll
-    for (int i = 0; i < n; ++i)  // log(2/0) = +inf, log(0/2) = -inf, NaN -> NaN
-      E[i] = __builtin_fabs(T[i]) < 1.0 ? E[i]
-                                         : (T[i] != T[i] ? T[i] + T[i]
-                                                         : __builtin_copysign(__builtin_inf(), T[i]));
+    LDPC_EX_COLD();
+    ratio_fix_n<n>(T, E);
   }
 }
 

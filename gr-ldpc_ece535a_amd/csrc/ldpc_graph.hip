@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(256) g_check(GraphView g, GraphWork w_, int h)
       // ascending k (:503-516)
 #pragma unroll
       for (int t = 0; t < DC; ++t)
-        if (t < d) q[t] = Math<PREC>::tanh_half(q[t]);
+        if (t < d) q[t] = Math<PREC>::tanh_half(q[t], logtab);
       for (int e = 0; e < d; ++e) {
         Real T = Real(1);
 #pragma unroll

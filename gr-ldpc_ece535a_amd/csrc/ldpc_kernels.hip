@@ -261,7 +261,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       rc[q] = rb[lane + 64 * q];  // written by this lane above
       if constexpr (FIN) nr[lane + 64 * q] = -rc[q];
       // initial bit messages M(j,i) = r(i) (:489-496)
-      const Real t0 = Math<PREC>::tanh_half(rc[q]);
+      const Real t0 = Math<PREC>::tanh_half(rc[q], logtab);
       open = open && __builtin_amdgcn_ballot_w64(!(__builtin_fabs((double)rc[q]) <=
                                                     LDPC_TANH_SPLIT)) == 0;
 #pragma unroll
@@ -296,9 +296,14 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       }
       if constexpr (PREC != 3) {
         // the S check messages; modes 0 / 2: glibc's log((1+T)/(1-T)) bit for
-        // bit, mode 0 with the S quotients from one reciprocal
+        // bit, mode 0 with the S quotients from one reciprocal and the near-1
+        // logs packed (tb is free once its gathers above have completed --
+        // the products below consume them -- until the variable pass)
         Real Es[S];
-        Math<PREC>::template check_msg_n<S>(Ts, logtab, Es);
+        if constexpr (PREC == 0)
+          log_ratio_n_packed<S>(Ts, logtab, Es, tb, lane);
+        else
+          Math<PREC>::template check_msg_n<S>(Ts, logtab, Es);
 #pragma unroll
         for (int s = 0; s < S; ++s) eb[lane + 64 * s] = Es[s];
       } else if constexpr (FIN && LDPC_TANH_SPLIT > 0) {
@@ -402,7 +407,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
         for (int q = 0; q < NW; ++q) {
           Real th[DVN];
-          Math<PREC>::template tanh_half_n<DVN>(mv[q], th);
+          Math<PREC>::template tanh_half_n<DVN>(mv[q], th, logtab);
 #pragma unroll
           for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], th[k]);
         }
@@ -435,14 +440,14 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
 #pragma unroll
           for (int q = 0; q < NW; ++q)
 #pragma unroll
-            for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], Math<PREC>::tanh_half(mv[q][k]));
+            for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], Math<PREC>::tanh_half(mv[q][k], logtab));
           open = false;
         }
       } else {
 #pragma unroll
         for (int q = 0; q < NW; ++q)
 #pragma unroll
-          for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], Math<PREC>::tanh_half(mv[q][k]));
+          for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], Math<PREC>::tanh_half(mv[q][k], logtab));
       }
       weight = syndrome();
       used = h + 1;
@@ -510,7 +515,7 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
       // ---- check-pass operand of every edge -> LDS ----------------------
       if constexpr (METHOD == 1) {
         Real th[S];
-        Math<PREC>::template tanh_half_n<S>(msg, th);  // :509
+        Math<PREC>::template tanh_half_n<S>(msg, th, logtab);  // :509
 #pragma unroll
         for (int s = 0; s < S; ++s) tb[lane + 64 * s] = th[s];
       } else {
@@ -540,7 +545,11 @@ __device__ __forceinline__ void decode_frame(const CodeView &code, const DecodeA
           for (int k = 0; k < DCN; ++k) T = T * nb[s][k];
           Ts[s] = T;
         }
-        Math<PREC>::template check_msg_n<S>(Ts, logtab, Es);
+        // tb is free from here to the next iteration's tanh stores
+        if constexpr (PREC == 0)
+          log_ratio_n_packed<S>(Ts, logtab, Es, tb, lane);
+        else
+          Math<PREC>::template check_msg_n<S>(Ts, logtab, Es);
 #pragma unroll
         for (int s = 0; s < S; ++s) eb[lane + 64 * s] = Es[s];
       }
@@ -1011,7 +1020,7 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
       opaque(rn);
       opaque(cn);
       if constexpr (METHOD == 1)
-        tb[tid] = Math<PREC>::tanh_half(msg);  // :509
+        tb[tid] = Math<PREC>::tanh_half(msg, logtab);  // :509
       else
         tb[tid] = msg;
       __syncthreads();

@@ -11,7 +11,8 @@
 
 using namespace ldpc::ex;
 
-static const GlLogEntry kTab[1 << kGlTabBits] = {LDPC_GLIBC_LOG_TAB};
+static const ExTab kEx = make_ex_tab();
+static const GlLogEntry *const kTab = kEx.log;
 
 static int64_t ulps(double a, double b) {
   if (a != a && b != b) return 0;
@@ -39,7 +40,7 @@ void check_tanh_half(const double *m, int64_t n, int64_t *out) {
   for (int64_t i = 0; i + 3 <= n; i += 3) {
     const double v[3] = {m[i], m[i + 1], m[i + 2]};
     double z[3];
-    tanh_half_n<3>(v, z);
+    tanh_half_n<3>(v, z, &kEx);
     for (int j = 0; j < 3; ++j) tally(z[j], tanh(v[j] / 2.0), out);
   }
 }
@@ -50,7 +51,7 @@ void check_expm1(const double *u, int64_t n, int64_t *out) {
   for (int64_t i = 0; i + 3 <= n; i += 3) {
     const double v[3] = {u[i], u[i + 1], u[i + 2]};
     double t[3];
-    expm1_n<3>(v, t);
+    expm1_n<3>(v, t, kEx.tail);
     for (int j = 0; j < 3; ++j) tally(t[j], expm1(v[j]), out);
   }
 }
@@ -68,7 +69,7 @@ void check_log_ratio(const double *T, int64_t n, int64_t *out) {
   for (int64_t i = 0; i + 3 <= n; i += 3) {
     const double v[3] = {T[i], T[i + 1], T[i + 2]};
     double e[3];
-    log_ratio_n<3>(v, kTab, e);
+    log_ratio_n<3>(v, &kEx, e);
     for (int j = 0; j < 3; ++j) tally(e[j], log((1.0 + v[j]) / (1.0 - v[j])), out);
   }
 }
