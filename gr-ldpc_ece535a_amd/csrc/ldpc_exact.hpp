@@ -156,19 +156,17 @@ LDPC_HD void div_n(const double (&a)[n], const double (&b)[n], double (&q)[n]) {
   q[0] = div_core(a[0], b[0], y);
 }
 
-// Per-k constants of expm1's result formula (below): high words of A and B
-// (their low words are zero), for k in [kTailLo, kTailLo + kTailN).
+// Per-k constants A, B of expm1's result formula (below), as doubles, for k
+// in [kTailLo, kTailLo + kTailN).
 struct TailEntry {
-  uint32_t a_hi, b_hi;
+  double a, b;
 };
 constexpr int kTailLo = -3, kTailN = 68;  // k = -3 .. 64
 constexpr TailEntry tail_entry(int k) {
-  return TailEntry{(k == 0 || k == -1) ? 0u                                            // A = 0
-                   : (k >= 2 && k <= 19) ? 0x3ff00000u - (0x200000u >> k)              // 1 - 2^-k
-                                         : 0x3ff00000u,                                // 1
-                   k == -1 ? 0xbfe00000u                                               // B = -0.5
-                   : (k >= 0 && k <= 56) ? 0x80000000u                                 // -0
-                                         : 0xbff00000u};                               // -1
+  return TailEntry{(k == 0 || k == -1) ? 0.0                                    // A = 0
+                   : (k >= 2 && k <= 19) ? 1.0 - 1.0 / (double)(1ull << k)     // 1 - 2^-k
+                                         : 1.0,                                 // 1
+                   k == -1 ? -0.5 : (k >= 0 && k <= 56) ? -0.0 : -1.0};         // B
 }
 // Everything the exact functions look up: glibc's log table and the tails.
 struct ExTab {
@@ -208,8 +206,12 @@ constexpr ExTab make_ex_tab() {
 //            exact, so the fma's rounding is the product's (none).
 // Everything else is glibc's operation sequence, unchanged.
 // ---------------------------------------------------------------------------
+// mid_possible: false if the caller knows every |u| < 13.5 (k <= 19), so
+// the k = 20..56 formula need not be checked for (tanh_half_n folds that
+// test into its own rare-case test).
 template <int n>
-LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n], const TailEntry *tail) {
+LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n], const TailEntry *tail,
+                     bool mid_possible = true) {
   constexpr double ln2_hi = 6.93147180369123816490e-01;
   constexpr double ln2_lo = 1.90821492927058770002e-10;
   constexpr double invln2 = 1.44269504088896338700e+00;
@@ -226,11 +228,12 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n], const TailEntry *tail
     const uint32_t hx = hw & 0x7fffffffu, sgn = hw & 0x80000000u;
     // k = (int)(invln2 * u + (u > 0 ? 0.5 : -0.5)), truncation toward zero;
     // |k| <= 63 here, so the integral double has a zero low word and the
-    // three-way choice of k is made on high words
+    // choice of k is made on high words
+    // glibc takes k = -1 for hx in (0x3fd62e42, 0x3FF0A2B2) instead of this
+    // rounding, but on that range (u < 0 here) invln2 u - 0.5 lies in
+    // (-2, -1): kg is -1 there too.  Only k = 0 needs its own select.
     const double kg = __builtin_trunc(invln2 * u[i] + from_hi(0x3fe00000u | sgn));
-    uint32_t th = hx < 0x3FF0A2B2u ? (0x3ff00000u | sgn) : hiw(kg);  // +-1 below 1.5 ln2
-    th = hx > 0x3fd62e42u ? th : 0u;                                  // 0 up to 0.5 ln2
-    const double tk = from_hi(th);
+    const double tk = from_hi(hx > 0x3fd62e42u ? hiw(kg) : 0u);
     k[i] = (int)tk;
     const double hi = fma_(-tk, ln2_hi, u[i]);  // tk * ln2_hi is exact (|k| <= 64)
     const double lo = tk * ln2_lo;
@@ -256,14 +259,12 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n], const TailEntry *tail
     ep[i] = (x[i] * (e - c[i]) - c[i]) - hxs[i];
     const double d = ep[i] - x[i];
     const int kk = k[i];
-    // per-lane constants (high words; every low word is zero): 2^k, and A, B
-    // from the table (tail_entry)
-    const uint32_t sh = (uint32_t)(0x3ff + kk) << 20;
+    // per-lane constants: A, B from the table (tail_entry), 2^k exact
     const TailEntry te = tail[kk - kTailLo];
-    t[i] = fma_(from_hi(te.a_hi) - d, from_hi(sh), from_hi(te.b_hi));
-    any_mid |= (uint32_t)(kk - 20) <= 36u;
+    t[i] = fma_(te.a - d, __builtin_ldexp(1.0, kk), te.b);
+    if (mid_possible) any_mid |= (uint32_t)(kk - 20) <= 36u;
   }
-  if (LDPC_EX_ANY(any_mid)) {
+  if (mid_possible && LDPC_EX_ANY(any_mid)) {
     LDPC_EX_COLD();
 #pragma unroll
     for (int i = 0; i < n; ++i) {
@@ -306,9 +307,11 @@ LDPC_HD void tanh_half_n(const double (&m)[n], double (&z)[n], const ExTab *tab)
     const double ac = __builtin_fmin(__builtin_fmax(__builtin_fabs(m[i]), 0x1p-54), 43.0);
     // u = |m| for |x| >= 1, else -|m|: the sign bit of im - bits(2.0)
     u[i] = dbl(bits(ac) ^ ((uint64_t)((im - 0x40000000u) & 0x80000000u) << 32));
-    special |= im - 0x3c900000u >= 0x7ff00000u - 0x3c900000u;  // |x| < 2^-55, inf, NaN
+    // outside [2^-54, 13.5): |x| < 2^-55, inf, NaN, or possibly k >= 20
+    special |= im - 0x3c900000u >= 0x402b0000u - 0x3c900000u;
   }
-  expm1_n<n>(u, t, tab->tail);
+  const bool any_special = LDPC_EX_ANY(special);
+  expm1_n<n>(u, t, tab->tail, any_special);
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     const bool big = (hm[i] & 0x7fffffffu) >= 0x40000000u;  // |x| >= 1
@@ -322,7 +325,7 @@ LDPC_HD void tanh_half_n(const double (&m)[n], double (&z)[n], const ExTab *tab)
     const double r = big ? 1.0 - q[i] : q[i];  // >= 0: the sign is x's (m's)
     z[i] = dbl(bits(r) | ((uint64_t)(hm[i] & 0x80000000u) << 32));
   }
-  if (LDPC_EX_ANY(special)) {
+  if (any_special) {
     LDPC_EX_COLD();
 #pragma unroll
     for (int i = 0; i < n; ++i) {
