@@ -56,7 +56,13 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SIMDS, CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMDs, max clock
 F64_PEAK_TFLOPS = 78.6         # MI355X FP64 vector spec
 # VALU issue cycles per wave64 instruction on gfx950 (profiles/round2/ubench_f64.txt)
-ISSUE_F64, ISSUE_TRANS64, ISSUE_OTHER = 4.0, 16.0, 2.0
+# issue cycles per wave64 instruction at 4 waves/SIMD (tools/ubench_f64.hip,
+# tools/ubench_valu.hip; profiles/round3/ubench_valu.txt): f64 add/mul/fma
+# 4.31, v_rcp_f64 16.3; "other VALU" (the PMC's remainder: 32-bit VOP2 ops at
+# 2.75, VOP3 / 64-bit ones -- compares, e64 selects, converts, 64-bit moves --
+# at 4.31) takes the kernel's hot-path mix (tools/isa_hot.py, recorded with
+# the counters) or this default
+ISSUE_F64, ISSUE_TRANS64, ISSUE_OTHER = 4.31, 16.3, 3.5
 METRIC = "decoded info Mbit/s @ 50 BP iters, batch=4096; achieved HBM GB/s vs peak"
 
 
@@ -337,13 +343,14 @@ def load_pmc(path, key):
         return None
 
 
-def valu_roofline(pmc, per_launch_ms):
+def valu_roofline(pmc, per_launch_ms, w_other=None):
     """VALU issue-cycle roofline from PMC instruction counts per launch."""
+    w_other = ISSUE_OTHER if w_other is None else w_other
     f64 = sum(pmc.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
                                          "SQ_INSTS_VALU_FMA_F64"))
     trans = pmc.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
     other = max(0.0, pmc["SQ_INSTS_VALU"] - f64 - trans)
-    cycles = ISSUE_F64 * f64 + ISSUE_TRANS64 * trans + ISSUE_OTHER * other
+    cycles = ISSUE_F64 * f64 + ISSUE_TRANS64 * trans + w_other * other
     peak = SIMDS * CLOCK_HZ / 1e9
     ach = cycles / (per_launch_ms * 1e-3) / 1e9
     flop = 64.0 * (2.0 * pmc.get("SQ_INSTS_VALU_FMA_F64", 0.0) +
@@ -354,8 +361,9 @@ def valu_roofline(pmc, per_launch_ms):
             "f64_tflops": round(flop / (per_launch_ms * 1e-3) / 1e12, 2),
             "f64_tflops_frac": round(flop / (per_launch_ms * 1e-3) / 1e12 / F64_PEAK_TFLOPS, 4),
             "weights": "issue cycles per wave64 instruction: f64 add/mul/fma %g, f64 "
-                       "transcendental %g, other VALU %g (profiles/round2/ubench_f64.txt)"
-                       % (ISSUE_F64, ISSUE_TRANS64, ISSUE_OTHER)}
+                       "transcendental %g, other VALU %g (profiles/round3/ubench_valu.txt; "
+                       "'other' = the kernel's hot-path VOP2/VOP3 mix, tools/isa_hot.py)"
+                       % (ISSUE_F64, ISSUE_TRANS64, w_other)}
 
 
 class _quiet_stdout:
@@ -720,7 +728,8 @@ def main():
                             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                             "traffic": traffic, "model": hbm_model["model"]}
     elif pmc and "SQ_INSTS_VALU" in pmc:
-        line["roofline"] = valu_roofline(pmc, per_launch_ms)
+        line["roofline"] = valu_roofline(pmc, per_launch_ms,
+                                         (entry.get("isa_hot") or {}).get("other_weight"))
         line["roofline"]["traffic"] = traffic
         line["roofline"]["pmc_source"] = entry.get("source")
         hbm_model["label"] = ("equivalent streaming bandwidth of a decoder that streams its edge "
