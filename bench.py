@@ -473,7 +473,7 @@ def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
         ref = orc.decode_batch_sparse(0, csr[2], csr[3], csr[0], csr[1], kept["y"], args.iters,
                                       nthreads=threads, want_bits=False)
         cpu_s = time.perf_counter() - t0
-        out["min-sum f64"]["parity_sample"] = {
+        out["min-sum f64"]["parity"] = {
             "frames": cpu_sample,
             "packed_mismatch_frames": int((ref["packed"] != kept["pk"]).any(axis=1).sum()),
             "iters_mismatch_frames": int((ref["iters"] != kept["it"]).sum()),
@@ -493,7 +493,7 @@ def gpu_variants(L, torch, dec, args, dev, inputs, B, D, prec, dvb, world, rank)
     if not dvb and not args.no_config4:
         var["config4"], res["config4_check"] = config4_variant(
             L, torch, dev, args, args.seed + 31,
-            cpu_sample=0 if (args.no_cpu_baseline or rank != 0) else 64)
+            cpu_sample=0 if (args.no_cpu_baseline or rank != 0) else 1024)
     if not dvb and not args.no_block and world == 1:
         from ldpc_ece535a import blocks
         with _quiet_stdout():
@@ -765,8 +765,8 @@ def main():
         threads = args.cpu_threads or threads
         llr = inputs[0].cpu().numpy()
         packed = r["outs"][0][0].cpu().numpy()
-        if dvb:  # bounded sample: the sparse restatement on the first 128 frames
-            nb = min(B, 128)
+        if dvb:  # the sparse restatement on every frame of rank 0's batch (~2 s)
+            nb = B
             t0 = time.perf_counter()
             ref = orc.decode_batch_sparse(args.method, csr[2], csr[3], csr[0], csr[1], llr[:nb],
                                           args.iters, nthreads=threads, want_bits=False)
@@ -774,7 +774,7 @@ def main():
             line["cpu_baseline"] = {
                 "value": round(nb * dec.K / cpu_s / 1e6, 5), "unit": "Mbit/s", "cores": threads,
                 "kind": "port",
-                "sample": "first %d of rank 0's %d frames, sparse oracle, %d threads on %s"
+                "sample": "%d of rank 0's %d frames, sparse oracle, %d threads on %s"
                           % (nb, B, threads, cpu_model())}
             line["parity"] = {"frames": nb,
                               "packed_mismatch_frames": int((ref["packed"] != packed[:nb]).any(axis=1).sum()),

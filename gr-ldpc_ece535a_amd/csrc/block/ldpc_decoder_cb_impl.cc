@@ -64,8 +64,15 @@ namespace ldpc_ece535a {
 #define STATE_IN_SYNC_INVERTED 2
 
 namespace {
-const int kMaxWindows = 1 << 17;  // windows per launch (bounds staging memory)
-const int kSearchFirst = 128;     // out-of-sync positions a launch first guesses past; x4 after
+// Per launch at most kWindowSamples samples of windows (1 << 17 windows of
+// the reference's N = 64; a DVB-S2-size code gets ~130), which bounds the
+// staging memory and the launch for any N; the out-of-sync search starts
+// with at most kSearchFirst positions and widens x4 per launch.
+const int64_t kWindowSamples = (int64_t)64 << 17;
+const int kSearchFirst = 128;
+int max_windows(unsigned N) {
+  return (int)std::max<int64_t>(16, std::min<int64_t>((int64_t)1 << 17, kWindowSamples / (int64_t)N));
+}
 const int kForkFrames = 13;       // frames a guessed sync at a search position is followed for
 const int kForkSearch = 3;        // x N: the search after such a sync is lost, per fork
 const size_t kDenseMax = (size_t)1 << 22;  // alist codes up to M N entries go dense
@@ -249,7 +256,7 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
 }
 
 void ldpc_decoder_cb_impl::want(int64_t pos, int pol, int nin) {
-  if (pos < 0 || pos + (int64_t)d_N > nin || d_want.size() >= (size_t)kMaxWindows) return;
+  if (pos < 0 || pos + (int64_t)d_N > nin || d_want.size() >= (size_t)max_windows(d_N)) return;
   int32_t &m = d_memo[pol][pos];
   if (m == -1) {
     m = -2;  // pending: wanted by this launch
@@ -451,7 +458,8 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   d_rpacked.clear();
 
   Replay r{d_state, d_errors, 0, 0};
-  int out_budget = kSearchFirst;  // out-of-sync positions one launch may guess past
+  const int search_first = std::min(kSearchFirst, max_windows(d_N));
+  int out_budget = search_first;  // out-of-sync positions one launch may guess past
   bool first = true, last_out = false;
   double t0 = d_profile ? now_s() : 0.0;
   while (replay(r, true, nin, noutput_items, out, 0, 0) == STALLED) {
@@ -460,21 +468,21 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
     // collect the windows it will probably need, and decode them at once
     const bool now_out = r.state == STATE_OUT_OF_SYNC;
     if (now_out && last_out)
-      out_budget = std::min(4 * out_budget, kMaxWindows);  // the search goes on: wider
+      out_budget = std::min(4 * out_budget, max_windows(d_N));  // the search goes on: wider
     else if (!now_out)
-      out_budget = kSearchFirst;
+      out_budget = search_first;
     last_out = now_out;
     d_want.clear();
     d_forks.clear();
     Replay dry = r;
     if (d_profile) t0 = now_s();
-    replay(dry, false, nin, noutput_items, nullptr, out_budget, (size_t)kMaxWindows);
+    replay(dry, false, nin, noutput_items, nullptr, out_budget, (size_t)max_windows(d_N));
     // then the branches where a search position passes, nearest first, while
     // the launch has room: windows up to about one per wave slot of the GPU
     // cost little more than the launch's latency (50 iterations of one frame)
     if (d_fork)
       for (int64_t q : d_forks) {
-        if (d_want.size() >= (size_t)d_budget) break;
+        if (d_want.size() >= (size_t)std::min(d_budget, max_windows(d_N))) break;
         fork(q, nin);
       }
     if (d_debug)

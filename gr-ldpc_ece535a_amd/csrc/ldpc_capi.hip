@@ -1057,9 +1057,12 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   while (q < ctx->queues.size() && ctx->queues[q].stream != st) ++q;
   if (q == ctx->queues.size()) {
     if (q == LDPC_TICKET_SLOTS) {
-      // more streams than counters: drain the device, start every queue over
+      // more streams than counters: drain the device, start every queue over.
+      // The memset runs on the null stream, which non-blocking streams are
+      // not ordered after: wait for it before any stream launches again.
       if ((e = hipDeviceSynchronize()) != hipSuccess ||
-          (e = hipMemset(ctx->d_tickets, 0, LDPC_TICKET_SLOTS * sizeof(uint32_t))) != hipSuccess)
+          (e = hipMemset(ctx->d_tickets, 0, LDPC_TICKET_SLOTS * sizeof(uint32_t))) != hipSuccess ||
+          (e = hipDeviceSynchronize()) != hipSuccess)
         return hip_err(ctx, e, "ticket reset");
       ctx->queues.clear();
       q = 0;
@@ -1167,7 +1170,8 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
       return set_err(ctx, LDPC_EINVAL, "window outside the input span");
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t b_span = al((size_t)S * 4), b_win = al((size_t)B * 8),
-               b_fr = al((size_t)B * N * 4), b_pk = al((size_t)B * ctx->KB),
+               // gathered frames: only the large-code kernels need them
+               b_fr = ctx->graph ? al((size_t)B * N * 4) : 0, b_pk = al((size_t)B * ctx->KB),
                b_sy = al((size_t)B * 4);
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");

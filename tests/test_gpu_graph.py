@@ -121,17 +121,19 @@ def test_dvbs2_like_minsum_f64_vs_sparse_oracle(dvb, db, iters):
     np.testing.assert_array_equal(out["packed"], ref["packed"])
 
 
+@pytest.mark.parametrize("prec", [0, 2])
 @pytest.mark.parametrize("method", [1, 2, 3])
-def test_dvbs2_like_other_methods_vs_sparse_oracle(dvb, method):
+def test_dvbs2_like_other_methods_vs_sparse_oracle(dvb, method, prec):
     """Sum-product on this code saturates tanh -> log(2/0) = inf -> NaN
-    messages, exactly as the reference's unclipped arithmetic does; the
-    F64_LIBM mode (glibc-identical tanh) must follow the oracle through it."""
+    messages, exactly as the reference's unclipped arithmetic does; both
+    exact f64 modes (glibc's tanh / log reproduced) must follow the oracle
+    through it."""
     from oracle import oracle as orc
     csr, d = dvb
     M, N, rp, ci = csr
     info, y = _noisy(csr, 16, 2, seed=20 + method)
     iters = 12
-    out = d.decode(y, method=method, max_iters=iters, precision=2)
+    out = d.decode(y, method=method, max_iters=iters, precision=prec)
     ref = orc.decode_batch_sparse(method, rp, ci, M, N, y, iters, nthreads=16)
     np.testing.assert_array_equal(out["iters"], ref["iters"])
     np.testing.assert_array_equal(out["synd"], ref["synd"])
@@ -140,21 +142,32 @@ def test_dvbs2_like_other_methods_vs_sparse_oracle(dvb, method):
 
 def test_dvbs2_like_full_batch_roundtrip(dvb):
     """Config-4 batch (1024 frames at 2 dB): every frame decodes to its info
-    bits with a zero syndrome, f64 and f32; the f64 run's first 64 frames
-    equal the sparse oracle's."""
+    bits with a zero syndrome, f64 and f32; all 1024 f64 frames (packed
+    bytes, iterations, syndromes) equal the sparse oracle's -- on the
+    compressed-message pipeline (the default) and on the edge-message passes
+    (LDPC_MS_PIPELINE=0)."""
+    import os
+    import ldpc_ece535a as L
     from oracle import oracle as orc
     csr, d = dvb
     M, N, rp, ci = csr
     info, y = _noisy(csr, 1024, 2, seed=4)
     want = np.packbits(info, axis=1)
-    for prec in (0, 1):
-        out = d.decode(y, method=0, max_iters=50, precision=prec, want_bits=False)
-        assert (out["synd"] == 0).all()
-        assert (out["packed"] == want).all()
-        if prec == 0:
-            ref = orc.decode_batch_sparse(0, rp, ci, M, N, y[:64], 50, nthreads=16,
-                                          want_bits=False)
-            np.testing.assert_array_equal(out["iters"][:64], ref["iters"])
+    ref = orc.decode_batch_sparse(0, rp, ci, M, N, y, 50, nthreads=16, want_bits=False)
+    os.environ["LDPC_MS_PIPELINE"] = "0"
+    try:
+        edge = L.Decoder(csr=csr)
+    finally:
+        del os.environ["LDPC_MS_PIPELINE"]
+    for dec, name in ((d, "pipeline"), (edge, "edge passes")):
+        for prec in (0, 1):
+            out = dec.decode(y, method=0, max_iters=50, precision=prec, want_bits=False)
+            assert (out["synd"] == 0).all(), name
+            assert (out["packed"] == want).all(), name
+            if prec == 0:
+                for k in ("packed", "iters", "synd"):
+                    np.testing.assert_array_equal(out[k], ref[k], err_msg="%s %s" % (name, k))
+    edge.close()
 
 
 @pytest.mark.parametrize("method,db", [(0, 2), (1, 2), (0, 4), (1, 1)])
