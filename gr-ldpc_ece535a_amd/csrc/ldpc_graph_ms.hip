@@ -623,6 +623,24 @@ int launch_graph_decode_ms(const GraphView &g, const MsWork &w, const DecodeArgs
   // drains within ceil(B/S) (max+1) passes and the last frames finish
   // within max+1 more; passes past the end return at once (empty chunks)
   const int64_t bound = ((int64_t)(a.B + w.S - 1) / w.S + 1) * (a.max_iters + 1) + 2;
+  // Default: the host reads the progress counter back every kRound passes
+  // (one round behind, so the GPU never waits) and stops enqueueing when
+  // every frame is done -- the call returns once the decode has finished.
+  // LDPC_MS_ASYNC=1: all `bound` passes are enqueued and the call returns at
+  // once, like the other ldpc_decode_device paths; the passes after the last
+  // frame find no running chunk and return, but with 128 slots the bound is
+  // ~3x the passes a 2 dB batch needs and the empty ones cost 11 % of config
+  // 4's throughput (profiles/round3/ab_ms_async.txt).
+  static const bool async = getenv("LDPC_MS_ASYNC") && getenv("LDPC_MS_ASYNC")[0] == '1';
+  if (async) {
+    for (int64_t pass = 0; pass < bound; ++pass) {
+      if (prec == 1)
+        ms_pass<1>(g, w, a, a.max_iters, st);
+      else
+        ms_pass<0>(g, w, a, a.max_iters, st);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   const int kRound = 8;
   hipEvent_t ev[2] = {nullptr, nullptr};
   for (int i = 0; i < 2; ++i)

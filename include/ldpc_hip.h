@@ -230,10 +230,14 @@ int ldpc_decode_windows(ldpc_ctx *ctx, int method, int max_iters, int et_period,
 
 /* Device-resident buffers (already in HBM); enqueues on `hip_stream`
  * (hipStream_t, NULL = the context's own stream) and returns without
- * synchronising.  One host thread may enqueue on several streams: small-code
- * launches on different streams run concurrently (each stream has its own
- * frame queue), large-code launches share the context's workspace and are
- * ordered after the previous one when the stream changes. */
+ * synchronising -- except min-sum on a large-code context, whose pass loop
+ * stops on a progress counter the host reads back: that call returns when
+ * its decode has finished (LDPC_MS_ASYNC=1 enqueues the worst-case number of
+ * passes instead and returns at once, ~11 % slower on config 4).  One host
+ * thread may enqueue on several streams: small-code launches on different
+ * streams run concurrently (each stream has its own frame queue), large-code
+ * launches share the context's workspace and are ordered after the previous
+ * one when the stream changes. */
 int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
                        int et_period, int precision, const float *d_in,
                        int64_t cw_stride, int elem_stride, float polarity,

@@ -21,14 +21,17 @@ def _frames(Hr, B, db, seed):
     return (x + np.sqrt(10 ** (-db / 10)) * rng.standard_normal(x.shape)).astype(np.float32)
 
 
+@pytest.mark.parametrize("method", [1, 0])
 @pytest.mark.parametrize("graph", [False, True])
-def test_interleaved_streams(graph):
+def test_interleaved_streams(graph, method):
+    """method 0 on the large-code path is the compressed-message min-sum
+    pipeline, whose passes are all enqueued without a host round trip."""
     import torch
     import ldpc_ece535a as L
     dec = L.Decoder(force_graph=graph)
     B = 4096 if not graph else 512
     ys = [_frames(dec.H, B, db, 900 + k) for k, db in enumerate((2.0, 0.0, 3.0))]
-    refs = [dec.decode(y, method=1, max_iters=50) for y in ys]
+    refs = [dec.decode(y, method=method, max_iters=50) for y in ys]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     d_in = [torch.from_numpy(y).cuda() for y in ys]
     launches = []
@@ -39,12 +42,12 @@ def test_interleaved_streams(graph):
         it = torch.empty(B, dtype=torch.int32, device="cuda")
         sy = torch.empty(B, dtype=torch.int32, device="cuda")
         with torch.cuda.stream(st):
-            dec.decode_device(d_in[j].data_ptr(), B, pk.data_ptr(), method=1, max_iters=50,
-                              d_iters=it.data_ptr(), d_synd=sy.data_ptr(),
+            dec.decode_device(d_in[j].data_ptr(), B, pk.data_ptr(), method=method,
+                              max_iters=50, d_iters=it.data_ptr(), d_synd=sy.data_ptr(),
                               stream=st.cuda_stream)
         launches.append((j, pk, it, sy))
         if k == 5:  # a host-buffer decode on the context's own stream meanwhile
-            mid = dec.decode(ys[1], method=1, max_iters=50)
+            mid = dec.decode(ys[1], method=method, max_iters=50)
             assert (mid["packed"] == refs[1]["packed"]).all()
     torch.cuda.synchronize()
     for j, pk, it, sy in launches:
