@@ -41,6 +41,7 @@ SIGNATURES = {
     "ldpc_create_csr": (_vp, [_i, _i, _i32p, _i32p, _i, _i]),
     "ldpc_ctx_csr": (_i, [_vp, _i32p, _i32p]),
     "ldpc_ctx_path": (_i, [_vp]),
+    "ldpc_ctx_packed_frames": (_i, [_vp]),
     "ldpc_ctx_layout": (_i, [_vp, _i32p]),
     "ldpc_plan_layout": (_i, [_u8p, _i, _i, _i, _i32p, _i32p, _i32p]),
     "ldpc_set_work_limit": (_i, [_vp, _i64]),
@@ -195,6 +196,11 @@ class Decoder:
         _check(lib().ldpc_ctx_csr(self._ctx, _p(self.row_ptr, _i32p), _p(self.col_idx, _i32p)),
                self._ctx)
         self._H = None
+
+    def packed_frames_per_wave(self):
+        """ldpc_ctx_packed_frames: frames per wave of the packed sum-product
+        kernel (throughput mode, f64), 0 if the code does not fit it."""
+        return _check(lib().ldpc_ctx_packed_frames(self._ctx), self._ctx)
 
     @property
     def layout_model(self):
