@@ -391,6 +391,7 @@ def drive_stream(blk, cx, B):
     pos = 0
     o, used = blk.general_work(B * 4, cx[:chunk])
     pos += used
+    outs = [o]
     l0, f0 = blk.launches, blk.frames_decoded
     made = calls = 0
     t0 = time.perf_counter()
@@ -399,23 +400,35 @@ def drive_stream(blk, cx, B):
         pos += used
         made += o.size
         calls += 1
+        outs.append(o)
         if used == 0:
             break
-    return (time.perf_counter() - t0, made, calls, blk.launches - l0, blk.frames_decoded - f0)
+    dt = time.perf_counter() - t0
+    drive_stream.last_out = np.concatenate(outs)  # every byte, the untimed first call's too
+    return (dt, made, calls, blk.launches - l0, blk.frames_decoded - f0)
 
 
-def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4):
+def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
     """The drop-in block's own throughput: ldpc_decoder_cb (method 1, f64; the
     bench's iteration cap, and the reference block's own 5) general_work over
     a continuous stream of gr_complex frames in host memory, as a GNU Radio
     scheduler drives it
     (lib/ldpc_decoder_cb_impl.cc:133-234): calls of B frames of input,
-    packed bytes out."""
+    packed bytes out.  Beside each: the reference block restated on the CPU
+    (oracle Block, one core: the state machine is sequential) over the
+    stream's first `cpu_frames` frames of samples -- its rate, and whether its
+    bytes equal the GPU block's for that prefix (the block is causal)."""
     out = {}
-    runs = (("in-sync stream (4 dB)", 4.0, args.iters), ("2 dB stream (sync losses)", 2.0, args.iters),
+    orc = None
+    if cpu_frames and not args.no_cpu_baseline:
+        sys.path.insert(0, REPO)
+        from oracle import oracle as orc
+    # (name, Eb/N0, iterations, CPU sample in frames: ~3-15 s of one core each)
+    runs = (("in-sync stream (4 dB)", 4.0, args.iters, cpu_frames),
+            ("2 dB stream (sync losses)", 2.0, args.iters, cpu_frames // 2),
             # make(method) as the reference builds it: 5 iterations (:40)
-            ("make(1) defaults, 5 iterations, 4 dB", 4.0, 5))
-    for name, ebn0, iters in runs:
+            ("make(1) defaults, 5 iterations, 4 dB", 4.0, 5, cpu_frames))
+    for name, ebn0, iters, n_cpu in runs:
         dec = L.Decoder(device=dev.index or 0)
         y, _ = synth_device(L, torch, dec, (reps + 1) * B, ebn0, args.seed + 77, dev,
                             check_frames=0)
@@ -430,7 +443,21 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4):
                      "launches_per_call": round(launches / max(1, calls), 2),
                      "windows_per_output_frame": round(windows / max(1, made // 4), 2),
                      "bytes_out": int(made)}
+        if orc is not None:
+            gpu_bytes = drive_stream.last_out
+            sample = cx[:n_cpu * 64]
+            t0 = time.perf_counter()
+            ref = orc.run_stream(1, Hr, sample, iterations=iters)
+            cpu_s = time.perf_counter() - t0
+            out[name]["cpu_baseline"] = {
+                "Mbit/s": round(ref.size * 8 / cpu_s / 1e6, 5), "cores": 1, "kind": "port",
+                "sample": "the stream's first %d frames of samples through the restated "
+                          "general_work (oracle Block, :133-234), one thread" % n_cpu,
+                "bytes": int(ref.size),
+                "bytes_equal_gpu_prefix": bool(gpu_bytes.size >= ref.size and
+                                               (gpu_bytes[:ref.size] == ref).all())}
     return out
+
 
 
 def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):

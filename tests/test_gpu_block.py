@@ -83,3 +83,35 @@ def test_dump_app_noisy_sum_product():
                          stream=open("/dev/null", "w"))
     assert len(got) == len(sent)
     assert (got != sent).mean() < 0.02
+
+
+def _zero_region_stream(Hr, seed):
+    """Frames, a region of exact zeros (not a whole number of frames), frames
+    again, negative zeros, negated frames.  What a window of +-0 samples
+    decodes to (all-zero or all-one bytes, a sync loss or not) is decided by
+    each method's sign rule at exactly zero (lib/ldpc_decoder_cb_impl.cc
+    :398, :426, :527, :564); the bytes must be the restated
+    general_work's, including the resynchronisation after the region."""
+    rng = np.random.default_rng(seed)
+    x = (2.0 * L.encode(Hr, rng.integers(0, 2, size=(90, 32), dtype=np.uint8)) - 1.0)
+    x = (x + 0.7 * rng.standard_normal(x.shape)).astype(np.float32)
+    z = np.zeros(64 * 9 + 23, np.float32)
+    s = np.concatenate([rng.standard_normal(11).astype(np.float32), x[:30].ravel(), z,
+                        x[30:60].ravel(), -z, np.zeros(5, np.float32), -x[60:].ravel()])
+    return s.astype(np.complex64)
+
+
+@pytest.mark.parametrize("method,iters", [(0, 5), (1, 5), (1, 50), (2, 5), (3, 5)])
+def test_gpu_block_zero_filled_region(golden, method, iters):
+    from oracle import oracle as orc
+    Hr = golden("frames_default.npz")["H_reordered"]
+    s = _zero_region_stream(Hr, 31 + method)
+    exp = orc.run_stream(method, Hr, s, iterations=iters)
+    assert len(exp) > 0
+    for chunk in ([97, 13, 640, 5, 2000] * 8, 100000):
+        blk = L.ldpc_decoder_cb(method, iterations=iters)
+        tb = fg.top_block(chunk=chunk, out_space=61)
+        src, dst = fg.vector_source_c(s), fg.vector_sink_b()
+        tb.connect(src, blk, dst)
+        tb.run()
+        assert (dst.array() == exp).all(), chunk
