@@ -432,6 +432,7 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
         dec = L.Decoder(device=dev.index or 0)
         y, _ = synth_device(L, torch, dec, (reps + 1) * B, ebn0, args.seed + 77, dev,
                             check_frames=0)
+        Hr = dec.H.copy()  # the block's H: the reference default, reordered (:98-106)
         dec.close()
         stream = np.zeros(2 * y.numel(), np.float32)
         stream[0::2] = y.cpu().numpy().ravel()
