@@ -93,11 +93,12 @@ LDPC_HD double rcp_seed(double p) {
 #endif
 }
 
-// a / b, correctly rounded, from y ~ 1/b (relative error < 2^-45).
-//  1. q0 = a y; r = fma(-b, q0, a); q1 = fma(r, y, q0).  q1 - a/b =
-//     (a/b - q0)(b y - 1) + rounding: q1 is within 1/2 ulp + 2^-40 ulp of
-//     a/b, i.e. faithful -- and RN(a/b) unless a/b lies within 2^-40 ulp of
-//     a rounding boundary (the Markstein step alone is not enough there:
+// a / b, correctly rounded, from yk = y (1 + 2^-40), y ~ 1/b with relative
+// error < 2^-45 (so b yk lies in (1 + 2^-41, 1 + 2^-39)).
+//  1. q0 = a yk; r = fma(-b, q0, a); q1 = fma(r, yk, q0).  q1 - a/b =
+//     (a/b - q0)(b yk - 1) + rounding: q1 is within 1/2 ulp + 2^-26 ulp of
+//     a/b (the product is below 2^-78 relative), i.e. faithful -- and
+//     RN(a/b) unless a/b lies within 2^-26 ulp of a rounding boundary (the Markstein step alone is not enough there:
 //     a = 1, b = 1 - 2^-53 with y = 1 gives 1 instead of 1 + 2^-52).
 //  2. The decision is then made exactly.  For faithful q1 the residual
 //     r1 = a - b q1 is a double, so fma(-b, q1, a) is exact, and
@@ -110,17 +111,15 @@ LDPC_HD double rcp_seed(double p) {
 //     (halved below a power of two), in a branch the wave takes only then.
 // Domain: a, b normal (or a = +-0), a / b normal, all far from
 // over/underflow (|exponents| < 900).
-LDPC_HD double div_core(double a, double b, double y) {
-  const double q0 = a * y;
+LDPC_HD double div_core(double a, double b, double yk) {
+  const double q0 = a * yk;
   const double r = fma_(-b, q0, a);
-  double q1 = fma_(r, y, q0);
+  double q1 = fma_(r, yk, q0);
   const double r1 = fma_(-b, q1, a);  // exact: a/b = q1 + r1/b
-  // t' = r1 yk with yk = y (1 + 2^-40), |b yk| in (1 + 2^-41, 1 + 2^-39)
-  // (y's relative error is below 2^-45): t' has r1/b's sign and a larger
-  // magnitude, so RN(q1 + t') == q1 implies |r1/b| < |t'| <= half the gap
-  // on that side (the addition itself takes the smaller gap below a power
-  // of two), i.e. RN(a/b) == q1.  Anything else is flagged.
-  const double yk = y * (1.0 + 0x1p-40);
+  // t' = r1 yk, |b yk| in (1 + 2^-41, 1 + 2^-39): t' has r1/b's sign and a
+  // larger magnitude, so RN(q1 + t') == q1 implies |r1/b| < |t'| <= half
+  // the gap on that side (the addition itself takes the smaller gap below a
+  // power of two), i.e. RN(a/b) == q1.  Anything else is flagged.
   const bool flag = fma_(r1, yk, q1) != q1;
   if (LDPC_EX_ANY(flag)) {
     LDPC_EX_COLD();
@@ -136,9 +135,10 @@ LDPC_HD double div_core(double a, double b, double y) {
 }
 
 // q[i] = a[i] / b[i], correctly rounded, from ONE reciprocal: prefix products
-// p_i = b_0 ... b_i, y = 1 / p_{n-1} (v_rcp_f64 + one Newton step), then
-// backwards 1/b_i ~ y p_{i-1}, y <- y b_i (a few ulp); each quotient then
-// takes div_core.  Domain: div_core's, and every prefix product normal.
+// p_i = b_0 ... b_i, y = 1 / p_{n-1} (v_rcp_f64 + one Newton step), scaled
+// once by 1 + 2^-40 (div_core's yk), then backwards 1/b_i (1 + 2^-40) ~
+// y p_{i-1}, y <- y b_i (a few ulp); each quotient then takes div_core.
+// Domain: div_core's, and every prefix product normal.
 template <int n>
 LDPC_HD void div_n(const double (&a)[n], const double (&b)[n], double (&q)[n]) {
   double p[n];
@@ -147,6 +147,7 @@ LDPC_HD void div_n(const double (&a)[n], const double (&b)[n], double (&q)[n]) {
   for (int i = 1; i < n; ++i) p[i] = p[i - 1] * b[i];
   double y = rcp_seed(p[n - 1]);
   y = fma_(fma_(-p[n - 1], y, 1.0), y, y);
+  y = y * (1.0 + 0x1p-40);
 #pragma unroll
   for (int i = n - 1; i > 0; --i) {
     const double inv = y * p[i - 1];
@@ -156,12 +157,21 @@ LDPC_HD void div_n(const double (&a)[n], const double (&b)[n], double (&q)[n]) {
   q[0] = div_core(a[0], b[0], y);
 }
 
-// Per-k constants A, B of expm1's result formula (below), as doubles, for k
-// in [kTailLo, kTailLo + kTailN).
+// Per-k constants of expm1 (below), as doubles, for k in [kTailLo,
+// kTailLo + kTailN), in two 16-byte tables (a 16-byte stride spreads the
+// lanes' lookups over the LDS banks): the argument reduction's k ln2_hi
+// (exact: ln2_hi has 32 significant bits) and k ln2_lo (glibc's rounded
+// product, the same double), and A, B of the result formula.
+struct RedEntry {
+  double khi, klo;  // k ln2_hi, RN(k ln2_lo)
+};
 struct TailEntry {
-  double a, b;
+  double a, b;  // A, B
 };
 constexpr int kTailLo = -3, kTailN = 68;  // k = -3 .. 64
+constexpr double kLn2Hi = 6.93147180369123816490e-01;
+constexpr double kLn2Lo = 1.90821492927058770002e-10;
+constexpr RedEntry red_entry(int k) { return RedEntry{(double)k * kLn2Hi, (double)k * kLn2Lo}; }
 constexpr TailEntry tail_entry(int k) {
   return TailEntry{(k == 0 || k == -1) ? 0.0                                    // A = 0
                    : (k >= 2 && k <= 19) ? 1.0 - 1.0 / (double)(1ull << k)     // 1 - 2^-k
@@ -171,11 +181,15 @@ constexpr TailEntry tail_entry(int k) {
 // Everything the exact functions look up: glibc's log table and the tails.
 struct ExTab {
   GlLogEntry log[1 << kGlTabBits];
+  RedEntry red[kTailN];
   TailEntry tail[kTailN];
 };
 constexpr ExTab make_ex_tab() {
-  ExTab t{{LDPC_GLIBC_LOG_TAB}, {}};
-  for (int k = kTailLo; k < kTailLo + kTailN; ++k) t.tail[k - kTailLo] = tail_entry(k);
+  ExTab t{{LDPC_GLIBC_LOG_TAB}, {}, {}};
+  for (int k = kTailLo; k < kTailLo + kTailN; ++k) {
+    t.red[k - kTailLo] = red_entry(k);
+    t.tail[k - kTailLo] = tail_entry(k);
+  }
   return t;
 }
 
@@ -184,7 +198,9 @@ constexpr ExTab make_ex_tab() {
 // (-2|x| for |x| < 1, 2|x| for 1 <= |x| < 22).  glibc 2.35 s_expm1.c:
 //   k = 0 if |u| <= 0.5 ln2 (by the high word), -1 if |u| < 1.5 ln2 (u < 0),
 //       else (int)(invln2 u +- 0.5);
-//   hi = u - k ln2_hi (exact product), lo = k ln2_lo, x = hi - lo,
+//   hi = u - k ln2_hi (exact product), lo = k ln2_lo, x = hi - lo
+//   (both products are table entries: hi is one subtraction, lo a load;
+//   at k = 0 they are +0.0, so x = u and c = 0 as glibc's k == 0 path),
 //   c = (hi - x) - lo; hfx = 0.5 x, hxs = x hfx;
 //   r1 = 1 + hxs Q1 + hxs^2 (Q2 + hxs Q3) + hxs^4 (Q4 + hxs Q5)  (this grouping);
 //   t = 3 - r1 hfx; e = hxs ((r1 - t) / (6 - x t));
@@ -208,12 +224,11 @@ constexpr ExTab make_ex_tab() {
 // ---------------------------------------------------------------------------
 // mid_possible: false if the caller knows every |u| < 13.5 (k <= 19), so
 // the k = 20..56 formula need not be checked for (tanh_half_n folds that
-// test into its own rare-case test).
+// test into its own rare-case test).  hx[i]: the high word of |u[i]|, or any
+// word that is above 0x3fd62e42 exactly when that one is.
 template <int n>
-LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n], const TailEntry *tail,
-                     bool mid_possible = true) {
-  constexpr double ln2_hi = 6.93147180369123816490e-01;
-  constexpr double ln2_lo = 1.90821492927058770002e-10;
+LDPC_HD void expm1_n(const double (&u)[n], const uint32_t (&hx)[n], double (&t)[n],
+                     const ExTab *tab, bool mid_possible = true) {
   constexpr double invln2 = 1.44269504088896338700e+00;
   constexpr double Q1 = -3.33333333333331316428e-02;
   constexpr double Q2 = 1.58730158725481460165e-03;
@@ -224,19 +239,17 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n], const TailEntry *tail
   int k[n];
 #pragma unroll
   for (int i = 0; i < n; ++i) {
-    const uint32_t hw = hiw(u[i]);
-    const uint32_t hx = hw & 0x7fffffffu, sgn = hw & 0x80000000u;
-    // k = (int)(invln2 * u + (u > 0 ? 0.5 : -0.5)), truncation toward zero;
-    // |k| <= 63 here, so the integral double has a zero low word and the
-    // choice of k is made on high words
-    // glibc takes k = -1 for hx in (0x3fd62e42, 0x3FF0A2B2) instead of this
-    // rounding, but on that range (u < 0 here) invln2 u - 0.5 lies in
-    // (-2, -1): kg is -1 there too.  Only k = 0 needs its own select.
-    const double kg = __builtin_trunc(invln2 * u[i] + from_hi(0x3fe00000u | sgn));
-    const double tk = from_hi(hx > 0x3fd62e42u ? hiw(kg) : 0u);
-    k[i] = (int)tk;
-    const double hi = fma_(-tk, ln2_hi, u[i]);  // tk * ln2_hi is exact (|k| <= 64)
-    const double lo = tk * ln2_lo;
+    const uint32_t sgn = hiw(u[i]) & 0x80000000u;
+    // k = (int)(invln2 * u + (u > 0 ? 0.5 : -0.5)), truncation toward zero
+    // (|k| <= 63 here).  glibc takes k = -1 for hx in (0x3fd62e42,
+    // 0x3FF0A2B2) instead of this rounding, but on that range (u < 0 here)
+    // invln2 u - 0.5 lies in (-2, -1): the conversion gives -1 there too.
+    // Only k = 0 needs its own select.
+    const int kc = (int)(invln2 * u[i] + from_hi(0x3fe00000u | sgn));
+    k[i] = hx[i] > 0x3fd62e42u ? kc : 0;
+    const RedEntry re = tab->red[k[i] - kTailLo];
+    const double hi = u[i] - re.khi;
+    const double lo = re.klo;
     x[i] = hi - lo;
     c[i] = (hi - x[i]) - lo;
     const double hfx = 0.5 * x[i];
@@ -260,8 +273,8 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n], const TailEntry *tail
     const double d = ep[i] - x[i];
     const int kk = k[i];
     // per-lane constants: A, B from the table (tail_entry), 2^k exact
-    const TailEntry te = tail[kk - kTailLo];
-    t[i] = fma_(te.a - d, __builtin_ldexp(1.0, kk), te.b);
+    const TailEntry te = tab->tail[kk - kTailLo];
+    t[i] = fma_(te.a - d, from_hi((uint32_t)(kk + 0x3ff) << 20), te.b);
     if (mid_possible) any_mid |= (uint32_t)(kk - 20) <= 36u;
   }
   if (mid_possible && LDPC_EX_ANY(any_mid)) {
@@ -276,6 +289,15 @@ LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n], const TailEntry *tail
       t[i] = (uint32_t)(kk - 20) <= 36u ? v : t[i];
     }
   }
+}
+
+template <int n>
+LDPC_HD void expm1_n(const double (&u)[n], double (&t)[n], const ExTab *tab,
+                     bool mid_possible = true) {
+  uint32_t hx[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) hx[i] = hiw(u[i]) & 0x7fffffffu;
+  expm1_n<n>(u, hx, t, tab, mid_possible);
 }
 
 // ---------------------------------------------------------------------------
@@ -301,17 +323,32 @@ LDPC_HD void tanh_half_n(const double (&m)[n], double (&z)[n], const ExTab *tab)
     // thresholds on |x| are thresholds on |m| one binade up
     hm[i] = hiw(m[i]);
     const uint32_t im = hm[i] & 0x7fffffffu;
-    // |m| clamped into [2^-54, 43] (NaN -> 2^-54): lanes outside glibc's
-    // expm1 range are replaced below, and any |m| >= 38.2 gives exactly 1,
-    // as glibc's 1 - tiny for |x| >= 22 (2 / (expm1(|m|) + 2) < 2^-54)
-    const double ac = __builtin_fmin(__builtin_fmax(__builtin_fabs(m[i]), 0x1p-54), 43.0);
     // u = |m| for |x| >= 1, else -|m|: the sign bit of im - bits(2.0)
-    u[i] = dbl(bits(ac) ^ ((uint64_t)((im - 0x40000000u) & 0x80000000u) << 32));
+    u[i] = dbl(((uint64_t)(im | ((im - 0x40000000u) & 0x80000000u)) << 32) | (uint32_t)bits(m[i]));
     // outside [2^-54, 13.5): |x| < 2^-55, inf, NaN, or possibly k >= 20
     special |= im - 0x3c900000u >= 0x402b0000u - 0x3c900000u;
   }
   const bool any_special = LDPC_EX_ANY(special);
-  expm1_n<n>(u, t, tab->tail, any_special);
+  if (any_special) {
+    LDPC_EX_COLD();
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      // |m| clamped into [2^-54, 43] (NaN -> 2^-54): lanes outside glibc's
+      // expm1 range are replaced below, and any |m| >= 38.2 gives exactly 1,
+      // as glibc's 1 - tiny for |x| >= 22 (2 / (expm1(|m|) + 2) < 2^-54)
+      const uint32_t im = hm[i] & 0x7fffffffu;
+      const double ac = __builtin_fmin(__builtin_fmax(__builtin_fabs(m[i]), 0x1p-54), 43.0);
+      u[i] = dbl(bits(ac) ^ ((uint64_t)((im - 0x40000000u) & 0x80000000u) << 32));
+    }
+  }
+  // im is the high word of |u| except on the clamped lanes, where it gives
+  // the same k: |m| < 2^-54 and 2^-54 are both below 0x3fd62e42, |m| > 43
+  // (inf) and 43 both above; a NaN is above, but its u = 2^-54 converts to
+  // k = 0 all the same
+  uint32_t hx[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) hx[i] = hm[i] & 0x7fffffffu;
+  expm1_n<n>(u, hx, t, tab, any_special);
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     const bool big = (hm[i] & 0x7fffffffu) >= 0x40000000u;  // |x| >= 1
@@ -323,7 +360,8 @@ LDPC_HD void tanh_half_n(const double (&m)[n], double (&z)[n], const ExTab *tab)
   for (int i = 0; i < n; ++i) {
     const bool big = (hm[i] & 0x7fffffffu) >= 0x40000000u;
     const double r = big ? 1.0 - q[i] : q[i];  // >= 0: the sign is x's (m's)
-    z[i] = dbl(bits(r) | ((uint64_t)(hm[i] & 0x80000000u) << 32));
+    const uint32_t zh = (hiw(r) & 0x7fffffffu) | (hm[i] & 0x80000000u);
+    z[i] = dbl(((uint64_t)zh << 32) | (uint32_t)bits(r));
   }
   if (any_special) {
     LDPC_EX_COLD();
@@ -435,10 +473,16 @@ LDPC_HD bool ratio_n(const double (&T)[n], double (&q)[n]) {
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     num[i] = 1.0 + T[i];
-    // 1 - T >= 2^-53 unless T = 1 or NaN: those divide by 2^-60 here (a
-    // finite quotient in the shared product) and are replaced by ratio_fix_n
-    den[i] = __builtin_fmax(1.0 - T[i], 0x1p-60);
+    den[i] = 1.0 - T[i];
     special |= !(__builtin_fabs(T[i]) < 1.0);  // T = +-1 (2/0, 0/2) or NaN
+  }
+  // 1 - T >= 2^-53 unless T = 1 or NaN: when some lane has one, every lane's
+  // divisor is raised to >= 2^-60 (a finite quotient in the shared product;
+  // the other lanes' divisors are unchanged) and ratio_fix_n replaces them
+  if (LDPC_EX_ANY(special)) {
+    LDPC_EX_COLD();
+#pragma unroll
+    for (int i = 0; i < n; ++i) den[i] = __builtin_fmax(den[i], 0x1p-60);
   }
   div_n<n>(num, den, q);
   return special;

@@ -51,7 +51,7 @@ void check_expm1(const double *u, int64_t n, int64_t *out) {
   for (int64_t i = 0; i + 3 <= n; i += 3) {
     const double v[3] = {u[i], u[i + 1], u[i + 2]};
     double t[3];
-    expm1_n<3>(v, t, kEx.tail);
+    expm1_n<3>(v, t, &kEx);
     for (int j = 0; j < 3; ++j) tally(t[j], expm1(v[j]), out);
   }
 }

@@ -59,7 +59,7 @@ def loops(lines):
     return out
 
 
-def hot_path(lines):
+def hot_path(lines, full=False):
     hot, i = [], 0
     while i < len(lines):
         l = lines[i]
@@ -80,8 +80,8 @@ def hot_path(lines):
                 continue
         hot.append(l)
         i += 1
-    return [l.split()[0] for l in hot
-            if l and not l.startswith((".", ";")) and not re.match(r"^\S+:", l)]
+    keep = [l for l in hot if l and not l.startswith((".", ";")) and not re.match(r"^\S+:", l)]
+    return keep if full else [l.split()[0] for l in keep]
 
 
 def main():
@@ -92,6 +92,7 @@ def main():
                     help="0: the loop with the most VALU that is not the frame loop")
     ap.add_argument("--json", default=None)
     ap.add_argument("--key", default=None)
+    ap.add_argument("--dump", default=None, help="write the hot path's instructions here")
     a = ap.parse_args()
     s = open(a.asm).read()
     m = re.search(r"^(\S*%s\S*):" % a.kernel, s, re.M)
@@ -108,6 +109,8 @@ def main():
                         for o in cand)]
     inner.sort(key=lambda c: -c[0])
     n, lo, hi, ins = inner[min(a.loop_rank, len(inner) - 1)]
+    if a.dump:
+        open(a.dump, "w").write("\n".join(hot_path(lines[lo:hi], full=True)) + "\n")
     c = collections.Counter(x for x in ins if x.startswith("v_"))
     cyc = {"f64": 0.0, "trans": 0.0, "other": 0.0}
     cnt = {"f64": 0, "trans": 0, "other": 0}
