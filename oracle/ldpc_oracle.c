@@ -716,9 +716,23 @@ void orc_block_init(orc_block *blk, int method, int iterations,
   blk->H = Hr;
 }
 
-int orc_block_general_work(orc_block *blk, int noutput_items,
-                           int ninput_items, const float *in_complex,
-                           uint8_t *out, int *consumed) {
+/* One window's decode and frame check for the loop below: dense H (the
+ * block's own, :155-166) or, for large codes, the sparse restatement of the
+ * same decoders (g != NULL).  Returns checkFrame's count. */
+static int block_decode_check(const orc_block *blk, const orc_graph *g, const int32_t *rp,
+                              const int32_t *ci, const double *tx, int *v) {
+  const int threshold = blk->M / 8; /* :142 */
+  if (g) {
+    orc_decode_graph(blk->method, g, tx, blk->iterations, 1, v, NULL);
+    return orc_check_frame_sparse(rp, ci, blk->M, v, threshold);
+  }
+  orc_decode(blk->method, blk->H, blk->M, blk->N, tx, blk->iterations, v, NULL);
+  return orc_check_frame(blk->H, blk->M, blk->N, v, threshold);
+}
+
+static int block_general_work(orc_block *blk, const orc_graph *g, const int32_t *rp,
+                              const int32_t *ci, int noutput_items, int ninput_items,
+                              const float *in_complex, uint8_t *out, int *consumed) {
   const int M = blk->M, N = blk->N;
   const int per_frame_out = M / 8;  /* :141 */
   const int threshold = M / 8;      /* :142 */
@@ -734,8 +748,7 @@ int orc_block_general_work(orc_block *blk, int noutput_items,
                  (float)(blk->state == ORC_STATE_IN_SYNC_INVERTED ? -1 : 1);
       tx[i] = (double)re;
     }
-    orc_decode(blk->method, blk->H, M, N, tx, blk->iterations, v, NULL);
-    int s = orc_check_frame(blk->H, M, N, v, threshold);
+    int s = block_decode_check(blk, g, rp, ci, tx, v);
     if (s > threshold) {
       if (blk->state == ORC_STATE_IN_SYNC ||
           blk->state == ORC_STATE_IN_SYNC_INVERTED) {
@@ -747,8 +760,7 @@ int orc_block_general_work(orc_block *blk, int noutput_items,
       }
       if (blk->state == ORC_STATE_OUT_OF_SYNC) { /* retry negated :178-199 */
         for (int i = 0; i < N; i++) ntx[i] = -tx[i];
-        orc_decode(blk->method, blk->H, M, N, ntx, blk->iterations, v, NULL);
-        if (orc_check_frame(blk->H, M, N, v, threshold) <= threshold) {
+        if (block_decode_check(blk, g, rp, ci, ntx, v) <= threshold) {
           blk->state = ORC_STATE_IN_SYNC_INVERTED;
           blk->errors = 0;
         } else {
@@ -777,5 +789,23 @@ int orc_block_general_work(orc_block *blk, int noutput_items,
   free(ntx);
   free(v);
   *consumed = used_in;
+  return made;
+}
+
+int orc_block_general_work(orc_block *blk, int noutput_items,
+                           int ninput_items, const float *in_complex,
+                           uint8_t *out, int *consumed) {
+  return block_general_work(blk, NULL, NULL, NULL, noutput_items, ninput_items, in_complex, out,
+                            consumed);
+}
+
+int orc_block_general_work_sparse(orc_block *blk, const int32_t *row_ptr, const int32_t *col_idx,
+                                  int noutput_items, int ninput_items, const float *in_complex,
+                                  uint8_t *out, int *consumed) {
+  orc_graph g;
+  orc_graph_build(&g, row_ptr, col_idx, blk->M, blk->N);
+  const int made = block_general_work(blk, &g, row_ptr, col_idx, noutput_items, ninput_items,
+                                      in_complex, out, consumed);
+  orc_graph_free(&g);
   return made;
 }

@@ -133,6 +133,11 @@ void orc_block_init(orc_block *blk, int method, int iterations,
 int orc_block_general_work(orc_block *blk, int noutput_items,
                            int ninput_items, const float *in_complex,
                            uint8_t *out, int *consumed);
+/* The same loop for a large code: every window decoded by the sparse
+ * restatement on CSR (row_ptr, col_idx); blk->H is unused (may be NULL). */
+int orc_block_general_work_sparse(orc_block *blk, const int32_t *row_ptr, const int32_t *col_idx,
+                                  int noutput_items, int ninput_items, const float *in_complex,
+                                  uint8_t *out, int *consumed);
 
 #ifdef __cplusplus
 }

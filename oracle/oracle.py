@@ -65,6 +65,9 @@ def lib():
         L.orc_block_general_work.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _f32p,
                                              _u8p, _i32p]
         L.orc_block_general_work.restype = ctypes.c_int
+        L.orc_block_general_work_sparse.argtypes = [ctypes.c_void_p, _i32p, _i32p, ctypes.c_int,
+                                                    ctypes.c_int, _f32p, _u8p, _i32p]
+        L.orc_block_general_work_sparse.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -196,12 +199,24 @@ class _OrcBlock(ctypes.Structure):
 class Block:
     """general_work restatement (lib/ldpc_decoder_cb_impl.cc:126-234)."""
 
-    def __init__(self, method, Hr, iterations=5):
-        self.H = np.ascontiguousarray(Hr, np.uint8)
-        M, N = self.H.shape
+    def __init__(self, method, Hr, iterations=5, csr=None):
+        """Hr: the reordered dense H; or csr = (M, N, row_ptr, col_idx) for a
+        large code, whose windows the sparse restatement decodes (the same
+        loop, orc_block_general_work_sparse)."""
+        self.csr = None
+        if csr is not None:
+            M, N, rp, ci = csr
+            self.csr = (np.ascontiguousarray(rp, np.int32), np.ascontiguousarray(ci, np.int32))
+            self.H = None
+            self.MN = (int(M), int(N))
+            hp = None
+        else:
+            self.H = np.ascontiguousarray(Hr, np.uint8)
+            self.MN = self.H.shape
+            hp = _p(self.H, _u8p)
+        M, N = self.MN
         self.s = _OrcBlock()
-        lib().orc_block_init(ctypes.byref(self.s), int(method), int(iterations),
-                             _p(self.H, _u8p), M, N)
+        lib().orc_block_init(ctypes.byref(self.s), int(method), int(iterations), hp, M, N)
 
     @property
     def state(self):
@@ -215,23 +230,30 @@ class Block:
         """in_complex: complex64 array (ninput_items long).  Returns
         (out_bytes, consumed)."""
         x = np.ascontiguousarray(in_complex, np.complex64).view(np.float32)
-        M, N = self.H.shape
+        M, N = self.MN
         bound = (x.size // 2) // N * (M // 8)  # each output frame consumes N
         noutput_items = min(int(noutput_items), bound)
         out = np.zeros(max(noutput_items, 1), np.uint8)
         used = ctypes.c_int32(0)
-        made = lib().orc_block_general_work(ctypes.byref(self.s), int(noutput_items),
-                                            int(x.size // 2), _p(x, _f32p), _p(out, _u8p),
-                                            ctypes.byref(used))
+        if self.csr is not None:
+            made = lib().orc_block_general_work_sparse(
+                ctypes.byref(self.s), _p(self.csr[0], _i32p), _p(self.csr[1], _i32p),
+                int(noutput_items), int(x.size // 2), _p(x, _f32p), _p(out, _u8p),
+                ctypes.byref(used))
+        else:
+            made = lib().orc_block_general_work(ctypes.byref(self.s), int(noutput_items),
+                                                int(x.size // 2), _p(x, _f32p), _p(out, _u8p),
+                                                ctypes.byref(used))
         return out[:made].copy(), used.value
 
 
-def run_stream(method, Hr, samples, iterations=5, chunks=None, out_space=1 << 30):
+def run_stream(method, Hr, samples, iterations=5, chunks=None, out_space=1 << 30, csr=None):
     """Feed a complex stream through the restated block the way the GR
     scheduler does: input arrives in `chunks` (sizes), unconsumed input is
     kept, and general_work is called again until it consumes nothing.
-    Returns the concatenated output bytes."""
-    blk = Block(method, Hr, iterations)
+    Returns the concatenated output bytes.  csr: a large code's (M, N,
+    row_ptr, col_idx) instead of Hr (sparse window decodes)."""
+    blk = Block(method, Hr, iterations, csr=csr)
     samples = np.asarray(samples, np.complex64)
     ends = list(np.cumsum(chunks)) if chunks is not None else []
     ends = [min(int(e), len(samples)) for e in ends] + [len(samples)]

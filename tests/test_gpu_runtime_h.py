@@ -207,3 +207,40 @@ def test_decode_windows_rejects_out_of_span():
     cx = np.zeros(2 * 100, np.float32)
     with pytest.raises(L.LdpcError):
         dec.decode_windows(cx, np.array([(40 << 1)], np.int64), elem_stride=2)  # 40 + 64 > 100
+
+
+def _ira_code():
+    """A quasi-cyclic IRA code of the config-4 family at N = 720 (the
+    large-code kernels: N > 256), [parity | info] as the block emits it."""
+    t = codes.dvbs2_like_table(3, K=360, N=720, hi_groups=1, hi_deg=6, lo_deg=3)
+    return codes.ira_from_table(t, 360, 720)
+
+
+@pytest.mark.parametrize("method,ebn0,garbage", [(0, 2.0, True), (1, 4.0, False)])
+def test_block_large_csr_stream(method, ebn0, garbage):
+    """The block on a large runtime H given as CSR (the min-sum frame pipeline
+    / the sum-product graph passes, window limits sized by N): a misaligned
+    start, frames, [3 frames of noise then frames off the old grid: 11
+    errors, a sync loss and an N-position search,] a polarity flip -- the
+    bytes of the restated general_work decoding every window with the sparse
+    restatement (orc_block_general_work_sparse)."""
+    from oracle import oracle as orc
+    csr = _ira_code()
+    M, N, rp, ci = csr
+    rng = np.random.default_rng(40 + method)
+    x = 2.0 * codes.ira_encode(csr, rng.integers(0, 2, size=(36, N - M), dtype=np.uint8)) - 1.0
+    x = (x + np.sqrt(10 ** (-ebn0 / 10)) * rng.standard_normal(x.shape)).astype(np.float32)
+    parts = [rng.standard_normal(5).astype(np.float32), x[:18].ravel()]
+    if garbage:
+        parts.append(rng.standard_normal(3 * N + 5).astype(np.float32))
+    parts.append(-x[18:].ravel())
+    s = np.concatenate(parts).astype(np.complex64)
+    exp = orc.run_stream(method, None, s, iterations=5, csr=csr)
+    assert len(exp) >= 10 * (M // 8)
+    blk = L.ldpc_decoder_cb(method, iterations=5, csr=csr)
+    assert (blk.M, blk.N) == (M, N)
+    tb = fg.top_block(chunk=[N * 7 + 3, 999, N * 20] * 4, out_space=M // 8 * 5)
+    src, dst = fg.vector_source_c(s), fg.vector_sink_b()
+    tb.connect(src, blk, dst)
+    tb.run()
+    assert (dst.array() == exp).all()

@@ -203,3 +203,18 @@ def test_et_period_stops_only_on_period(golden):
         o1c = orc.decode_batch(m, Hr, y, 50, nthreads=4)
         for k in ("bits", "iters", "synd"):
             assert (o1[k] == o1c[k]).all()
+
+
+@pytest.mark.parametrize("name", ["offset", "burst"])
+def test_sparse_block_restatement_matches_dense(golden, name):
+    """orc_block_general_work_sparse (the loop with every window decoded by
+    the sparse restatement, for large codes) gives the dense block's bytes --
+    and the fixtures' -- on the default H."""
+    st = golden("streams.npz")
+    Hr = golden("frames_default.npz")["H_reordered"]
+    rp, ci = orc.dense_to_csr(Hr)
+    s = st[name + "_in"]
+    for m in (0, 1, 2, 3):
+        sp = orc.run_stream(m, None, s, iterations=5, csr=(Hr.shape[0], Hr.shape[1], rp, ci),
+                            chunks=[700, 33, 5000] * 40)
+        assert (sp == st["%s_m%d_out" % (name, m)]).all(), m
