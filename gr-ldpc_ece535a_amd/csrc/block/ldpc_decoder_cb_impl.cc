@@ -67,9 +67,8 @@ namespace {
 // Per launch at most kWindowSamples samples of windows (1 << 17 windows of
 // the reference's N = 64; a DVB-S2-size code gets ~130), which bounds the
 // staging memory and the launch for any N; the out-of-sync search starts
-// with at most kSearchFirst positions and widens x4 per launch.
+// with at most d_search_first (128) positions and widens x4 per launch.
 const int64_t kWindowSamples = (int64_t)64 << 17;
-const int kSearchFirst = 128;
 int max_windows(unsigned N) {
   return (int)std::max<int64_t>(16, std::min<int64_t>((int64_t)1 << 17, kWindowSamples / (int64_t)N));
 }
@@ -357,6 +356,13 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       const bool on_grid = d_anchor < 0 || (d_abs + pos) % N == d_anchor;
       pass = d_anchor_guess ? (on_grid && (r.state != STATE_OUT_OF_SYNC || d_anchor >= 0))
                             : r.state != STATE_OUT_OF_SYNC;
+      // the same samples known to pass at the other polarity: this one fails
+      // (the complement of a codeword leaves every odd-weight row unsatisfied:
+      // 20 of the default H's 32)
+      if (pass && d_opposite) {
+        const int32_t o = d_memo[pol ^ 1][pos];
+        if (o >= 0 && d_rsynd[o] <= thr) pass = false;
+      }
       guessed_out = !pass;
       // a frame in sync is also wanted at the other polarity when its result
       // decides a sync loss's "-tx" retry (:178-187)
@@ -458,7 +464,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   d_rpacked.clear();
 
   Replay r{d_state, d_errors, 0, 0};
-  const int search_first = std::min(kSearchFirst, max_windows(d_N));
+  const int search_first = std::min(std::max(d_search_first, 1), max_windows(d_N));
   int out_budget = search_first;  // out-of-sync positions one launch may guess past
   bool first = true, last_out = false;
   double t0 = d_profile ? now_s() : 0.0;

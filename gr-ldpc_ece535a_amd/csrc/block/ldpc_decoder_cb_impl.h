@@ -60,6 +60,13 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   // after such a false sync move, yet a limit of 1 or 2 costs more launches
   // than the windows it saves (tools/block_policy_sim.py)
   int d_searches = getenv("LDPC_BLOCK_SEARCHES") ? atoi(getenv("LDPC_BLOCK_SEARCHES")) : 0;
+  // out-of-sync positions a dry run may guess past in a row before the launch
+  // (LDPC_BLOCK_SEARCH_FIRST, default 128; x4 per launch while the search goes on)
+  int d_search_first = getenv("LDPC_BLOCK_SEARCH_FIRST") ? atoi(getenv("LDPC_BLOCK_SEARCH_FIRST"))
+                                                         : 128;
+  // A/B knob: LDPC_BLOCK_OPPOSITE=0 ignores, when guessing a window, that the
+  // same samples at the other polarity are known to pass
+  bool d_opposite = !(getenv("LDPC_BLOCK_OPPOSITE") && getenv("LDPC_BLOCK_OPPOSITE")[0] == '0');
   // windows a launch is filled up to with branch speculation (LDPC_BLOCK_BUDGET)
   int d_budget = getenv("LDPC_BLOCK_BUDGET") ? atoi(getenv("LDPC_BLOCK_BUDGET")) : 3072;
   // grid: absolute sample index of the call's first input item; the phase

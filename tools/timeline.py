@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--launches", type=int, default=0,
                     help="instead: run this many launches from a cold process and print the span "
                          "and median in-kernel clock of selected ones (warmup behaviour)")
+    ap.add_argument("--steady", type=int, default=0,
+                    help="instead: K steps of the bench's throughput setting (4 batches in flight, "
+                         "launch mode 1) after 300 warm ones; print the in-kernel clock of the "
+                         "last frames recorded")
     a = ap.parse_args()
     import torch  # first: one HIP runtime
     import bench  # noqa: E402  (sets sys.path from LDPC_PKG_DIR)
@@ -47,6 +51,21 @@ def main():
     B = a.batch
     buf = np.zeros(4 * B, np.uint64)
     lib.ldpc_debug_timeline.restype = ctypes.c_int
+    if a.steady:
+        dec.set_launch_mode(1)
+        ins = [torch.from_numpy(bench.synth(dec.H, B, a.ebn0, 2024 + j)[0]).cuda() for j in range(4)]
+        for k, steps in (("warm", 300), ("steady", a.steady)):
+            r = bench.time_decoder(dec, torch, ins, B, a.method, 50, a.et, a.precision, steps, 10,
+                                   inflight=4)
+            torch.cuda.synchronize()
+            assert lib.ldpc_debug_timeline(buf.ctypes.data_as(ctypes.c_void_p), B) == B
+            t = buf.reshape(B, 4)
+            dur = np.maximum((t[:, 1] - t[:, 0]).astype(np.float64) / 100.0, 1e-3)
+            clk = t[:, 3] / dur / 1e3
+            print("%s: %d steps, %.1f Mbit/s, in-kernel clock GHz median %.3f p5 %.3f p95 %.3f" % (
+                k, steps, B * dec.K * steps / r["wall"] / 1e6, np.median(clk),
+                np.percentile(clk, 5), np.percentile(clk, 95)), flush=True)
+        return
     if a.launches:
         show = {0, 1, 2, 5, 10, 20, 50, 100, 150, 200, 300, 400, 600, 800}
         for i in range(a.launches):
