@@ -260,23 +260,26 @@ __device__ void decide_chunk(MsWork w, int k, int max_iters, int et_period, int 
 
 // One block per chunk.  (Deciding in ms_check's last block instead needs
 // agent-scope fences in every block, which write back the XCD's L2: slower.)
-__global__ void __launch_bounds__(256) ms_decide(MsWork w, int max_iters, int et_period, int B,
-                                                 int32_t *synd) {
+constexpr int kDecideThreads = 1024;  // the OR over ~4 000 check waves' words: 4 loads each
+__global__ void __launch_bounds__(kDecideThreads) ms_decide(MsWork w, int max_iters, int et_period,
+                                                            int B, int32_t *synd) {
   decide_chunk(w, blockIdx.x, max_iters, et_period, B, synd);
 }
 
-// One 256-thread block per chunk.  A running slot that has executed `it`
-// iterations stops at the cap, or -- min-sum's rule (:406-408) -- when
-// it < cap, it % et_period == 0 and its decision satisfies every check.
-// Freed (and empty) slots take the next frames of the batch in lane order.
-// (256 threads)
+// One kDecideThreads-thread block per chunk.  A running slot that has
+// executed `it` iterations stops at the cap, or -- min-sum's rule (:406-408)
+// -- when it < cap, it % et_period == 0 and its decision satisfies every
+// check.  Freed (and empty) slots take the next frames of the batch in lane
+// order.
 __device__ void decide_chunk(MsWork w, int k, int max_iters, int et_period, int B, int32_t *synd) {
-  __shared__ uint64_t part[4];
+  constexpr int kWaves = kDecideThreads / 64;
+  __shared__ uint64_t part[kWaves];
   const int lane = threadIdx.x & 63;
   const int64_t chunks = w.chunks;
   uint64_t odd = 0;
   if (w.live_w[k])
-    for (int i = threadIdx.x; i < w.check_waves; i += 256) odd |= w.odd[(int64_t)i * chunks + k];
+    for (int i = threadIdx.x; i < w.check_waves; i += kDecideThreads)
+      odd |= w.odd[(int64_t)i * chunks + k];
   for (int off = 32; off > 0; off >>= 1) {
     const uint32_t lo = __shfl_xor((uint32_t)odd, off), hi = __shfl_xor((uint32_t)(odd >> 32), off);
     odd |= ((uint64_t)hi << 32) | lo;
@@ -284,7 +287,9 @@ __device__ void decide_chunk(MsWork w, int k, int max_iters, int et_period, int 
   if (lane == 0) part[threadIdx.x >> 6] = odd;
   __syncthreads();
   if (threadIdx.x >= 64) return;
-  odd = part[0] | part[1] | part[2] | part[3];
+  odd = 0;
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) odd |= part[i];
   const int slot = k * 64 + lane;
   const int it = w.it[slot], f = w.frame[slot];
   const bool running = f >= 0;
@@ -375,11 +380,21 @@ __global__ void __launch_bounds__(256) ms_flush_cols(GraphView g, MsWork w, uint
   }
 }
 
+__device__ void flush_synd_rows(const GraphView &g, const MsWork &w, int32_t *synd, int bx, int k);
+
 // Uncapped syndrome weight of the frames that stopped at the cap with
-// unsatisfied checks (added to the zero decide_chunk wrote).
-__device__ void flush_synd(const GraphView &g, const MsWork &w, int32_t *synd, int bx, int k) {
+// unsatisfied checks (added to the zero decide_chunk wrote).  nb blocks per
+// chunk stride over the check waves' row groups: a pass where no frame
+// stopped at the cap (most) costs nb near-empty blocks, not one per group.
+__device__ void flush_synd(const GraphView &g, const MsWork &w, int32_t *synd, int bx, int nb,
+                           int k) {
   const uint64_t sel = w.cap_w[k];
   if (!sel || !synd) return;
+  for (int grp = bx; grp < w.check_waves / 4; grp += nb) flush_synd_rows(g, w, synd, grp, k);
+}
+
+__device__ void flush_synd_rows(const GraphView &g, const MsWork &w, int32_t *synd, int bx, int k) {
+  const uint64_t sel = w.cap_w[k];
   const int lane = threadIdx.x & 63;
   const int64_t chunks = w.chunks;
   const int j0 = (bx * 4 + wave_id()) * kMsRows;
@@ -412,7 +427,7 @@ __global__ void __launch_bounds__(256) ms_post(GraphView g, MsWork w, DecodeArgs
   if ((int)blockIdx.x < nb_flush)
     flush_packed(g, w, a, blockIdx.x, k);
   else
-    flush_synd(g, w, a.synd, blockIdx.x - nb_flush, k);
+    flush_synd(g, w, a.synd, blockIdx.x - nb_flush, (int)gridDim.x - nb_flush, k);
 }
 
 // Vertical step (:379-403) for the running slots: L(r_ji) of every edge of
@@ -544,10 +559,11 @@ void ms_pass(const GraphView &g, const MsWork &w, const DecodeArgs &a, int metho
     ms_check<PREC, 16><<<rgrid, 256, 0, st>>>(g, w);
   else
     ms_check<PREC, 32><<<rgrid, 256, 0, st>>>(g, w);
-  ms_decide<<<w.chunks, 256, 0, st>>>(w, method_iters, a.et_period, a.B, a.synd);
+  ms_decide<<<w.chunks, kDecideThreads, 0, st>>>(w, method_iters, a.et_period, a.B, a.synd);
   if (a.bits || (a.llr && w.post)) ms_flush_cols<<<tgrid, 256, 0, st>>>(g, w, a.bits, a.llr);
   const int nb_flush = (g.KB + 63) / 64;
-  ms_post<<<dim3(nb_flush + w.check_waves / 4, w.chunks), 256, 0, st>>>(g, w, a, nb_flush);
+  const int nb_synd = std::min(64, std::max(1, w.check_waves / 4));
+  ms_post<<<dim3(nb_flush + nb_synd, w.chunks), 256, 0, st>>>(g, w, a, nb_flush);
   if (g.dv_max <= 4)
     ms_var_fill<Real, 4><<<cgrid, 256, 0, st>>>(g, w, a);
   else if (g.dv_max <= 8)
