@@ -56,7 +56,11 @@ struct ldpc_ctx {
   int64_t *h_win = nullptr;
   size_t h_win_bytes = 0;
   int64_t span_samples = 0;
-  bool ms_pipeline = true;    // large-code min-sum: compressed messages + pipeline
+  // large-code min-sum: 2 narrow-chunk pipeline (ldpc_graph_msn.hip), 1 the
+  // 64-frame-chunk pipeline (ldpc_graph_ms.hip), 0 the edge-message passes
+  int ms_mode = 2;
+  ldpc::MsnTables msn;  // storage order of the narrow pipeline
+  int32_t *d_msn[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   // small-code frame queues: one monotonic counter per stream that has
   // launched on this context (ldpc_kernels.hpp DecodeArgs::ticket)
   uint32_t *d_tickets = nullptr;
@@ -496,7 +500,49 @@ ldpc::CodeView code_view(const ldpc_ctx *ctx) {
 int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int precision, void *st) {
   const ldpc::GraphView g = graph_view(ctx);
   const bool want_post = a.llr != nullptr;
-  if (method == 0 && ctx->ms_pipeline) {
+  if (method == 0 && ctx->ms_mode == 2) {
+    // min-sum: narrow chunks, gathered state L2-resident per XCD
+    ldpc::MsnView v;
+    v.rp = ctx->d_msn[0];
+    v.cp = ctx->d_msn[1];
+    v.rcs = ctx->d_msn[2];
+    v.crs = ctx->d_msn[3];
+    v.corig = ctx->d_msn[4];
+    v.cpos = ctx->d_msn[5];
+    v.M = g.M;
+    v.N = g.N;
+    v.E = g.E;
+    v.KB = g.KB;
+    v.dc_max = g.dc_max;
+    v.dv_max = g.dv_max;
+    v.out_var = ctx->msn.out_var && !getenv("LDPC_MSN_POST") ? 1 : 0;
+    int C = ldpc::msn_default_chunks();
+    const int need_c = (a.B + ldpc::kMsnFrames - 1) / ldpc::kMsnFrames;
+    if (need_c < C) C = need_c >= 8 ? (need_c + 7) / 8 * 8 : need_c;
+    const size_t need = ldpc::msn_work_bytes(v, C, precision);
+    if (need > ctx->work_bytes) {
+      if (ctx->d_work) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ctx->d_work);
+        ctx->d_work = nullptr;
+        ctx->work_bytes = 0;
+      }
+      hipError_t e = hipMalloc(&ctx->d_work, need);
+      if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(graph workspace)");
+      ctx->work_bytes = need;
+    }
+    if (!ctx->h_ctrl) {
+      hipError_t e = hipHostMalloc((void **)&ctx->h_ctrl, 64, hipHostMallocDefault);
+      if (e != hipSuccess) return hip_err(ctx, e, "hipHostMalloc(ctrl)");
+    }
+    ldpc::MsnWork w;
+    ldpc::msn_work_carve(w, ctx->d_work, v, C, precision);
+    const int rc = ldpc::launch_graph_decode_msn(v, w, a, precision, ctx->h_ctrl, st);
+    if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "code degrees outside the large-code kernels");
+    if (rc != 0) return hip_err(ctx, hipGetLastError(), "graph kernel launch");
+    return LDPC_OK;
+  }
+  if (method == 0 && ctx->ms_mode == 1) {
     // min-sum: compressed check messages, frames pipelined through S slots
     const int S = std::min(ldpc::ms_default_slots(), (a.B + 63) / 64 * 64);
     const size_t need = ldpc::ms_work_bytes(g, S, precision, want_post);
@@ -846,9 +892,13 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     return nullptr;
   }
   ctx->device = device;
-  {  // A/B knob: LDPC_MS_PIPELINE=0 keeps large-code min-sum on the edge-message passes
+  {  // A/B knob: LDPC_MS_PIPELINE=0 edge-message passes, 1 the 64-frame-chunk
+     // pipeline, 2 (default) the narrow-chunk pipeline
     const char *v = getenv("LDPC_MS_PIPELINE");
-    ctx->ms_pipeline = !(v && v[0] == '0');
+    ctx->ms_mode = v && v[0] >= '0' && v[0] <= '2' ? v[0] - '0' : 2;
+    // the narrow pipeline packs a row and an edge's place in it in 32 bits
+    if (ctx->graph && ctx->ms_mode == 2 && (ctx->M >= (1 << 24) || ctx->dc_max > 128)) ctx->ms_mode = 1;
+    if (ctx->graph && ctx->ms_mode == 2) ldpc::msn_build(ctx->M, ctx->N, ctx->rp, ctx->ci, ctx->msn);
   }
   const char *what = nullptr;
   if ((e = hipSetDevice(device)) != hipSuccess) what = "hipSetDevice";
@@ -860,6 +910,11 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     upload(ctx, &ctx->d_cp, cp, "upload(col_ptr)", what, e);
     upload(ctx, &ctx->d_ce, ce, "upload(col_edges)", what, e);
     upload(ctx, &ctx->d_cr, cr, "upload(col_rows)", what, e);
+    if (ctx->ms_mode == 2) {
+      const std::vector<int32_t> *t[6] = {&ctx->msn.rp,  &ctx->msn.cp,    &ctx->msn.rcs,
+                                          &ctx->msn.crs, &ctx->msn.corig, &ctx->msn.cpos};
+      for (int i = 0; i < 6; ++i) upload(ctx, &ctx->d_msn[i], *t[i], "upload(storage order)", what, e);
+    }
   } else {
     upload(ctx, &ctx->d_erow, erecs, "upload(erow)", what, e);
     upload(ctx, &ctx->d_ecol, crecs, "upload(ecol)", what, e);
@@ -943,6 +998,8 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->h_win) (void)hipHostFree(ctx->h_win);
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
+    if (p) (void)hipFree(p);
+  for (int32_t *p : ctx->d_msn)
     if (p) (void)hipFree(p);
   if (ctx->d_work) {
     (void)hipDeviceSynchronize();  // graph decodes may run on caller streams

@@ -16,6 +16,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "ldpc_kernels.hpp"
 
 namespace ldpc {
@@ -99,6 +101,61 @@ struct MsWork {
   uint64_t *live_w, *run_w, *stop_w, *fill_w, *cap_w;  // per-chunk lane masks
   int32_t *ctrl;     // [0] next frame of the batch, [1] frames finished
 };
+
+// ---- min-sum with the gathered state in one XCD's L2 (ldpc_graph_msn.hip):
+// chunks of kMsnFrames frames, XCD-aware chunk placement, storage order ------
+#ifndef LDPC_MSN_FRAMES
+#define LDPC_MSN_FRAMES 4
+#endif
+constexpr int kMsnFrames = LDPC_MSN_FRAMES;
+
+// H in storage order: rows and columns renumbered (rpos / cpos), each row's
+// edges still in ascending original column, each column's in ascending
+// original row.
+struct MsnView {
+  const int32_t *rp;     // M + 1: row offsets (storage rows; degrees)
+  const int32_t *cp;     // N + 1: column offsets (storage columns; degrees)
+  const int32_t *rcs;    // dc_max x M: [t][p] storage column of row p's t-th edge
+  const int32_t *crs;    // dv_max x N: [t][x] storage row of column x's t-th edge
+                         //   | its place in that row << 24
+  const int32_t *corig;  // N: original column of a storage column
+  const int32_t *cpos;   // N: storage column of an original column
+  int M, N, E, KB, dc_max, dv_max;
+  int out_var;           // outputs written by the variable pass (MsnTables::out_var)
+};
+
+struct MsnTables {  // host copies of MsnView's arrays
+  std::vector<int32_t> rp, cp, rcs, crs, corig, cpos;  // rcs / crs: -1 past the degree
+  int order = 0;         // 0 identity, 1 DVB-S2 residue classes
+  bool out_var = false;  // info columns in place and M % 8 == 0
+};
+
+struct MsnWork {
+  int S, chunks, nb_check, nb_var, check_waves, real_bytes, out_var;
+  float *L;          // chunks x N x F: Lci = -tx
+  void *LQ;          // chunks x N x F Real: Lci + sum of the column's L(r)
+  void *m1, *m2;     // chunks x M x F Real
+  uint8_t *meta;     // chunks x M x F: (P + 1) << 6 | (i1 + 1)
+  uint8_t *alpha;    // chunks x dc_max x M ([t][p]): bit 2f L(q) < 0, bit 2f+1 sign 0
+  uint8_t *odd;      // chunks x check_waves: frames with an unsatisfied row
+  int32_t *capsyn;   // S: syndrome weight of a frame stopping at the cap
+  int32_t *it;       // S: iterations the slot's frame has executed
+  int32_t *frame;    // S: the slot's frame (-1: empty); a refill's new frame after decide
+  int32_t *out_frame;  // S: the frame that stopped in this pass
+  int32_t *used;     // S: iterations of that frame
+  uint32_t *live, *run, *stop, *fill;  // per chunk: F-bit slot masks
+  int32_t *ctrl;     // [0] next frame of the batch, [1] frames finished
+};
+
+void msn_build(int M, int N, const std::vector<int32_t> &rp, const std::vector<int32_t> &ci,
+               MsnTables &t);
+void msn_tables(int M, int N, const std::vector<int32_t> &rp0, const std::vector<int32_t> &ci0,
+                const std::vector<int32_t> &rpos, const std::vector<int32_t> &cpos, MsnTables &t);
+int msn_default_chunks();
+size_t msn_work_bytes(const MsnView &g, int chunks, int prec);
+void msn_work_carve(MsnWork &w, void *base, const MsnView &g, int chunks, int prec);
+int launch_graph_decode_msn(const MsnView &g, const MsnWork &w, const DecodeArgs &args, int prec,
+                            int32_t *h_ctrl, void *stream);
 
 int ms_default_slots();
 size_t ms_work_bytes(const GraphView &g, int S, int prec, bool want_post);

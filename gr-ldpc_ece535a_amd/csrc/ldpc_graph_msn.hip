@@ -1,0 +1,652 @@
+// ldpc_graph_msn.hip -- large-code min-sum with the
+// gathered state kept in one XCD's L2.
+//
+// Same arithmetic as ldpc_graph_ms.hip (the reference's horizontal and
+// vertical steps, lib/ldpc_decoder_cb_impl.cc:340-403, with a row's L(r)
+// recovered exactly from {m1, m2, i1, P} and a 2-bit alpha per edge), laid
+// out for the cache hierarchy instead of for one wave per 64 frames:
+//
+// * Narrow chunks.  A chunk holds F = 4 frames (element x of frame f at
+//   (k * n + x) * F + f), so the tables a pass gathers from -- LQ in the check
+//   pass (8 N F bytes = 2.1 MB for N = 64800), the row state {m1, m2, meta}
+//   in the variable pass (17 M F = 2.2 MB) -- fit one XCD's 4 MiB L2.  With
+//   64-frame chunks they were 33-35 MB, every gather went to the Infinity
+//   Cache (~8 TB/s) and the passes moved 8.4 MB per frame-iteration.
+// * XCD-aware placement.  Workgroup b runs on XCD b mod 8; chunk k's blocks
+//   are the ones with b mod 8 == k mod 8, in chunk order, so each XCD works
+//   through its chunks one after another and a chunk's table is gathered
+//   by the CUs whose L2 holds it.
+// * Storage order.  Rows and columns are stored in an order chosen on the
+//   host (ldpc_msn_build): for codes with the DVB-S2 structure (IRA, 360-
+//   column groups, row r = x + s q mod M) rows by residue class mod q, which
+//   makes every circulant a shifted identity, so the 16 rows of a wave read
+//   16 consecutive columns for each of their edges and the 16 columns of a
+//   wave read 16 consecutive rows -- 512 contiguous bytes per wave
+//   instruction.  The arithmetic still visits a row's edges in ascending
+//   original column and a column's edges in ascending original row (the
+//   reference's scan order); the order only moves where values are stored.
+// * A lane is (item, frame): 16 rows / columns x 4 frames per wave.  The
+//   decisions are the signs of LQ (vhat = LQ < 0, :398-402), so the check
+//   pass forms the parities of the last decisions from the LQ values it
+//   gathers anyway (no separate hard-decision array), and outputs (packed
+//   bytes, bits, posteriors = (float) LQ) are read from LQ when a frame stops.
+// * The uncapped syndrome weight of a frame stopped at the cap is counted by
+//   the check pass of its last pass (atomic adds per wave, only at the cap).
+//
+// Per pass: msn_check -> msn_decide -> msn_post (packed bytes, iterations;
+// msn_cols for bits / posteriors) -> msn_var.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "ldpc_device.hpp"
+#include "ldpc_graph.hpp"
+
+namespace ldpc {
+namespace {
+
+constexpr int kF = kMsnFrames;  // frames per chunk
+constexpr int kIB = 256;        // rows / columns per 256-thread block (one per lane)
+static_assert(kF == 2 || kF == 4, "frames per chunk: 2 or 4");
+
+// Workgroup b -> (chunk, block of the chunk).  With a multiple of 8 chunks,
+// chunk k's blocks run on XCD k mod 8 (the dispatcher deals workgroups to the
+// XCDs round robin), the XCD's chunks one after another.
+__device__ __forceinline__ void map_block(int b, int chunks, int nbpc, int &k, int &bi) {
+  if ((chunks & 7) == 0) {
+    const int idx = b >> 3, c = idx / nbpc;
+    bi = idx - c * nbpc;
+    k = (b & 7) + 8 * c;
+  } else {
+    k = b / nbpc;
+    bi = b - k * nbpc;
+  }
+}
+
+__device__ __forceinline__ int64_t el(int k, int n, int x) { return ((int64_t)k * n + x) * kF; }
+
+// F consecutive values (one vector load / store)
+template <typename Real>
+struct Vec {
+  Real v[kF];
+};
+template <typename Real>
+__device__ __forceinline__ Vec<Real> ldv(const Real *p) {
+  return *(const Vec<Real> *)p;
+}
+template <typename Real>
+__device__ __forceinline__ void stv(Real *p, const Vec<Real> &x) {
+  *(Vec<Real> *)p = x;
+}
+typedef uint32_t MetaWord;  // F meta bytes (F <= 4)
+__device__ __forceinline__ MetaWord ld_meta(const uint8_t *p) {
+  if constexpr (kF == 4) return *(const uint32_t *)p;
+  else return *(const uint16_t *)p;
+}
+__device__ __forceinline__ void st_meta(uint8_t *p, MetaWord m) {
+  if constexpr (kF == 4) *(uint32_t *)p = m;
+  else *(uint16_t *)p = (uint16_t)m;
+}
+
+// alpha of an edge for frame f from the chunk's byte: bit 2f L(q) < 0, bit
+// 2f+1 sign 0 (:338, sign(0) = sign(NaN) = 0)
+__device__ __forceinline__ int alpha_of(uint32_t byte, int f) {
+  const uint32_t b = byte >> (2 * f);
+  return (b & 2u) ? 0 : ((b & 1u) ? -1 : 1);
+}
+
+// ---------------------------------------------------------------------------
+// Horizontal step (:340-376), one row per lane, the chunk's F frames in the
+// lane.  L(q) of each edge is LQ - L(r_old) (:387-392); a frame's first step
+// takes L(q) = Lci (LQ = Lci, no old message).  The parity of the last
+// decisions (checkFrame, :236-253) comes from the signs of the same LQ.
+// Frames whose slot is not live compute on stale values nobody reads.
+template <int PREC, int DC>
+__global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int max_iters) {
+  typedef typename Math<PREC>::Real Real;
+  int k, bi;
+  map_block(blockIdx.x, w.chunks, w.nb_check, k, bi);
+  const uint32_t live = w.live[k];
+  if (!live) return;
+  const int p = bi * kIB + threadIdx.x;  // row storage position
+  int itf[kF];
+#pragma unroll
+  for (int f = 0; f < kF; ++f) itf[f] = w.it[k * kF + f];
+  bool par[kF];
+#pragma unroll
+  for (int f = 0; f < kF; ++f) par[f] = false;
+  if (p < g.M) {
+    // the row's edges: rcs[t][p] >= 0 for t < degree, -1 after (one load
+    // level less than reading the degree first)
+    int cs[DC];
+#pragma unroll
+    for (int t = 0; t < DC; ++t) cs[t] = t < g.dc_max ? g.rcs[(int64_t)t * g.M + p] : -1;
+    Real *m1 = (Real *)w.m1, *m2 = (Real *)w.m2;
+    const Real *LQ = (const Real *)w.LQ;
+    const int64_t ro = el(k, g.M, p);
+    const Vec<Real> om1 = ldv(m1 + ro), om2 = ldv(m2 + ro);
+    const MetaWord omt = ld_meta(w.meta + ro);
+    uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M + p;  // [t][p]
+    Real q[kF][DC];
+#pragma unroll
+    for (int t = 0; t < DC; ++t) {
+#pragma unroll
+      for (int f = 0; f < kF; ++f) q[f][t] = Real(0);
+      if (cs[t] >= 0) {
+        const Vec<Real> lq = ldv(LQ + el(k, g.N, cs[t]));
+        const uint32_t ab = alpha[(int64_t)t * g.M];
+#pragma unroll
+        for (int f = 0; f < kF; ++f) {
+          par[f] ^= lq.v[f] < Real(0);
+          const int mt = (int)((omt >> (8 * f)) & 0xffu);
+          const int oP = (mt >> 6) - 1, oi1 = (mt & 63) - 1;
+          const Real r = itf[f] == 0 ? Real(0)
+                                     : (Real)(oP * alpha_of(ab, f)) * (t == oi1 ? om2.v[f] : om1.v[f]);
+          q[f][t] = lq.v[f] - r;
+        }
+      }
+    }
+    // sign product, smallest and second smallest |L(q)| (strict <, first
+    // occurrence, DBL_MAX seeds; NaN never passes)
+    Vec<Real> n1, n2;
+    MetaWord nmt = 0;
+#pragma unroll
+    for (int f = 0; f < kF; ++f) {
+      int P = 1, i1 = -1;
+      Real a1 = Math<PREC>::max_(), a2 = Math<PREC>::max_();
+#pragma unroll
+      for (int t = 0; t < DC; ++t)
+        if (cs[t] >= 0) {
+          P *= sgn(q[f][t]);
+          const Real a = Math<PREC>::abs_(q[f][t]);
+          if (a < a1) {
+            a2 = a1;
+            a1 = a;
+            i1 = t;
+          } else if (a < a2) {
+            a2 = a;
+          }
+        }
+      n1.v[f] = a1;
+      n2.v[f] = a2;
+      nmt |= (MetaWord)(((P + 1) << 6) | (i1 + 1)) << (8 * f);
+    }
+    stv(m1 + ro, n1);
+    stv(m2 + ro, n2);
+    st_meta(w.meta + ro, nmt);
+#pragma unroll
+    for (int t = 0; t < DC; ++t)
+      if (cs[t] >= 0) {
+        uint32_t nb = 0;
+#pragma unroll
+        for (int f = 0; f < kF; ++f) {
+          const bool neg = q[f][t] < Real(0);
+          const bool zero = !(q[f][t] > Real(0)) && !neg;
+          nb |= ((uint32_t)neg | ((uint32_t)zero << 1)) << (2 * f);
+        }
+        alpha[(int64_t)t * g.M] = (uint8_t)nb;
+      }
+  }
+  uint32_t odd = 0;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int f = 0; f < kF; ++f) {
+    const bool on = ((live >> f) & 1u) != 0;
+    const uint64_t pm = __ballot(par[f]);
+    if (on && pm) odd |= 1u << f;
+    // a frame at the cap stops in this pass: its uncapped syndrome weight
+    if (on && itf[f] >= 1 && itf[f] >= max_iters && pm && lane == 0)
+      atomicAdd(&w.capsyn[k * kF + f], __popcll(pm));
+  }
+  if (lane == 0) w.odd[(int64_t)k * w.check_waves + bi * 4 + (threadIdx.x >> 6)] = (uint8_t)odd;
+}
+
+// One block per chunk: OR of the chunk's check-wave parities, then the
+// reference's stopping rule per slot -- at the cap, or (min-sum, :406-408)
+// when it < cap, it % et_period == 0 and every check is satisfied -- and
+// freed (and empty) slots take the next frames of the batch.
+__global__ void __launch_bounds__(256) msn_decide(MsnWork w, int max_iters, int et_period, int B,
+                                                  int32_t *synd) {
+  const int k = blockIdx.x;
+  __shared__ uint32_t part[4];
+  uint32_t odd = 0;
+  if (w.live[k])
+    for (int i = threadIdx.x; i < w.check_waves; i += 256) odd |= w.odd[(int64_t)k * w.check_waves + i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) odd |= (uint32_t)__shfl_xor((int)odd, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = odd;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  odd = part[0] | part[1] | part[2] | part[3];
+  const int lane = threadIdx.x;
+  const bool on = lane < kF;
+  const int slot = k * kF + lane;
+  const int it = on ? w.it[slot] : 0, fr = on ? w.frame[slot] : -1;
+  const bool running = fr >= 0;
+  const bool unsat = ((odd >> lane) & 1u) != 0;
+  const bool stop = running && it >= 1 && (it >= max_iters || (it % et_period == 0 && !unsat));
+  const bool want = on && (stop || !running);
+  const uint64_t wm = __ballot(want);
+  int base = 0;
+  if (lane == 0 && wm) base = atomicAdd(&w.ctrl[0], __popcll(wm));
+  base = __shfl(base, 0);
+  const int rank = __popcll(wm & ((1ull << lane) - 1ull));
+  const int nf = want && base + rank < B ? base + rank : -1;
+  const bool fill = nf >= 0;
+  const bool run = running && !stop;
+  if (stop) {
+    w.used[slot] = it;
+    w.out_frame[slot] = fr;  // its outputs go out in this pass
+    if (synd) synd[fr] = w.capsyn[slot];  // 0 unless stopped at the cap unsatisfied
+  }
+  if (on) {
+    w.capsyn[slot] = 0;
+    w.frame[slot] = want ? nf : fr;  // a refilled slot's new frame
+    w.it[slot] = run ? it + 1 : 0;
+  }
+  const uint32_t sw = (uint32_t)__ballot(stop), rw = (uint32_t)__ballot(run),
+                 fw = (uint32_t)__ballot(fill);
+  if (lane == 0) {
+    w.stop[k] = sw;
+    w.run[k] = rw;
+    w.fill[k] = fw;
+    w.live[k] = rw | fw;
+    if (sw) atomicAdd(&w.ctrl[1], __popc(sw));
+  }
+}
+
+// Packed info bits (columns M.., MSB first, :207-219) and iterations of the
+// frames that stopped in this pass, from the signs of their LQ.
+__global__ void __launch_bounds__(256) msn_post(MsnView g, MsnWork w, DecodeArgs a) {
+  const int k = blockIdx.y;
+  const uint32_t sel = w.stop[k];
+  if (!sel) return;
+  const double *LQd = (const double *)w.LQ;
+  const float *LQf = (const float *)w.LQ;
+  const bool f32 = w.real_bytes == 4;
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < g.KB; q += gridDim.x * 256) {
+    int xs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = g.M + q * 8 + j;
+      xs[j] = c < g.N ? g.cpos[c] : -1;
+    }
+    for (int f = 0; f < kF; ++f) {
+      if (!((sel >> f) & 1u)) continue;
+      unsigned o = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (xs[j] >= 0) {
+          const int64_t i = el(k, g.N, xs[j]) + f;
+          const bool neg = f32 ? LQf[i] < 0.0f : LQd[i] < 0.0;
+          o |= (unsigned)neg << (7 - j);
+        }
+      a.packed[(int64_t)w.out_frame[k * kF + f] * g.KB + q] = (uint8_t)o;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < kF && ((sel >> threadIdx.x) & 1u) && a.iters) {
+    const int slot = k * kF + threadIdx.x;
+    a.iters[w.out_frame[slot]] = w.used[slot];
+  }
+}
+
+// Hard decisions (B x N bytes) and posteriors L(Q) as float (B x N) of the
+// frames that stopped.
+__global__ void __launch_bounds__(256) msn_cols(MsnView g, MsnWork w, uint8_t *bits, float *llr) {
+  const int k = blockIdx.y;
+  const uint32_t sel = w.stop[k];
+  if (!sel) return;
+  const double *LQd = (const double *)w.LQ;
+  const float *LQf = (const float *)w.LQ;
+  const bool f32 = w.real_bytes == 4;
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < g.N; c += gridDim.x * 256) {
+    const int x = g.cpos[c];
+    for (int f = 0; f < kF; ++f) {
+      if (!((sel >> f) & 1u)) continue;
+      const int64_t i = el(k, g.N, x) + f, fr = w.out_frame[k * kF + f];
+      const float v = f32 ? LQf[i] : (float)LQd[i];
+      const bool neg = f32 ? LQf[i] < 0.0f : LQd[i] < 0.0;
+      if (bits) bits[fr * g.N + c] = (uint8_t)neg;
+      if (llr) llr[fr * g.N + c] = v;
+    }
+  }
+}
+
+// Vertical step (:379-403), one column per lane, the chunk's F frames in the
+// lane: L(r_ji) of each edge from its row's state, s = sum_j L(r_ji) over
+// ascending original rows from +0.0, LQ = Lci + s.  Refilled slots:
+// Lci = LQ = -tx of their new frame (:318-331; exact in float, tx is a float).
+// With out_var (info columns in place, M % 8 == 0) the frames that stopped
+// in this pass write their outputs here from the LQ being replaced -- packed
+// bytes (8 lanes' decisions, MSB first, :207-219), iterations, and the
+// optional bits / posteriors -- instead of in msn_post / msn_cols.
+template <typename Real, int DV>
+__global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs a) {
+  int k, bi;
+  map_block(blockIdx.x, w.chunks, w.nb_var, k, bi);
+  const uint32_t run = w.run[k], fill = w.fill[k], stop = w.stop[k];
+  const int x = bi * kIB + threadIdx.x;  // column storage position
+  const int64_t ci = el(k, g.N, x);
+  Real *LQ = (Real *)w.LQ;
+  if (w.out_var && stop) {
+    const int lane = threadIdx.x & 63;
+    const bool in = x < g.N;
+    const Vec<Real> old = in ? ldv((const Real *)LQ + ci) : Vec<Real>{};
+    const int c = in ? g.corig[x] : 0;
+#pragma unroll
+    for (int f = 0; f < kF; ++f) {
+      if (!((stop >> f) & 1u)) continue;
+      const int64_t fr = w.out_frame[k * kF + f];
+      const bool neg = in && old.v[f] < Real(0);
+      const uint64_t m = __ballot(neg);
+      if (in && c >= g.M && ((c - g.M) & 7) == 0)
+        a.packed[fr * g.KB + ((c - g.M) >> 3)] =
+            (uint8_t)(__builtin_bitreverse32((uint32_t)(m >> lane) & 0xffu) >> 24);
+      if (in && a.bits) a.bits[fr * g.N + c] = (uint8_t)neg;
+      if (in && a.llr) a.llr[fr * g.N + c] = (float)old.v[f];
+      if (bi == 0 && threadIdx.x == 0 && a.iters) a.iters[fr] = w.used[k * kF + f];
+    }
+  }
+  if (!(run | fill) || x >= g.N) return;
+  Vec<float> lci = ldv(w.L + ci);
+  if (fill) {
+    const int64_t src = (int64_t)g.corig[x] * a.elem_stride;
+#pragma unroll
+    for (int f = 0; f < kF; ++f)
+      if ((fill >> f) & 1u)
+        lci.v[f] = -(a.in[(int64_t)w.frame[k * kF + f] * a.cw_stride + src] * a.polarity);
+    stv(w.L + ci, lci);
+  }
+  Vec<Real> s;
+#pragma unroll
+  for (int f = 0; f < kF; ++f) s.v[f] = Real(0);
+  if (run) {
+    const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
+    const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M;
+    // the column's edges: crs[t][x] = row | place << 24 for t < degree, -1
+    // after; every load of an edge's state is issued before any is used
+    // (m1 and m2 both: one load level less than selecting by meta first)
+    uint32_t cv[DV];
+#pragma unroll
+    for (int t = 0; t < DV; ++t)
+      cv[t] = t < g.dv_max ? (uint32_t)g.crs[(int64_t)t * g.N + x] : 0xffffffffu;
+#pragma unroll
+    for (int t = 0; t < DV; ++t)
+      if (cv[t] != 0xffffffffu) {
+        const int rp = (int)(cv[t] & 0xffffffu), place = (int)(cv[t] >> 24);
+        const int64_t ro = el(k, g.M, rp);
+        const MetaWord mt = ld_meta(w.meta + ro);
+        const uint32_t ab = alpha[(int64_t)place * g.M + rp];
+        const Vec<Real> v1 = ldv(m1 + ro), v2 = ldv(m2 + ro);
+#pragma unroll
+        for (int f = 0; f < kF; ++f) {
+          const int m = (int)((mt >> (8 * f)) & 0xffu);
+          const Real mag = place == (m & 63) - 1 ? v2.v[f] : v1.v[f];
+          s.v[f] = s.v[f] + (Real)(((m >> 6) - 1) * alpha_of(ab, f)) * mag;
+        }
+      }
+  }
+  // running frames: Lci + s; refilled: Lci; other slots are not read again
+  Vec<Real> lq;
+#pragma unroll
+  for (int f = 0; f < kF; ++f) lq.v[f] = ((fill >> f) & 1u) ? (Real)lci.v[f] : (Real)lci.v[f] + s.v[f];
+  stv(LQ + ci, lq);
+}
+
+__global__ void msn_init(MsnWork w) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < w.S; i += gridDim.x * blockDim.x) {
+    w.frame[i] = -1;
+    w.it[i] = 0;
+    w.capsyn[i] = 0;
+  }
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < w.chunks; k += gridDim.x * blockDim.x)
+    w.live[k] = w.run[k] = w.stop[k] = w.fill[k] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.ctrl[0] = 0;
+    w.ctrl[1] = 0;
+  }
+}
+
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+template <int PREC>
+void msn_pass(const MsnView &g, const MsnWork &w, const DecodeArgs &a, hipStream_t st) {
+  typedef typename Math<PREC>::Real Real;
+  const int rblocks = w.nb_check * w.chunks, cblocks = w.nb_var * w.chunks;
+  static_assert(kMsnFrames == kF, "");
+  if (g.dc_max <= 8)
+    msn_check<PREC, 8><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+  else if (g.dc_max <= 16)
+    msn_check<PREC, 16><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+  else
+    msn_check<PREC, 32><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+  msn_decide<<<w.chunks, 256, 0, st>>>(w, a.max_iters, a.et_period, a.B, a.synd);
+  if (!w.out_var) {
+    const int pb = std::min(16, (g.KB + 255) / 256);
+    msn_post<<<dim3(pb, w.chunks), 256, 0, st>>>(g, w, a);
+    if (a.bits || a.llr)
+      msn_cols<<<dim3(std::min(64, (g.N + 255) / 256), w.chunks), 256, 0, st>>>(g, w, a.bits, a.llr);
+  }
+  if (g.dv_max <= 4)
+    msn_var<Real, 4><<<cblocks, 256, 0, st>>>(g, w, a);
+  else if (g.dv_max <= 8)
+    msn_var<Real, 8><<<cblocks, 256, 0, st>>>(g, w, a);
+  else
+    msn_var<Real, 16><<<cblocks, 256, 0, st>>>(g, w, a);
+}
+
+}  // namespace
+
+int msn_default_chunks() {
+  const char *e = getenv("LDPC_MSN_CHUNKS");  // A/B knob
+  const int v = e ? atoi(e) : 0;
+  return v >= 1 ? v : 32;
+}
+
+size_t msn_work_bytes(const MsnView &g, int chunks, int prec) {
+  const size_t real = prec == 1 ? 4 : 8, F = kF, C = chunks;
+  const size_t nbc = (size_t)((g.M + kIB - 1) / kIB);
+  size_t n = al256(C * g.N * F * 4) + al256(C * g.N * F * real);  // L, LQ
+  n += 2 * al256(C * g.M * F * real) + al256(C * g.M * F);        // m1, m2, meta
+  n += al256(C * g.dc_max * g.M);                                 // alpha
+  n += al256(C * nbc * 4);                                        // odd
+  n += 5 * al256(C * F * 4);                                      // capsyn, it, frame, out_frame, used
+  n += 4 * al256(C * 4) + al256(64);                              // masks, ctrl
+  return n;
+}
+
+void msn_work_carve(MsnWork &w, void *base, const MsnView &g, int chunks, int prec) {
+  const size_t real = prec == 1 ? 4 : 8, F = kF, C = chunks;
+  char *p = (char *)base;
+  auto take = [&](size_t bytes) {
+    char *r = p;
+    p += al256(bytes);
+    return (void *)r;
+  };
+  w = MsnWork{};
+  w.chunks = chunks;
+  w.S = chunks * kF;
+  w.real_bytes = (int)real;
+  w.nb_check = (g.M + kIB - 1) / kIB;
+  w.nb_var = (g.N + kIB - 1) / kIB;
+  w.check_waves = w.nb_check * 4;
+  w.out_var = g.out_var;
+  w.L = (float *)take(C * g.N * F * 4);
+  w.LQ = take(C * g.N * F * real);
+  w.m1 = take(C * g.M * F * real);
+  w.m2 = take(C * g.M * F * real);
+  w.meta = (uint8_t *)take(C * g.M * F);
+  w.alpha = (uint8_t *)take(C * g.dc_max * g.M);
+  w.odd = (uint8_t *)take(C * (size_t)w.check_waves);
+  w.capsyn = (int32_t *)take(C * F * 4);
+  w.it = (int32_t *)take(C * F * 4);
+  w.frame = (int32_t *)take(C * F * 4);
+  w.out_frame = (int32_t *)take(C * F * 4);
+  w.used = (int32_t *)take(C * F * 4);
+  w.live = (uint32_t *)take(C * 4);
+  w.run = (uint32_t *)take(C * 4);
+  w.stop = (uint32_t *)take(C * 4);
+  w.fill = (uint32_t *)take(C * 4);
+  w.ctrl = (int32_t *)take(64);
+}
+
+int launch_graph_decode_msn(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int prec,
+                            int32_t *h_ctrl, void *stream) {
+  if (g.dc_max > kGraphDcMax || g.dv_max > kGraphDvMax) return -2;
+  if (a.B <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  msn_init<<<std::max(1, std::min(64, (w.S + 255) / 256)), 256, 0, st>>>(w);
+  // every slot finishes a frame at least every max_iters + 1 passes (as
+  // launch_graph_decode_ms); the host stops enqueueing once every frame is done
+  const int64_t bound = ((int64_t)(a.B + w.S - 1) / w.S + 1) * (a.max_iters + 1) + 2;
+  const int kRound = 8;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  for (int i = 0; i < 2; ++i)
+    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return -1;
+  int rc = 0;
+  int64_t pass = 0;
+  for (int round = 0; pass < bound; ++round) {
+    for (int i = 0; i < kRound && pass < bound; ++i, ++pass) {
+      if (prec == 1)
+        msn_pass<1>(g, w, a, st);
+      else
+        msn_pass<0>(g, w, a, st);
+    }
+    if (hipMemcpyAsync(h_ctrl + 2 * (round & 1), w.ctrl, 8, hipMemcpyDeviceToHost, st) !=
+            hipSuccess ||
+        hipEventRecord(ev[round & 1], st) != hipSuccess) {
+      rc = -1;
+      break;
+    }
+    if (round > 0) {
+      if (hipEventSynchronize(ev[(round - 1) & 1]) != hipSuccess) {
+        rc = -1;
+        break;
+      }
+      if (h_ctrl[2 * ((round - 1) & 1) + 1] >= a.B) break;  // all frames finished
+    }
+  }
+  for (int i = 0; i < 2; ++i) (void)hipEventDestroy(ev[i]);
+  if (rc == 0 && hipGetLastError() != hipSuccess) rc = -1;
+  return rc;
+}
+
+// ---- storage order (host) --------------------------------------------------
+
+namespace {
+
+// Pairs of neighbouring storage rows (columns) of equal degree whose t-th
+// edges land on neighbouring storage columns (rows): the contiguity a wave's
+// gathers get from the order.
+long contiguity(const MsnTables &t) {
+  long s = 0;
+  const int M = (int)t.rp.size() - 1, N = (int)t.cp.size() - 1;
+  for (int p = 0; p + 1 < M; ++p) {
+    const int d = t.rp[p + 1] - t.rp[p];
+    if (t.rp[p + 2] - t.rp[p + 1] != d) continue;
+    for (int e = 0; e < d; ++e) s += t.rcs[(size_t)e * M + p + 1] == t.rcs[(size_t)e * M + p] + 1;
+  }
+  for (int x = 0; x + 1 < N; ++x) {
+    const int d = t.cp[x + 1] - t.cp[x];
+    if (t.cp[x + 2] - t.cp[x + 1] != d) continue;
+    for (int e = 0; e < d; ++e)
+      s += (t.crs[(size_t)e * N + x + 1] & 0xffffff) == (t.crs[(size_t)e * N + x] & 0xffffff) + 1;
+  }
+  return s;
+}
+
+}  // namespace
+
+// Storage-ordered tables of H (rows rpos, columns cpos): row offsets and
+// column offsets for the degrees, and slot-major edge lists -- rcs[t][p] the
+// storage column of row p's t-th edge (ascending original column), crs[t][x]
+// the storage row of column x's t-th edge (ascending original row) | the
+// edge's place in that row << 24 -- so a wave's t-th edges are one
+// coalesced load.
+void msn_tables(int M, int N, const std::vector<int32_t> &rp0, const std::vector<int32_t> &ci0,
+                const std::vector<int32_t> &rpos, const std::vector<int32_t> &cpos,
+                MsnTables &t) {
+  std::vector<int32_t> rorig(M), corig(N);
+  for (int j = 0; j < M; ++j) rorig[rpos[j]] = j;
+  for (int c = 0; c < N; ++c) corig[cpos[c]] = c;
+  int dc = 0, dv = 0;
+  std::vector<int32_t> cdeg((size_t)N, 0);
+  for (int j = 0; j < M; ++j) {
+    dc = std::max(dc, rp0[j + 1] - rp0[j]);
+    for (int32_t o = rp0[j]; o < rp0[j + 1]; ++o) cdeg[cpos[ci0[o]]]++;
+  }
+  for (int x = 0; x < N; ++x) dv = std::max(dv, cdeg[x]);
+  t.rp.assign((size_t)M + 1, 0);
+  t.rcs.assign((size_t)dc * M, -1);
+  for (int p = 0; p < M; ++p) {
+    const int j = rorig[p];
+    t.rp[p + 1] = t.rp[p] + (rp0[j + 1] - rp0[j]);
+    for (int32_t o = rp0[j]; o < rp0[j + 1]; ++o) t.rcs[(size_t)(o - rp0[j]) * M + p] = cpos[ci0[o]];
+  }
+  t.cp.assign((size_t)N + 1, 0);
+  for (int x = 0; x < N; ++x) t.cp[x + 1] = t.cp[x] + cdeg[x];
+  t.crs.assign((size_t)dv * N, -1);
+  std::vector<int32_t> fill((size_t)N, 0);
+  for (int j = 0; j < M; ++j)  // original rows ascending
+    for (int32_t o = rp0[j]; o < rp0[j + 1]; ++o) {
+      const int x = cpos[ci0[o]];
+      t.crs[(size_t)fill[x]++ * N + x] = rpos[j] | ((o - rp0[j]) << 24);
+    }
+  t.corig = corig;
+  t.cpos = cpos;
+  // outputs from the variable pass need the info columns in place, 8 per byte
+  t.out_var = M % 8 == 0;
+  for (int c = M; c < N && t.out_var; ++c) t.out_var = cpos[c] == c;
+}
+
+// Chooses the storage order: the identity, or for M a multiple of 360 the
+// DVB-S2 residue-class order (row r -> (r mod q) * 360 + r / q, q = M / 360,
+// and the staircase's degree <= 2 columns {r, r+1} moved among their own
+// positions in the order of r's class position) -- whichever gives the
+// kernels' gathers more contiguity.  LDPC_MSN_ORDER=0 / 1 forces one.
+void msn_build(int M, int N, const std::vector<int32_t> &rp0, const std::vector<int32_t> &ci0,
+               MsnTables &t) {
+  std::vector<int32_t> rid(M), cid(N);
+  for (int j = 0; j < M; ++j) rid[j] = j;
+  for (int c = 0; c < N; ++c) cid[c] = c;
+  const char *env = getenv("LDPC_MSN_ORDER");
+  const int force = env ? atoi(env) : -1;
+  msn_tables(M, N, rp0, ci0, rid, cid, t);
+  t.order = 0;
+  if (M % 360 != 0 || force == 0) return;
+  const int q = M / 360;
+  std::vector<int32_t> rpos(M), cpos(cid);
+  for (int j = 0; j < M; ++j) rpos[j] = (j % q) * 360 + j / q;
+  // staircase columns: degree 1 or 2 with rows r (and r + 1)
+  std::vector<int32_t> cdeg(N, 0), cfirst(N, -1), clast(N, -1);
+  for (int j = 0; j < M; ++j)
+    for (int32_t o = rp0[j]; o < rp0[j + 1]; ++o) {
+      const int c = ci0[o];
+      if (cfirst[c] < 0) cfirst[c] = j;
+      clast[c] = j;
+      cdeg[c]++;
+    }
+  std::vector<int32_t> stair, slots;
+  for (int c = 0; c < N; ++c)
+    if ((cdeg[c] == 1) || (cdeg[c] == 2 && clast[c] == cfirst[c] + 1)) {
+      stair.push_back(c);
+      slots.push_back(c);
+    }
+  std::stable_sort(stair.begin(), stair.end(),
+                   [&](int a, int b) { return rpos[cfirst[a]] < rpos[cfirst[b]]; });
+  for (size_t i = 0; i < stair.size(); ++i) cpos[stair[i]] = slots[i];
+  MsnTables qc;
+  msn_tables(M, N, rp0, ci0, rpos, cpos, qc);
+  qc.order = 1;
+  const long s_id = contiguity(t), s_qc = contiguity(qc);
+  if (getenv("LDPC_MSN_DEBUG"))
+    fprintf(stderr, "msn order: contiguity identity %ld, residue classes %ld (E = %d)\n", s_id, s_qc,
+            rp0[M]);
+  if (force == 1 || s_qc > s_id) t = std::move(qc);
+}
+
+}  // namespace ldpc

@@ -144,8 +144,8 @@ def test_dvbs2_like_full_batch_roundtrip(dvb):
     """Config-4 batch (1024 frames at 2 dB): every frame decodes to its info
     bits with a zero syndrome, f64 and f32; all 1024 f64 frames (packed
     bytes, iterations, syndromes) equal the sparse oracle's -- on the
-    compressed-message pipeline (the default) and on the edge-message passes
-    (LDPC_MS_PIPELINE=0)."""
+    narrow-chunk pipeline (the default), the 64-frame-chunk pipeline
+    (LDPC_MS_PIPELINE=1) and the edge-message passes (LDPC_MS_PIPELINE=0)."""
     import os
     import ldpc_ece535a as L
     from oracle import oracle as orc
@@ -154,12 +154,14 @@ def test_dvbs2_like_full_batch_roundtrip(dvb):
     info, y = _noisy(csr, 1024, 2, seed=4)
     want = np.packbits(info, axis=1)
     ref = orc.decode_batch_sparse(0, rp, ci, M, N, y, 50, nthreads=16, want_bits=False)
-    os.environ["LDPC_MS_PIPELINE"] = "0"
-    try:
-        edge = L.Decoder(csr=csr)
-    finally:
-        del os.environ["LDPC_MS_PIPELINE"]
-    for dec, name in ((d, "pipeline"), (edge, "edge passes")):
+    others = []
+    for mode in ("1", "0"):
+        os.environ["LDPC_MS_PIPELINE"] = mode
+        try:
+            others.append(L.Decoder(csr=csr))
+        finally:
+            del os.environ["LDPC_MS_PIPELINE"]
+    for dec, name in ((d, "narrow"), (others[0], "pipeline"), (others[1], "edge passes")):
         for prec in (0, 1):
             out = dec.decode(y, method=0, max_iters=50, precision=prec, want_bits=False)
             assert (out["synd"] == 0).all(), name
@@ -167,7 +169,8 @@ def test_dvbs2_like_full_batch_roundtrip(dvb):
             if prec == 0:
                 for k in ("packed", "iters", "synd"):
                     np.testing.assert_array_equal(out[k], ref[k], err_msg="%s %s" % (name, k))
-    edge.close()
+    for o in others:
+        o.close()
 
 
 @pytest.mark.parametrize("method,db", [(0, 2), (1, 2), (0, 4), (1, 1)])

@@ -1,7 +1,8 @@
-"""Large-code min-sum has two implementations (ldpc_capi.hip decode_graph):
-the frame pipeline with compressed check messages (ldpc_graph_ms.hip, the
-default) and the edge-message passes (ldpc_graph.hip, LDPC_MS_PIPELINE=0 at
-context creation).  Both must reproduce the oracle exactly: the reference's
+"""Large-code min-sum has three implementations (ldpc_capi.hip decode_graph):
+the narrow-chunk frame pipeline (ldpc_graph_msn.hip, the default,
+LDPC_MS_PIPELINE=2), the 64-frame-chunk pipeline with compressed check
+messages (ldpc_graph_ms.hip, LDPC_MS_PIPELINE=1) and the edge-message passes
+(ldpc_graph.hip, LDPC_MS_PIPELINE=0), chosen at context creation.  Both must reproduce the oracle exactly: the reference's
 fixtures on its own H forced onto the large-code path (hard decisions, packed
 bytes, iterations, syndromes, posteriors), the DVB-S2-like code against the
 sparse restatement, non-finite samples, et_period 5, and batches far larger
@@ -14,10 +15,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _decoder(pipeline, **kw):
+MODES = ["2", "1", "0"]
+IDS = ["narrow", "pipeline", "edge"]
+
+
+def _decoder(mode, **kw):
     import ldpc_ece535a as L
     old = os.environ.get("LDPC_MS_PIPELINE")
-    os.environ["LDPC_MS_PIPELINE"] = "1" if pipeline else "0"
+    os.environ["LDPC_MS_PIPELINE"] = mode
     try:
         return L.Decoder(**kw)
     finally:
@@ -27,7 +32,7 @@ def _decoder(pipeline, **kw):
             os.environ["LDPC_MS_PIPELINE"] = old
 
 
-@pytest.fixture(scope="module", params=[True, False], ids=["pipeline", "edge"])
+@pytest.fixture(scope="module", params=MODES, ids=IDS)
 def gdec(request):
     return _decoder(request.param, force_graph=True)
 
@@ -75,12 +80,12 @@ def test_non_finite(gdec):
     np.testing.assert_array_equal(out["llr"], ref["post"])
 
 
-@pytest.mark.parametrize("pipeline", [True, False])
-def test_dvbs2_like_vs_sparse_oracle(pipeline):
+@pytest.mark.parametrize("mode", MODES, ids=IDS)
+def test_dvbs2_like_vs_sparse_oracle(mode):
     from ldpc_ece535a import codes
     from oracle import oracle as orc
     csr = codes.dvbs2_like(0)
-    d = _decoder(pipeline, csr=csr)
+    d = _decoder(mode, csr=csr)
     M, N, rp, ci = csr
     rng = np.random.Generator(np.random.PCG64(77))
     info = rng.integers(0, 2, size=(160, N - M), dtype=np.uint8)
