@@ -61,6 +61,7 @@ struct ldpc_ctx {
   int ms_mode = 2;
   ldpc::MsnTables msn;  // storage order of the narrow pipeline
   int32_t *d_msn[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint16_t *d_msn16 = nullptr;
   // small-code frame queues: one monotonic counter per stream that has
   // launched on this context (ldpc_kernels.hpp DecodeArgs::ticket)
   uint32_t *d_tickets = nullptr;
@@ -503,10 +504,11 @@ int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int preci
   if (method == 0 && ctx->ms_mode == 2) {
     // min-sum: narrow chunks, gathered state L2-resident per XCD
     ldpc::MsnView v;
-    v.rp = ctx->d_msn[0];
-    v.cp = ctx->d_msn[1];
-    v.rcs = ctx->d_msn[2];
-    v.crs = ctx->d_msn[3];
+    v.rblk = (const int2 *)ctx->d_msn[0];
+    v.cblk = (const int2 *)ctx->d_msn[1];
+    v.r16 = ctx->msn.r16 ? 1 : 0;
+    v.rtab = v.r16 ? (const void *)ctx->d_msn16 : (const void *)ctx->d_msn[2];
+    v.ctab = (const uint32_t *)ctx->d_msn[3];
     v.corig = ctx->d_msn[4];
     v.cpos = ctx->d_msn[5];
     v.M = g.M;
@@ -911,9 +913,11 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     upload(ctx, &ctx->d_ce, ce, "upload(col_edges)", what, e);
     upload(ctx, &ctx->d_cr, cr, "upload(col_rows)", what, e);
     if (ctx->ms_mode == 2) {
-      const std::vector<int32_t> *t[6] = {&ctx->msn.rp,  &ctx->msn.cp,    &ctx->msn.rcs,
-                                          &ctx->msn.crs, &ctx->msn.corig, &ctx->msn.cpos};
-      for (int i = 0; i < 6; ++i) upload(ctx, &ctx->d_msn[i], *t[i], "upload(storage order)", what, e);
+      const std::vector<int32_t> *t[6] = {&ctx->msn.rblk, &ctx->msn.cblk,  &ctx->msn.rtab,
+                                          &ctx->msn.ctab, &ctx->msn.corig, &ctx->msn.cpos};
+      for (int i = 0; i < 6; ++i)
+        if (i != 2 || !ctx->msn.r16) upload(ctx, &ctx->d_msn[i], *t[i], "upload(storage order)", what, e);
+      if (ctx->msn.r16) upload(ctx, &ctx->d_msn16, ctx->msn.rtab16, "upload(storage order)", what, e);
     }
   } else {
     upload(ctx, &ctx->d_erow, erecs, "upload(erow)", what, e);
@@ -1001,6 +1005,7 @@ void ldpc_destroy(ldpc_ctx *ctx) {
     if (p) (void)hipFree(p);
   for (int32_t *p : ctx->d_msn)
     if (p) (void)hipFree(p);
+  if (ctx->d_msn16) (void)hipFree(ctx->d_msn16);
   if (ctx->d_work) {
     (void)hipDeviceSynchronize();  // graph decodes may run on caller streams
     (void)hipFree(ctx->d_work);

@@ -113,11 +113,13 @@ constexpr int kMsnFrames = LDPC_MSN_FRAMES;
 // edges still in ascending original column, each column's in ascending
 // original row.
 struct MsnView {
-  const int32_t *rp;     // M + 1: row offsets (storage rows; degrees)
-  const int32_t *cp;     // N + 1: column offsets (storage columns; degrees)
-  const int32_t *rcs;    // dc_max x M: [t][p] storage column of row p's t-th edge
-  const int32_t *crs;    // dv_max x N: [t][x] storage row of column x's t-th edge
-                         //   | its place in that row << 24
+  // edge tables per block of 256 storage rows / columns ({offset, slots}
+  // per block; [t][lane] inside, -1 past an item's degree):
+  const int2 *rblk;      // check blocks
+  const void *rtab;      // storage column of a row's t-th edge (u16 when r16)
+  const int2 *cblk;      // variable blocks
+  const uint32_t *ctab;  // storage row of a column's t-th edge | its place in that row << 24
+  int r16;
   const int32_t *corig;  // N: original column of a storage column
   const int32_t *cpos;   // N: storage column of an original column
   int M, N, E, KB, dc_max, dv_max;
@@ -125,7 +127,12 @@ struct MsnView {
 };
 
 struct MsnTables {  // host copies of MsnView's arrays
-  std::vector<int32_t> rp, cp, rcs, crs, corig, cpos;  // rcs / crs: -1 past the degree
+  // full slot-major tables (D x n, -1 past the degree): rcs[t][p] storage
+  // column of row p's t-th edge, crs[t][x] storage row | place << 24
+  std::vector<int32_t> rp, cp, rcs, crs, corig, cpos;
+  std::vector<int32_t> rblk, rtab, cblk, ctab;  // per-block tables (MsnView)
+  std::vector<uint16_t> rtab16;
+  bool r16 = false;
   int order = 0;         // 0 identity, 1 DVB-S2 residue classes
   bool out_var = false;  // info columns in place and M % 8 == 0
 };

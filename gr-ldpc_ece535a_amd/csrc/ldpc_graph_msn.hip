@@ -105,7 +105,7 @@ __device__ __forceinline__ int alpha_of(uint32_t byte, int f) {
 // takes L(q) = Lci (LQ = Lci, no old message).  The parity of the last
 // decisions (checkFrame, :236-253) comes from the signs of the same LQ.
 // Frames whose slot is not live compute on stale values nobody reads.
-template <int PREC, int DC>
+template <int PREC, int DC, bool R16>
 __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int max_iters) {
   typedef typename Math<PREC>::Real Real;
   int k, bi;
@@ -120,11 +120,23 @@ __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int max_i
 #pragma unroll
   for (int f = 0; f < kF; ++f) par[f] = false;
   if (p < g.M) {
-    // the row's edges: rcs[t][p] >= 0 for t < degree, -1 after (one load
-    // level less than reading the degree first)
+    // the row's edges: the block's table [t][lane] of storage columns, -1
+    // (u16: 0xffff) past the row's degree -- no load level for the degree
+    const int2 rb = g.rblk[bi];  // table offset, the block's largest degree
     int cs[DC];
 #pragma unroll
-    for (int t = 0; t < DC; ++t) cs[t] = t < g.dc_max ? g.rcs[(int64_t)t * g.M + p] : -1;
+    for (int t = 0; t < DC; ++t) {
+      cs[t] = -1;
+      if (t < rb.y) {
+        const int64_t i = rb.x + t * kIB + (int)threadIdx.x;
+        if constexpr (R16) {
+          const int v = ((const uint16_t *)g.rtab)[i];
+          cs[t] = v == 0xffff ? -1 : v;
+        } else {
+          cs[t] = ((const int32_t *)g.rtab)[i];
+        }
+      }
+    }
     Real *m1 = (Real *)w.m1, *m2 = (Real *)w.m2;
     const Real *LQ = (const Real *)w.LQ;
     const int64_t ro = el(k, g.M, p);
@@ -367,13 +379,14 @@ __global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs 
   if (run) {
     const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
     const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M;
-    // the column's edges: crs[t][x] = row | place << 24 for t < degree, -1
-    // after; every load of an edge's state is issued before any is used
+    // the column's edges: the block's table [t][lane] of row | place << 24,
+    // -1 past the column's degree; every load of an edge's state is issued before any is used
     // (m1 and m2 both: one load level less than selecting by meta first)
+    const int2 cb = g.cblk[bi];  // table offset, the block's largest degree
     uint32_t cv[DV];
 #pragma unroll
     for (int t = 0; t < DV; ++t)
-      cv[t] = t < g.dv_max ? (uint32_t)g.crs[(int64_t)t * g.N + x] : 0xffffffffu;
+      cv[t] = t < cb.y ? g.ctab[cb.x + t * kIB + (int)threadIdx.x] : 0xffffffffu;
 #pragma unroll
     for (int t = 0; t < DV; ++t)
       if (cv[t] != 0xffffffffu) {
@@ -418,12 +431,16 @@ void msn_pass(const MsnView &g, const MsnWork &w, const DecodeArgs &a, hipStream
   typedef typename Math<PREC>::Real Real;
   const int rblocks = w.nb_check * w.chunks, cblocks = w.nb_var * w.chunks;
   static_assert(kMsnFrames == kF, "");
-  if (g.dc_max <= 8)
-    msn_check<PREC, 8><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
-  else if (g.dc_max <= 16)
-    msn_check<PREC, 16><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
-  else
-    msn_check<PREC, 32><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+  if (g.dc_max <= 8) {
+    if (g.r16)
+      msn_check<PREC, 8, true><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+    else
+      msn_check<PREC, 8, false><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+  } else if (g.dc_max <= 16) {
+    msn_check<PREC, 16, false><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+  } else {
+    msn_check<PREC, 32, false><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+  }
   msn_decide<<<w.chunks, 256, 0, st>>>(w, a.max_iters, a.et_period, a.B, a.synd);
   if (!w.out_var) {
     const int pb = std::min(16, (g.KB + 255) / 256);
@@ -561,6 +578,32 @@ long contiguity(const MsnTables &t) {
 
 }  // namespace
 
+// A slot-major table full[t][x] (D x n, -1 past each item's degree) cut in
+// blocks of the kernels' 256 items: block b keeps only its largest degree's
+// slots, [t][lane] at blk[2b] with blk[2b+1] slots.
+void msn_block_tables(const std::vector<int32_t> &full, int D, int n, std::vector<int32_t> &blk,
+                      std::vector<int32_t> &tab) {
+  const int nb = (n + kIB - 1) / kIB;
+  blk.assign((size_t)2 * nb, 0);
+  tab.clear();
+  for (int b = 0; b < nb; ++b) {
+    int deg = 0;
+    for (int i = 0; i < kIB; ++i) {
+      const int x = b * kIB + i;
+      if (x >= n) break;
+      for (int t = 0; t < D; ++t)
+        if (full[(size_t)t * n + x] != -1) deg = std::max(deg, t + 1);
+    }
+    blk[2 * b] = (int32_t)tab.size();
+    blk[2 * b + 1] = deg;
+    for (int t = 0; t < deg; ++t)
+      for (int i = 0; i < kIB; ++i) {
+        const int x = b * kIB + i;
+        tab.push_back(x < n ? full[(size_t)t * n + x] : -1);
+      }
+  }
+}
+
 // Storage-ordered tables of H (rows rpos, columns cpos): row offsets and
 // column offsets for the degrees, and slot-major edge lists -- rcs[t][p] the
 // storage column of row p's t-th edge (ascending original column), crs[t][x]
@@ -598,6 +641,13 @@ void msn_tables(int M, int N, const std::vector<int32_t> &rp0, const std::vector
     }
   t.corig = corig;
   t.cpos = cpos;
+  msn_block_tables(t.rcs, dc, M, t.rblk, t.rtab);
+  msn_block_tables(t.crs, dv, N, t.cblk, t.ctab);
+  t.r16 = N <= 0xffff;
+  if (t.r16) {
+    t.rtab16.resize(t.rtab.size());
+    for (size_t i = 0; i < t.rtab.size(); ++i) t.rtab16[i] = (uint16_t)(t.rtab[i] < 0 ? 0xffff : t.rtab[i]);
+  }
   // outputs from the variable pass need the info columns in place, 8 per byte
   t.out_var = M % 8 == 0;
   for (int c = M; c < N && t.out_var; ++c) t.out_var = cpos[c] == c;
