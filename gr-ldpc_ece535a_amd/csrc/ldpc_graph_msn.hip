@@ -100,14 +100,95 @@ __device__ __forceinline__ int alpha_of(uint32_t byte, int f) {
 }
 
 // ---------------------------------------------------------------------------
-// Horizontal step (:340-376), one row per lane, the chunk's F frames in the
-// lane.  L(q) of each edge is LQ - L(r_old) (:387-392); a frame's first step
-// takes L(q) = Lci (LQ = Lci, no old message).  The parity of the last
-// decisions (checkFrame, :236-253) comes from the signs of the same LQ.
-// Frames whose slot is not live compute on stale values nobody reads.
+// Horizontal step (:340-376) of one row (storage position p) for the chunk's
+// F frames, D = the block's largest row degree, every load of the row issued
+// before the first is used (edges past the row's own degree read column 0
+// and are masked).  L(q) of each edge is LQ - L(r_old) (:387-392); a frame's
+// first step takes L(q) = Lci (LQ = Lci, no old message).  The parity of the
+// last decisions (checkFrame, :236-253) comes from the signs of the same LQ.
+template <int PREC, int D, bool R16>
+__device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, int k, int p, int off,
+                                          const int (&itf)[kF], bool (&par)[kF]) {
+  typedef typename Math<PREC>::Real Real;
+  int cs[D];
+  bool ok[D];
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+    const int64_t i = off + t * kIB + (int)threadIdx.x;
+    int v;
+    if constexpr (R16) {
+      v = ((const uint16_t *)g.rtab)[i];
+      ok[t] = v != 0xffff;
+    } else {
+      v = ((const int32_t *)g.rtab)[i];
+      ok[t] = v >= 0;
+    }
+    cs[t] = ok[t] ? v : 0;
+  }
+  Real *m1 = (Real *)w.m1, *m2 = (Real *)w.m2;
+  const Real *LQ = (const Real *)w.LQ;
+  const int64_t ro = el(k, g.M, p);
+  const Vec<Real> om1 = ldv(m1 + ro), om2 = ldv(m2 + ro);
+  const MetaWord omt = ld_meta(w.meta + ro);
+  uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M + p;  // [t][p]
+  Vec<Real> lq[D];
+  uint32_t ab[D];
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+    lq[t] = ldv(LQ + el(k, g.N, cs[t]));
+    ab[t] = alpha[(int64_t)t * g.M];
+  }
+  // per frame: L(q) in ascending original column, sign product, smallest and
+  // second smallest |L(q)| (strict <, first occurrence, DBL_MAX seeds; NaN
+  // never passes), the new alpha bits
+  Vec<Real> n1, n2;
+  MetaWord nmt = 0;
+  uint32_t nb[D];
+#pragma unroll
+  for (int t = 0; t < D; ++t) nb[t] = 0;
+#pragma unroll
+  for (int f = 0; f < kF; ++f) {
+    const int mt = (int)((omt >> (8 * f)) & 0xffu);
+    const int oP = (mt >> 6) - 1, oi1 = (mt & 63) - 1;
+    int P = 1, i1 = -1;
+    Real a1 = Math<PREC>::max_(), a2 = Math<PREC>::max_();
+#pragma unroll
+    for (int t = 0; t < D; ++t)
+      if (ok[t]) {
+        const Real l = lq[t].v[f];
+        par[f] ^= l < Real(0);
+        const Real r = itf[f] == 0 ? Real(0)
+                                   : (Real)(oP * alpha_of(ab[t], f)) * (t == oi1 ? om2.v[f] : om1.v[f]);
+        const Real q = l - r;
+        P *= sgn(q);
+        const Real a = Math<PREC>::abs_(q);
+        if (a < a1) {
+          a2 = a1;
+          a1 = a;
+          i1 = t;
+        } else if (a < a2) {
+          a2 = a;
+        }
+        const bool neg = q < Real(0);
+        const bool zero = !(q > Real(0)) && !neg;
+        nb[t] |= ((uint32_t)neg | ((uint32_t)zero << 1)) << (2 * f);
+      }
+    n1.v[f] = a1;
+    n2.v[f] = a2;
+    nmt |= (MetaWord)(((P + 1) << 6) | (i1 + 1)) << (8 * f);
+  }
+  stv(m1 + ro, n1);
+  stv(m2 + ro, n2);
+  st_meta(w.meta + ro, nmt);
+#pragma unroll
+  for (int t = 0; t < D; ++t)
+    if (ok[t]) alpha[(int64_t)t * g.M] = (uint8_t)nb[t];
+}
+
+// One row per lane, the chunk's F frames in the lane.  Frames whose slot is
+// not live compute on stale values nobody reads.
 template <int PREC, int DC, bool R16>
 __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int max_iters) {
-  typedef typename Math<PREC>::Real Real;
   int k, bi;
   map_block(blockIdx.x, w.chunks, w.nb_check, k, bi);
   const uint32_t live = w.live[k];
@@ -120,88 +201,19 @@ __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int max_i
 #pragma unroll
   for (int f = 0; f < kF; ++f) par[f] = false;
   if (p < g.M) {
-    // the row's edges: the block's table [t][lane] of storage columns, -1
-    // (u16: 0xffff) past the row's degree -- no load level for the degree
-    const int2 rb = g.rblk[bi];  // table offset, the block's largest degree
-    int cs[DC];
-#pragma unroll
-    for (int t = 0; t < DC; ++t) {
-      cs[t] = -1;
-      if (t < rb.y) {
-        const int64_t i = rb.x + t * kIB + (int)threadIdx.x;
-        if constexpr (R16) {
-          const int v = ((const uint16_t *)g.rtab)[i];
-          cs[t] = v == 0xffff ? -1 : v;
-        } else {
-          cs[t] = ((const int32_t *)g.rtab)[i];
-        }
-      }
+    const int2 rb = g.rblk[bi];  // the block's table offset and largest degree
+    switch (rb.y) {
+#define LDPC_MSN_ROW(n) \
+  case n:               \
+    if constexpr (n <= DC) check_row<PREC, (n <= DC ? n : 1), R16>(g, w, k, p, rb.x, itf, par); \
+    break;
+      LDPC_MSN_ROW(1) LDPC_MSN_ROW(2) LDPC_MSN_ROW(3) LDPC_MSN_ROW(4) LDPC_MSN_ROW(5)
+      LDPC_MSN_ROW(6) LDPC_MSN_ROW(7) LDPC_MSN_ROW(8)
+#undef LDPC_MSN_ROW
+      default:
+        if constexpr (DC > 8) check_row<PREC, DC, R16>(g, w, k, p, rb.x, itf, par);
+        break;
     }
-    Real *m1 = (Real *)w.m1, *m2 = (Real *)w.m2;
-    const Real *LQ = (const Real *)w.LQ;
-    const int64_t ro = el(k, g.M, p);
-    const Vec<Real> om1 = ldv(m1 + ro), om2 = ldv(m2 + ro);
-    const MetaWord omt = ld_meta(w.meta + ro);
-    uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M + p;  // [t][p]
-    Real q[kF][DC];
-#pragma unroll
-    for (int t = 0; t < DC; ++t) {
-#pragma unroll
-      for (int f = 0; f < kF; ++f) q[f][t] = Real(0);
-      if (cs[t] >= 0) {
-        const Vec<Real> lq = ldv(LQ + el(k, g.N, cs[t]));
-        const uint32_t ab = alpha[(int64_t)t * g.M];
-#pragma unroll
-        for (int f = 0; f < kF; ++f) {
-          par[f] ^= lq.v[f] < Real(0);
-          const int mt = (int)((omt >> (8 * f)) & 0xffu);
-          const int oP = (mt >> 6) - 1, oi1 = (mt & 63) - 1;
-          const Real r = itf[f] == 0 ? Real(0)
-                                     : (Real)(oP * alpha_of(ab, f)) * (t == oi1 ? om2.v[f] : om1.v[f]);
-          q[f][t] = lq.v[f] - r;
-        }
-      }
-    }
-    // sign product, smallest and second smallest |L(q)| (strict <, first
-    // occurrence, DBL_MAX seeds; NaN never passes)
-    Vec<Real> n1, n2;
-    MetaWord nmt = 0;
-#pragma unroll
-    for (int f = 0; f < kF; ++f) {
-      int P = 1, i1 = -1;
-      Real a1 = Math<PREC>::max_(), a2 = Math<PREC>::max_();
-#pragma unroll
-      for (int t = 0; t < DC; ++t)
-        if (cs[t] >= 0) {
-          P *= sgn(q[f][t]);
-          const Real a = Math<PREC>::abs_(q[f][t]);
-          if (a < a1) {
-            a2 = a1;
-            a1 = a;
-            i1 = t;
-          } else if (a < a2) {
-            a2 = a;
-          }
-        }
-      n1.v[f] = a1;
-      n2.v[f] = a2;
-      nmt |= (MetaWord)(((P + 1) << 6) | (i1 + 1)) << (8 * f);
-    }
-    stv(m1 + ro, n1);
-    stv(m2 + ro, n2);
-    st_meta(w.meta + ro, nmt);
-#pragma unroll
-    for (int t = 0; t < DC; ++t)
-      if (cs[t] >= 0) {
-        uint32_t nb = 0;
-#pragma unroll
-        for (int f = 0; f < kF; ++f) {
-          const bool neg = q[f][t] < Real(0);
-          const bool zero = !(q[f][t] > Real(0)) && !neg;
-          nb |= ((uint32_t)neg | ((uint32_t)zero << 1)) << (2 * f);
-        }
-        alpha[(int64_t)t * g.M] = (uint8_t)nb;
-      }
   }
   uint32_t odd = 0;
   const int lane = threadIdx.x & 63;
@@ -328,6 +340,73 @@ __global__ void __launch_bounds__(256) msn_cols(MsnView g, MsnWork w, uint8_t *b
   }
 }
 
+// Edges T0 .. T0 + D - 1 of the lane's column (storage x = the block's
+// item): L(r_ji) from the row's state, added to s in ascending original row.
+// Every load of the group is issued before the first is used (m1 and m2 both,
+// rather than selecting by meta first: one load level less); edges past the
+// column's own degree read row 0 and are masked.
+template <typename Real, int T0, int D>
+__device__ __forceinline__ void var_edges(const MsnView &g, const MsnWork &w, int k, int off,
+                                          Vec<Real> &s) {
+  const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
+  const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M;
+  bool ok[D];
+  int place[D];
+  int64_t ro[D];
+  uint32_t ai[D];
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+    const uint32_t v = g.ctab[off + (T0 + t) * kIB + (int)threadIdx.x];
+    ok[t] = v != 0xffffffffu;
+    const int rp = ok[t] ? (int)(v & 0xffffffu) : 0;
+    place[t] = ok[t] ? (int)(v >> 24) : 0;
+    ro[t] = el(k, g.M, rp);
+    ai[t] = (uint32_t)place[t] * (uint32_t)g.M + (uint32_t)rp;
+  }
+  MetaWord mt[D];
+  uint32_t ab[D];
+  Vec<Real> v1[D], v2[D];
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+    mt[t] = ld_meta(w.meta + ro[t]);
+    ab[t] = alpha[ai[t]];
+    v1[t] = ldv(m1 + ro[t]);
+    v2[t] = ldv(m2 + ro[t]);
+  }
+#pragma unroll
+  for (int t = 0; t < D; ++t)
+    if (ok[t]) {
+#pragma unroll
+      for (int f = 0; f < kF; ++f) {
+        const int m = (int)((mt[t] >> (8 * f)) & 0xffu);
+        const Real mag = place[t] == (m & 63) - 1 ? v2[t].v[f] : v1[t].v[f];
+        s.v[f] = s.v[f] + (Real)(((m >> 6) - 1) * alpha_of(ab[t], f)) * mag;
+      }
+    }
+}
+
+// the same for n <= 4 edges from t0 (columns of degree > 8)
+template <typename Real>
+__device__ void var_edges_rt(const MsnView &g, const MsnWork &w, int k, int off, int t0, int n,
+                             Vec<Real> &s) {
+  const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
+  const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M;
+  for (int t = t0; t < t0 + n; ++t) {
+    const uint32_t v = g.ctab[off + t * kIB + (int)threadIdx.x];
+    if (v == 0xffffffffu) continue;
+    const int rp = (int)(v & 0xffffffu), place = (int)(v >> 24);
+    const int64_t ro = el(k, g.M, rp);
+    const MetaWord mt = ld_meta(w.meta + ro);
+    const uint32_t ab = alpha[(int64_t)place * g.M + rp];
+#pragma unroll
+    for (int f = 0; f < kF; ++f) {
+      const int m = (int)((mt >> (8 * f)) & 0xffu);
+      const Real *src = place == (m & 63) - 1 ? m2 : m1;
+      s.v[f] = s.v[f] + (Real)(((m >> 6) - 1) * alpha_of(ab, f)) * src[ro + f];
+    }
+  }
+}
+
 // Vertical step (:379-403), one column per lane, the chunk's F frames in the
 // lane: L(r_ji) of each edge from its row's state, s = sum_j L(r_ji) over
 // ascending original rows from +0.0, LQ = Lci + s.  Refilled slots:
@@ -377,31 +456,24 @@ __global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs 
 #pragma unroll
   for (int f = 0; f < kF; ++f) s.v[f] = Real(0);
   if (run) {
-    const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
-    const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M;
-    // the column's edges: the block's table [t][lane] of row | place << 24,
-    // -1 past the column's degree; every load of an edge's state is issued before any is used
-    // (m1 and m2 both: one load level less than selecting by meta first)
-    const int2 cb = g.cblk[bi];  // table offset, the block's largest degree
-    uint32_t cv[DV];
-#pragma unroll
-    for (int t = 0; t < DV; ++t)
-      cv[t] = t < cb.y ? g.ctab[cb.x + t * kIB + (int)threadIdx.x] : 0xffffffffu;
-#pragma unroll
-    for (int t = 0; t < DV; ++t)
-      if (cv[t] != 0xffffffffu) {
-        const int rp = (int)(cv[t] & 0xffffffu), place = (int)(cv[t] >> 24);
-        const int64_t ro = el(k, g.M, rp);
-        const MetaWord mt = ld_meta(w.meta + ro);
-        const uint32_t ab = alpha[(int64_t)place * g.M + rp];
-        const Vec<Real> v1 = ldv(m1 + ro), v2 = ldv(m2 + ro);
-#pragma unroll
-        for (int f = 0; f < kF; ++f) {
-          const int m = (int)((mt >> (8 * f)) & 0xffu);
-          const Real mag = place == (m & 63) - 1 ? v2.v[f] : v1.v[f];
-          s.v[f] = s.v[f] + (Real)(((m >> 6) - 1) * alpha_of(ab, f)) * mag;
+    const int2 cb = g.cblk[bi];  // the block's table offset and largest degree
+    switch (cb.y) {
+#define LDPC_MSN_COL(n)                                                    \
+  case n:                                                                  \
+    if constexpr (n <= DV) var_edges<Real, 0, (n < 4 ? n : 4)>(g, w, k, cb.x, s); \
+    if constexpr (n > 4 && n <= DV) var_edges<Real, 4, (n > 4 ? n - 4 : 1)>(g, w, k, cb.x, s); \
+    break;
+      LDPC_MSN_COL(1) LDPC_MSN_COL(2) LDPC_MSN_COL(3) LDPC_MSN_COL(4) LDPC_MSN_COL(5)
+      LDPC_MSN_COL(6) LDPC_MSN_COL(7) LDPC_MSN_COL(8)
+#undef LDPC_MSN_COL
+      default:
+        if constexpr (DV > 8) {
+          var_edges<Real, 0, 4>(g, w, k, cb.x, s);
+          var_edges<Real, 4, 4>(g, w, k, cb.x, s);
+          for (int t0 = 8; t0 < cb.y; t0 += 4) var_edges_rt<Real>(g, w, k, cb.x, t0, min(4, cb.y - t0), s);
         }
-      }
+        break;
+    }
   }
   // running frames: Lci + s; refilled: Lci; other slots are not read again
   Vec<Real> lq;
