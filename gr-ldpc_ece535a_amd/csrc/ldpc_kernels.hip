@@ -1567,11 +1567,20 @@ int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int 
 #endif
   if (waves_per_cu <= 0) waves_per_cu = LDPC_SMALL_WPC;
   // schedule: 1 one wave per frame, 2 one workgroup of `slots` waves per
-  // frame, 0 auto = 1.  Measured (bench.py --sweep-batch,
-  // profiles/round1/schedules_sweep.txt): the one-wave form is as fast as the
-  // workgroup form for every method at B = 16..256 and faster from B = 1024
-  // on (min-sum f64 at B = 4096: 0.0718 vs 0.0807 ms).
-  const bool mw = schedule == 2;
+  // frame, 0 auto.  Measured (bench.py --sweep-batch): with round 2's compact
+  // arithmetic the one-wave form was as fast as the workgroup form for every
+  // method at B = 16..256 and faster from B = 1024 on
+  // (profiles/round1/schedules_sweep.txt); with the exact sum-product
+  // arithmetic (precision 0 / 2) a frame's iteration is long enough that
+  // splitting it over `slots` waves lowers the latency of small launches --
+  // 50 iterations of one frame 60.8 vs 88.6 us, B = 256 0.066 vs 0.097 ms --
+  // while the one-wave form stays ahead at B = 1024 (0.0995 vs 0.113 ms;
+  // profiles/round3/latency_schedules_exact.txt).  Auto therefore takes the
+  // workgroup form for exact sum-product launches of <= kMwAutoMax frames
+  // (the block's dependent window launches) and the one-wave form otherwise.
+  constexpr int kMwAutoMax = 512;
+  const bool mw = schedule == 2 || (schedule == 0 && method == 1 && (prec == 0 || prec == 2) &&
+                                    a.B <= kMwAutoMax);
   // sum-product f64 in throughput mode on a code the packed kernel takes:
   // F frames per wave (waves_per_cu waves per CU, each with F frames)
 #ifndef LDPC_NO_PACKED  // A/B only

@@ -266,10 +266,11 @@ int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu);
 #define LDPC_MODE_THROUGHPUT 1
 int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode);
 
-/* Tuning: kernel schedule.  0 (default) = 1: one frame per wave; 2: one
- * frame per workgroup of ceil(E/64) waves, one edge per lane (kept for
- * latency experiments; measured no faster at any batch size on MI355X).
- * Results are identical across schedules. */
+/* Tuning: kernel schedule.  1: one frame per wave; 2: one frame per
+ * workgroup of ceil(E/64) waves, one edge per lane; 0 (default) = auto: 2 for
+ * exact sum-product launches (LDPC_PREC_F64 / _LIBM) of at most 512 frames,
+ * where it has the lower latency on MI355X (one 50-iteration frame 61 vs
+ * 89 us), else 1.  Results are identical across schedules. */
 int ldpc_set_schedule(ldpc_ctx *ctx, int schedule);
 
 /* Large-code path: device workspace cap in bytes (0 = default 8 GiB).  A
