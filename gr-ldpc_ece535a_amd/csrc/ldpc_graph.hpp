@@ -139,6 +139,7 @@ struct MsnTables {  // host copies of MsnView's arrays
 
 struct MsnWork {
   int S, chunks, nb_check, nb_var, check_waves, real_bytes, out_var;
+  int fuse;          // decision taken in the check pass (msn_check FUSE)
   float *L;          // chunks x N x F: Lci = -tx
   void *LQ;          // chunks x N x F Real: Lci + sum of the column's L(r)
   void *m1, *m2;     // chunks x M x F Real
@@ -150,7 +151,8 @@ struct MsnWork {
   int32_t *frame;    // S: the slot's frame (-1: empty); a refill's new frame after decide
   int32_t *out_frame;  // S: the frame that stopped in this pass
   int32_t *used;     // S: iterations of that frame
-  uint32_t *live, *run, *stop, *fill;  // per chunk: F-bit slot masks
+  uint32_t *live, *run, *stop, *fill;  // 2 x chunks: F-bit slot masks, by pass parity
+  uint64_t *arrive;  // chunks: fused decision's arrival word
   int32_t *ctrl;     // [0] next frame of the batch, [1] frames finished
 };
 

@@ -33,8 +33,10 @@
 // * The uncapped syndrome weight of a frame stopped at the cap is counted by
 //   the check pass of its last pass (atomic adds per wave, only at the cap).
 //
-// Per pass: msn_check -> msn_decide -> msn_post (packed bytes, iterations;
-// msn_cols for bits / posteriors) -> msn_var.
+// Per pass: msn_check -> msn_decide (stop / refill per slot; with
+// LDPC_MSN_FUSE=1 taken in the check pass instead) -> msn_var (outputs of the
+// stopped frames, the vertical step, refills); separate msn_post / msn_cols
+// launches for the outputs only for codes outside that fast path.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -98,6 +100,9 @@ __device__ __forceinline__ int alpha_of(uint32_t byte, int f) {
   const uint32_t b = byte >> (2 * f);
   return (b & 2u) ? 0 : ((b & 1u) ? -1 : 1);
 }
+
+__device__ void decide_slots(const MsnWork &w, int k, uint32_t odd, int nb, int max_iters,
+                             int et_period, int B, int32_t *synd);
 
 // ---------------------------------------------------------------------------
 // Horizontal step (:340-376) of one row (storage position p) for the chunk's
@@ -187,12 +192,23 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
 
 // One row per lane, the chunk's F frames in the lane.  Frames whose slot is
 // not live compute on stale values nobody reads.
-template <int PREC, int DC, bool R16>
-__global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int max_iters) {
+// mbuf: this pass's mask buffer (the decision writes the other).  FUSE: the
+// chunk's decision is taken in this launch by the block whose arrival
+// completes the chunk: one 64-bit atomic add per block carries the arrival
+// (bits 0-11) and, per frame f, "a row of this block is unsatisfied" (bits
+// 12(f+1)..); no fence and no waiting (a chunk that is not live decides in
+// its block 0 alone).
+template <int PREC, int DC, bool R16, bool FUSE>
+__global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int mbuf, int max_iters,
+                                                 int et_period, int B, int32_t *synd) {
   int k, bi;
   map_block(blockIdx.x, w.chunks, w.nb_check, k, bi);
-  const uint32_t live = w.live[k];
-  if (!live) return;
+  const uint32_t live = w.live[mbuf * w.chunks + k];
+  if (!live) {
+    if (FUSE && bi == 0 && threadIdx.x < 64)
+      decide_slots(w, k, 0u, mbuf ^ 1, max_iters, et_period, B, synd);
+    return;
+  }
   const int p = bi * kIB + threadIdx.x;  // row storage position
   int itf[kF];
 #pragma unroll
@@ -223,29 +239,49 @@ __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int max_i
     const uint64_t pm = __ballot(par[f]);
     if (on && pm) odd |= 1u << f;
     // a frame at the cap stops in this pass: its uncapped syndrome weight
-    if (on && itf[f] >= 1 && itf[f] >= max_iters && pm && lane == 0)
-      atomicAdd(&w.capsyn[k * kF + f], __popcll(pm));
+    // (returning atomic: performed before this block's arrival below)
+    if (on && itf[f] >= 1 && itf[f] >= max_iters && pm && lane == 0) {
+      const int r = atomicAdd(&w.capsyn[k * kF + f], __popcll(pm));
+      asm volatile("" ::"v"(r) : "memory");
+    }
   }
-  if (lane == 0) w.odd[(int64_t)k * w.check_waves + bi * 4 + (threadIdx.x >> 6)] = (uint8_t)odd;
+  if constexpr (!FUSE) {
+    if (lane == 0) w.odd[(int64_t)k * w.check_waves + bi * 4 + (threadIdx.x >> 6)] = (uint8_t)odd;
+  } else {
+    __shared__ uint32_t s_odd[4];
+    __shared__ int s_last;
+    __shared__ uint32_t s_tot;
+    if (lane == 0) s_odd[threadIdx.x >> 6] = odd;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t bo = s_odd[0] | s_odd[1] | s_odd[2] | s_odd[3];
+      uint64_t add = 1;
+#pragma unroll
+      for (int f = 0; f < kF; ++f)
+        if ((bo >> f) & 1u) add += 1ull << (12 * (f + 1));
+      const uint64_t old = atomicAdd((unsigned long long *)&w.arrive[k], (unsigned long long)add);
+      const uint64_t tot = old + add;
+      s_last = (int)(old & 0xfffu) == w.nb_check - 1;
+      uint32_t o = 0;
+#pragma unroll
+      for (int f = 0; f < kF; ++f)
+        if ((tot >> (12 * (f + 1))) & 0xfffu) o |= 1u << f;
+      s_tot = o;
+    }
+    __syncthreads();
+    if (!s_last || threadIdx.x >= 64) return;
+    if (threadIdx.x == 0) atomicExch((unsigned long long *)&w.arrive[k], 0ull);
+    decide_slots(w, k, s_tot, mbuf ^ 1, max_iters, et_period, B, synd);
+  }
 }
 
-// One block per chunk: OR of the chunk's check-wave parities, then the
-// reference's stopping rule per slot -- at the cap, or (min-sum, :406-408)
-// when it < cap, it % et_period == 0 and every check is satisfied -- and
-// freed (and empty) slots take the next frames of the batch.
-__global__ void __launch_bounds__(256) msn_decide(MsnWork w, int max_iters, int et_period, int B,
-                                                  int32_t *synd) {
-  const int k = blockIdx.x;
-  __shared__ uint32_t part[4];
-  uint32_t odd = 0;
-  if (w.live[k])
-    for (int i = threadIdx.x; i < w.check_waves; i += 256) odd |= w.odd[(int64_t)k * w.check_waves + i];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) odd |= (uint32_t)__shfl_xor((int)odd, o);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = odd;
-  __syncthreads();
-  if (threadIdx.x >= 64) return;
-  odd = part[0] | part[1] | part[2] | part[3];
+// The reference's stopping rule for chunk k's slots (one wave, lanes < F):
+// at the cap, or (min-sum, :406-408) when it < cap, it % et_period == 0 and
+// every check is satisfied (bit f of odd: frame f saw an unsatisfied row);
+// freed (and empty) slots take the next frames of the batch.  The new masks
+// go to mask buffer `nb` (the pass's check read the other one).
+__device__ void decide_slots(const MsnWork &w, int k, uint32_t odd, int nb, int max_iters,
+                             int et_period, int B, int32_t *synd) {
   const int lane = threadIdx.x;
   const bool on = lane < kF;
   const int slot = k * kF + lane;
@@ -262,32 +298,52 @@ __global__ void __launch_bounds__(256) msn_decide(MsnWork w, int max_iters, int 
   const int nf = want && base + rank < B ? base + rank : -1;
   const bool fill = nf >= 0;
   const bool run = running && !stop;
+  // the cap's syndrome weight (0 unless stopped at the cap unsatisfied);
+  // taken with an atomic: the check pass added it with atomics
+  const int cs = on ? atomicExch(&w.capsyn[slot], 0) : 0;
   if (stop) {
     w.used[slot] = it;
     w.out_frame[slot] = fr;  // its outputs go out in this pass
-    if (synd) synd[fr] = w.capsyn[slot];  // 0 unless stopped at the cap unsatisfied
+    if (synd) synd[fr] = cs;
   }
   if (on) {
-    w.capsyn[slot] = 0;
     w.frame[slot] = want ? nf : fr;  // a refilled slot's new frame
     w.it[slot] = run ? it + 1 : 0;
   }
   const uint32_t sw = (uint32_t)__ballot(stop), rw = (uint32_t)__ballot(run),
                  fw = (uint32_t)__ballot(fill);
   if (lane == 0) {
-    w.stop[k] = sw;
-    w.run[k] = rw;
-    w.fill[k] = fw;
-    w.live[k] = rw | fw;
+    const int m = nb * w.chunks + k;
+    w.stop[m] = sw;
+    w.run[m] = rw;
+    w.fill[m] = fw;
+    w.live[m] = rw | fw;
     if (sw) atomicAdd(&w.ctrl[1], __popc(sw));
   }
 }
 
+// The decision launch: one block per chunk ORs the chunk's check-wave
+// parities.
+__global__ void __launch_bounds__(256) msn_decide(MsnWork w, int par, int max_iters, int et_period,
+                                                  int B, int32_t *synd) {
+  const int k = blockIdx.x;
+  __shared__ uint32_t part[4];
+  uint32_t odd = 0;
+  if (w.live[par * w.chunks + k])
+    for (int i = threadIdx.x; i < w.check_waves; i += 256) odd |= w.odd[(int64_t)k * w.check_waves + i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) odd |= (uint32_t)__shfl_xor((int)odd, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = odd;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  decide_slots(w, k, part[0] | part[1] | part[2] | part[3], par ^ 1, max_iters, et_period, B, synd);
+}
+
 // Packed info bits (columns M.., MSB first, :207-219) and iterations of the
 // frames that stopped in this pass, from the signs of their LQ.
-__global__ void __launch_bounds__(256) msn_post(MsnView g, MsnWork w, DecodeArgs a) {
+__global__ void __launch_bounds__(256) msn_post(MsnView g, MsnWork w, DecodeArgs a, int nb) {
   const int k = blockIdx.y;
-  const uint32_t sel = w.stop[k];
+  const uint32_t sel = w.stop[nb * w.chunks + k];
   if (!sel) return;
   const double *LQd = (const double *)w.LQ;
   const float *LQf = (const float *)w.LQ;
@@ -320,9 +376,10 @@ __global__ void __launch_bounds__(256) msn_post(MsnView g, MsnWork w, DecodeArgs
 
 // Hard decisions (B x N bytes) and posteriors L(Q) as float (B x N) of the
 // frames that stopped.
-__global__ void __launch_bounds__(256) msn_cols(MsnView g, MsnWork w, uint8_t *bits, float *llr) {
+__global__ void __launch_bounds__(256) msn_cols(MsnView g, MsnWork w, uint8_t *bits, float *llr,
+                                                int nb) {
   const int k = blockIdx.y;
-  const uint32_t sel = w.stop[k];
+  const uint32_t sel = w.stop[nb * w.chunks + k];
   if (!sel) return;
   const double *LQd = (const double *)w.LQ;
   const float *LQf = (const float *)w.LQ;
@@ -416,10 +473,11 @@ __device__ void var_edges_rt(const MsnView &g, const MsnWork &w, int k, int off,
 // bytes (8 lanes' decisions, MSB first, :207-219), iterations, and the
 // optional bits / posteriors -- instead of in msn_post / msn_cols.
 template <typename Real, int DV>
-__global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs a) {
+__global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs a, int nb) {
   int k, bi;
   map_block(blockIdx.x, w.chunks, w.nb_var, k, bi);
-  const uint32_t run = w.run[k], fill = w.fill[k], stop = w.stop[k];
+  const int m = nb * w.chunks + k;  // the decision's mask buffer
+  const uint32_t run = w.run[m], fill = w.fill[m], stop = w.stop[m];
   const int x = bi * kIB + threadIdx.x;  // column storage position
   const int64_t ci = el(k, g.N, x);
   Real *LQ = (Real *)w.LQ;
@@ -488,8 +546,10 @@ __global__ void msn_init(MsnWork w) {
     w.it[i] = 0;
     w.capsyn[i] = 0;
   }
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < w.chunks; k += gridDim.x * blockDim.x)
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < 2 * w.chunks; k += gridDim.x * blockDim.x) {
     w.live[k] = w.run[k] = w.stop[k] = w.fill[k] = 0;
+    if (k < w.chunks) w.arrive[k] = 0;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     w.ctrl[0] = 0;
     w.ctrl[1] = 0;
@@ -498,34 +558,47 @@ __global__ void msn_init(MsnWork w) {
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-template <int PREC>
-void msn_pass(const MsnView &g, const MsnWork &w, const DecodeArgs &a, hipStream_t st) {
+// Pass p reads mask buffer p & 1 and decides into the other.
+template <int PREC, bool FUSE>
+void msn_pass_f(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int par, hipStream_t st) {
   typedef typename Math<PREC>::Real Real;
-  const int rblocks = w.nb_check * w.chunks, cblocks = w.nb_var * w.chunks;
+  const int rblocks = w.nb_check * w.chunks, cblocks = w.nb_var * w.chunks, nb = par ^ 1;
   static_assert(kMsnFrames == kF, "");
+#define LDPC_MSN_CHECK(DC, R16) \
+  msn_check<PREC, DC, R16, FUSE><<<rblocks, 256, 0, st>>>(g, w, par, a.max_iters, a.et_period, a.B, a.synd)
   if (g.dc_max <= 8) {
     if (g.r16)
-      msn_check<PREC, 8, true><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+      LDPC_MSN_CHECK(8, true);
     else
-      msn_check<PREC, 8, false><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+      LDPC_MSN_CHECK(8, false);
   } else if (g.dc_max <= 16) {
-    msn_check<PREC, 16, false><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+    LDPC_MSN_CHECK(16, false);
   } else {
-    msn_check<PREC, 32, false><<<rblocks, 256, 0, st>>>(g, w, a.max_iters);
+    LDPC_MSN_CHECK(32, false);
   }
-  msn_decide<<<w.chunks, 256, 0, st>>>(w, a.max_iters, a.et_period, a.B, a.synd);
+#undef LDPC_MSN_CHECK
+  if (!FUSE) msn_decide<<<w.chunks, 256, 0, st>>>(w, par, a.max_iters, a.et_period, a.B, a.synd);
   if (!w.out_var) {
     const int pb = std::min(16, (g.KB + 255) / 256);
-    msn_post<<<dim3(pb, w.chunks), 256, 0, st>>>(g, w, a);
+    msn_post<<<dim3(pb, w.chunks), 256, 0, st>>>(g, w, a, nb);
     if (a.bits || a.llr)
-      msn_cols<<<dim3(std::min(64, (g.N + 255) / 256), w.chunks), 256, 0, st>>>(g, w, a.bits, a.llr);
+      msn_cols<<<dim3(std::min(64, (g.N + 255) / 256), w.chunks), 256, 0, st>>>(g, w, a.bits, a.llr,
+                                                                                nb);
   }
   if (g.dv_max <= 4)
-    msn_var<Real, 4><<<cblocks, 256, 0, st>>>(g, w, a);
+    msn_var<Real, 4><<<cblocks, 256, 0, st>>>(g, w, a, nb);
   else if (g.dv_max <= 8)
-    msn_var<Real, 8><<<cblocks, 256, 0, st>>>(g, w, a);
+    msn_var<Real, 8><<<cblocks, 256, 0, st>>>(g, w, a, nb);
   else
-    msn_var<Real, 16><<<cblocks, 256, 0, st>>>(g, w, a);
+    msn_var<Real, 16><<<cblocks, 256, 0, st>>>(g, w, a, nb);
+}
+
+template <int PREC>
+void msn_pass(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int par, hipStream_t st) {
+  if (w.fuse)
+    msn_pass_f<PREC, true>(g, w, a, par, st);
+  else
+    msn_pass_f<PREC, false>(g, w, a, par, st);
 }
 
 }  // namespace
@@ -544,7 +617,7 @@ size_t msn_work_bytes(const MsnView &g, int chunks, int prec) {
   n += al256(C * g.dc_max * g.M);                                 // alpha
   n += al256(C * nbc * 4);                                        // odd
   n += 5 * al256(C * F * 4);                                      // capsyn, it, frame, out_frame, used
-  n += 4 * al256(C * 4) + al256(64);                              // masks, ctrl
+  n += 4 * al256(2 * C * 4) + al256(C * 8) + al256(64);          // masks x 2, arrive, ctrl
   return n;
 }
 
@@ -576,10 +649,16 @@ void msn_work_carve(MsnWork &w, void *base, const MsnView &g, int chunks, int pr
   w.frame = (int32_t *)take(C * F * 4);
   w.out_frame = (int32_t *)take(C * F * 4);
   w.used = (int32_t *)take(C * F * 4);
-  w.live = (uint32_t *)take(C * 4);
-  w.run = (uint32_t *)take(C * 4);
-  w.stop = (uint32_t *)take(C * 4);
-  w.fill = (uint32_t *)take(C * 4);
+  w.live = (uint32_t *)take(2 * C * 4);
+  w.run = (uint32_t *)take(2 * C * 4);
+  w.stop = (uint32_t *)take(2 * C * 4);
+  w.fill = (uint32_t *)take(2 * C * 4);
+  w.arrive = (uint64_t *)take(C * 8);
+  // LDPC_MSN_FUSE=1: the decision in the check pass's last block per chunk
+  // (12-bit arrival count).  Exact, but slower on config 4: the 127 blocks of
+  // a chunk contend on one atomic word (check pass 53.5 us against 40.8 + 4.9
+  // for the check and decision launches, profiles/round3/msn/fused_decide.txt)
+  w.fuse = w.nb_check <= 4095 && getenv("LDPC_MSN_FUSE") && getenv("LDPC_MSN_FUSE")[0] == '1';
   w.ctrl = (int32_t *)take(64);
 }
 
@@ -601,9 +680,9 @@ int launch_graph_decode_msn(const MsnView &g, const MsnWork &w, const DecodeArgs
   for (int round = 0; pass < bound; ++round) {
     for (int i = 0; i < kRound && pass < bound; ++i, ++pass) {
       if (prec == 1)
-        msn_pass<1>(g, w, a, st);
+        msn_pass<1>(g, w, a, (int)(pass & 1), st);
       else
-        msn_pass<0>(g, w, a, st);
+        msn_pass<0>(g, w, a, (int)(pass & 1), st);
     }
     if (hipMemcpyAsync(h_ctrl + 2 * (round & 1), w.ctrl, 8, hipMemcpyDeviceToHost, st) !=
             hipSuccess ||

@@ -95,3 +95,44 @@ def test_dvbs2_like_vs_sparse_oracle(mode):
     ref = orc.decode_batch_sparse(0, rp, ci, M, N, y, 50, nthreads=16)
     for k in ("bits", "packed", "iters", "synd"):
         np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
+
+
+@pytest.mark.parametrize("env", [{"LDPC_MSN_POST": "1"}, {"LDPC_MSN_ORDER": "0"},
+                                 {"LDPC_MSN_ORDER": "1"}, {"LDPC_MSN_CHUNKS": "5"},
+                                 {"LDPC_MSN_CHUNKS": "8"}, {"LDPC_MSN_FUSE": "1"},
+                                 {"LDPC_MSN_FUSE": "1", "LDPC_MSN_POST": "1"}],
+                         ids=["post-kernels", "identity-order", "residue-order", "5-chunks",
+                              "8-chunks", "fused-decision", "fused-decision-post-kernels"])
+def test_narrow_variants_dvbs2(env):
+    """The narrow-chunk pipeline's alternate paths on the DVB-S2-like code:
+    outputs from the separate post / column kernels instead of the variable
+    pass, the decision taken by the check pass's last block per chunk
+    instead of its own launch, the identity storage order instead of the residue-class order (and
+    the residue order forced), a chunk count that is not a multiple of 8 (no
+    XCD placement) and a single chunk per XCD.  Packed bytes, bits,
+    iterations and syndromes equal the sparse oracle's; posteriors equal the
+    edge-message passes' bit for bit."""
+    from ldpc_ece535a import codes
+    from oracle import oracle as orc
+    csr = codes.dvbs2_like(0)
+    M, N, rp, ci = csr
+    rng = np.random.Generator(np.random.PCG64(91))
+    info = rng.integers(0, 2, size=(96, N - M), dtype=np.uint8)
+    x = 2.0 * codes.ira_encode(csr, info) - 1.0
+    y = (x + np.sqrt(10 ** (-1.5 / 10)) * rng.standard_normal(x.shape)).astype(np.float32)
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        d = _decoder("2", csr=csr)
+        out = d.decode(y, method=0, max_iters=30, want_llr=True)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    ref = orc.decode_batch_sparse(0, rp, ci, M, N, y, 30, nthreads=16)
+    for k in ("bits", "packed", "iters", "synd"):
+        np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
+    edge = _decoder("0", csr=csr).decode(y, method=0, max_iters=30, want_llr=True)
+    np.testing.assert_array_equal(out["llr"].view(np.uint32), edge["llr"].view(np.uint32))

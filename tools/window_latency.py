@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--label", default="")
     ap.add_argument("--iters", default="50", help="iteration caps, comma-separated")
+    ap.add_argument("--schedules", default="0", help="kernel schedules (ldpc_set_schedule), comma-separated")
     a = ap.parse_args()
     import torch  # noqa: F401
     import bench
@@ -30,8 +31,10 @@ def main():
     Bmax = max(int(v) for v in a.sizes.split(","))
     y, _ = bench.synth(dec.H, Bmax + 1, -3.0, 11)
     span = y.ravel().astype(np.float32)
-    for it in [int(v) for v in a.iters.split(",")]:
-        for B in [int(v) for v in a.sizes.split(",")]:
+    for sched, it, B in [(s, int(i), int(b)) for s in a.schedules.split(",")
+                         for i in a.iters.split(",") for b in a.sizes.split(",")]:
+        dec.set_schedule(int(sched))
+        if True:
             rng = np.random.default_rng(B)
             w = (rng.integers(0, span.size - 64, size=B).astype(np.int64) << 1) | \
                 rng.integers(0, 2, B)
@@ -41,8 +44,8 @@ def main():
                 t0 = time.perf_counter()
                 dec.decode_windows(span, w, max_iters=it, reuse_span=True)
                 ts.append(time.perf_counter() - t0)
-            print("%s iters=%2d B=%5d median %.1f us  min %.1f us" % (
-                a.label, it, B, 1e6 * np.median(ts), 1e6 * np.min(ts)), flush=True)
+            print("%s schedule=%s iters=%2d B=%5d median %.1f us  min %.1f us" % (
+                a.label, sched, it, B, 1e6 * np.median(ts), 1e6 * np.min(ts)), flush=True)
 
 
 if __name__ == "__main__":
