@@ -482,7 +482,8 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
     d_forks.clear();
     Replay dry = r;
     if (d_profile) t0 = now_s();
-    replay(dry, false, nin, noutput_items, nullptr, out_budget, (size_t)max_windows(d_N));
+    replay(dry, false, nin, noutput_items, nullptr, out_budget,
+           (size_t)(d_max_want > 0 ? std::min(d_max_want, max_windows(d_N)) : max_windows(d_N)));
     // then the branches where a search position passes, nearest first, while
     // the launch has room: windows up to about one per wave slot of the GPU
     // cost little more than the launch's latency (50 iterations of one frame)
