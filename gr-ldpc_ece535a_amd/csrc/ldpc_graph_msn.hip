@@ -84,6 +84,48 @@ template <typename Real>
 __device__ __forceinline__ void stv(Real *p, const Vec<Real> &x) {
   *(Vec<Real> *)p = x;
 }
+// The same, non-temporal, for the state a pass streams once (row state in the
+// check pass, L and LQ in the variable pass) -- meant to keep the gathered
+// table and the edge tables in L2.  Measured slower (config 4: 1 973 vs
+// 2 212 Mbit/s, profiles/round3/msn/ab_nt.txt), so off unless built with
+// -DLDPC_MSN_NT=1.
+#ifndef LDPC_MSN_NT
+#define LDPC_MSN_NT 0
+#endif
+template <typename Real>
+__device__ __forceinline__ Vec<Real> ldv_nt(const Real *p) {
+#if LDPC_MSN_NT
+  typedef Real V2 __attribute__((ext_vector_type(16 / sizeof(Real))));
+  constexpr int n = kF * sizeof(Real) / 16;
+  Vec<Real> r;
+  static_assert(n >= 1 && sizeof(Vec<Real>) == 16 * n, "");
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    const V2 v = __builtin_nontemporal_load((const V2 *)p + i);
+#pragma unroll
+    for (int j = 0; j < (int)(16 / sizeof(Real)); ++j) r.v[i * (16 / sizeof(Real)) + j] = v[j];
+  }
+  return r;
+#else
+  return ldv(p);
+#endif
+}
+template <typename Real>
+__device__ __forceinline__ void stv_nt(Real *p, const Vec<Real> &x) {
+#if LDPC_MSN_NT
+  typedef Real V2 __attribute__((ext_vector_type(16 / sizeof(Real))));
+  constexpr int n = kF * sizeof(Real) / 16;
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    V2 v;
+#pragma unroll
+    for (int j = 0; j < (int)(16 / sizeof(Real)); ++j) v[j] = x.v[i * (16 / sizeof(Real)) + j];
+    __builtin_nontemporal_store(v, (V2 *)p + i);
+  }
+#else
+  stv(p, x);
+#endif
+}
 typedef uint32_t MetaWord;  // F meta bytes (F <= 4)
 __device__ __forceinline__ MetaWord ld_meta(const uint8_t *p) {
   if constexpr (kF == 4) return *(const uint32_t *)p;
@@ -133,7 +175,7 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
   Real *m1 = (Real *)w.m1, *m2 = (Real *)w.m2;
   const Real *LQ = (const Real *)w.LQ;
   const int64_t ro = el(k, g.M, p);
-  const Vec<Real> om1 = ldv(m1 + ro), om2 = ldv(m2 + ro);
+  const Vec<Real> om1 = ldv_nt(m1 + ro), om2 = ldv_nt(m2 + ro);
   const MetaWord omt = ld_meta(w.meta + ro);
   uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M + p;  // [t][p]
   Vec<Real> lq[D];
@@ -182,8 +224,8 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
     n2.v[f] = a2;
     nmt |= (MetaWord)(((P + 1) << 6) | (i1 + 1)) << (8 * f);
   }
-  stv(m1 + ro, n1);
-  stv(m2 + ro, n2);
+  stv_nt(m1 + ro, n1);
+  stv_nt(m2 + ro, n2);
   st_meta(w.meta + ro, nmt);
 #pragma unroll
   for (int t = 0; t < D; ++t)
@@ -501,7 +543,7 @@ __global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs 
     }
   }
   if (!(run | fill) || x >= g.N) return;
-  Vec<float> lci = ldv(w.L + ci);
+  Vec<float> lci = ldv_nt(w.L + ci);
   if (fill) {
     const int64_t src = (int64_t)g.corig[x] * a.elem_stride;
 #pragma unroll
@@ -537,7 +579,7 @@ __global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs 
   Vec<Real> lq;
 #pragma unroll
   for (int f = 0; f < kF; ++f) lq.v[f] = ((fill >> f) & 1u) ? (Real)lci.v[f] : (Real)lci.v[f] + s.v[f];
-  stv(LQ + ci, lq);
+  stv_nt(LQ + ci, lq);
 }
 
 __global__ void msn_init(MsnWork w) {
