@@ -772,6 +772,12 @@ def main():
         line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                             "traffic": traffic, "model": hbm_model["model"]}
+        if traffic:
+            # the compressed-message pipeline moves less than the edge-message
+            # model: its measured bytes over the same time, and their source
+            line["roofline"]["traffic_GB/s"] = round(traffic / (per_launch_ms * 1e-3) / 1e9, 1)
+            line["roofline"]["traffic_vs_model"] = round(traffic / alg_bytes, 3)
+            line["roofline"]["traffic_source"] = entry.get("source")
     elif pmc and "SQ_INSTS_VALU" in pmc:
         line["roofline"] = valu_roofline(pmc, per_launch_ms,
                                          (entry.get("isa_hot") or {}).get("other_weight"))
