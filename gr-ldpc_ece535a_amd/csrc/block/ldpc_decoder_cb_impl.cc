@@ -482,8 +482,19 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
     d_forks.clear();
     Replay dry = r;
     if (d_profile) t0 = now_s();
-    replay(dry, false, nin, noutput_items, nullptr, out_budget,
-           (size_t)(d_max_want > 0 ? std::min(d_max_want, max_windows(d_N)) : max_windows(d_N)));
+    // how many windows one dry run may collect: a launch of up to ~1024
+    // 50-iteration windows costs one window's latency, larger ones more
+    // (profiles/round3/window_latency_schedules.txt), so while the grid
+    // rarely fails (the high-SNR regime, few windows per sync loss) a dry run
+    // stops there; with many grid failures (low SNR) the launches stay whole
+    // (profiles/round3/block_plans_maxwant.txt: +7 % at 4 dB, -27 % at 2 dB
+    // for a fixed cap)
+    int cap = max_windows(d_N);
+    if (d_max_want > 0)
+      cap = std::min(d_max_want, cap);
+    else if (d_max_want == 0 && d_iterations >= 20 && 8 * d_grid_fails <= d_grid_frames)
+      cap = std::min(1024, cap);
+    replay(dry, false, nin, noutput_items, nullptr, out_budget, (size_t)cap);
     // then the branches where a search position passes, nearest first, while
     // the launch has room: windows up to about one per wave slot of the GPU
     // cost little more than the launch's latency (50 iterations of one frame)

@@ -70,7 +70,8 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   // windows a launch is filled up to with branch speculation (LDPC_BLOCK_BUDGET)
   int d_budget = getenv("LDPC_BLOCK_BUDGET") ? atoi(getenv("LDPC_BLOCK_BUDGET")) : 3072;
   // A/B knob: LDPC_BLOCK_MAXWANT=n stops a dry run once it has collected n
-  // windows (default: the launch limit, max_windows(N))
+  // windows; -1: the launch limit, max_windows(N), always; 0 (default): 1024
+  // while grid frames rarely fail, else the launch limit
   int d_max_want = getenv("LDPC_BLOCK_MAXWANT") ? atoi(getenv("LDPC_BLOCK_MAXWANT")) : 0;
   // grid: absolute sample index of the call's first input item; the phase
   // (mod N) of the last two consecutive frames that passed in sync (-1: none yet)
