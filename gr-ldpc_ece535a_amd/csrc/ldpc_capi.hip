@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <exception>
 #include <string>
 #include <vector>
 
@@ -1063,6 +1064,27 @@ int ldpc_ctx_layout(const ldpc_ctx *ctx, int32_t *model_out) {
   if (ctx->graph) return LDPC_EUNSUPPORTED;
   std::copy(ctx->layout_model, ctx->layout_model + 5, model_out);
   return LDPC_OK;
+}
+
+int ldpc_plan_storage_order(int M, int N, const int32_t *row_ptr, const int32_t *col_idx,
+                            int32_t *rpos_out_opt, int32_t *cpos_out_opt, int64_t *score_out_opt) {
+  g_create_error.clear();
+  if (!valid_csr(M, N, row_ptr, col_idx))
+    return set_err(nullptr, LDPC_EINVAL, "CSR H must be M x N (M < N), columns ascending and in range");
+  try {
+    std::vector<int32_t> rp(row_ptr, row_ptr + M + 1), ci(col_idx, col_idx + row_ptr[M]);
+    ldpc::MsnTables t;
+    ldpc::msn_build(M, N, rp, ci, t);
+    if (rpos_out_opt) std::copy(t.rpos.begin(), t.rpos.end(), rpos_out_opt);
+    if (cpos_out_opt) std::copy(t.cpos.begin(), t.cpos.end(), cpos_out_opt);
+    if (score_out_opt) {
+      score_out_opt[0] = t.score[0];
+      score_out_opt[1] = t.score[1];
+    }
+    return t.order;
+  } catch (const std::exception &e) {
+    return set_err(nullptr, LDPC_ENOMEM, e.what());
+  }
 }
 
 int ldpc_plan_layout(const uint8_t *H, int M, int N, int flags, int32_t *cell_out_opt,

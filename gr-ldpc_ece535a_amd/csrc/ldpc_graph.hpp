@@ -133,7 +133,9 @@ struct MsnTables {  // host copies of MsnView's arrays
   std::vector<int32_t> rblk, rtab, cblk, ctab;  // per-block tables (MsnView)
   std::vector<uint16_t> rtab16;
   bool r16 = false;
+  std::vector<int32_t> rpos;  // storage row of each original row
   int order = 0;         // 0 identity, 1 DVB-S2 residue classes
+  long score[2] = {0, 0};  // contiguity of the identity / residue-class order (-1: not tried)
   bool out_var = false;  // info columns in place and M % 8 == 0
 };
 
@@ -152,7 +154,7 @@ struct MsnWork {
   int32_t *out_frame;  // S: the frame that stopped in this pass
   int32_t *used;     // S: iterations of that frame
   uint32_t *live, *run, *stop, *fill;  // 2 x chunks: F-bit slot masks, by pass parity
-  uint64_t *arrive;  // chunks: fused decision's arrival word
+  uint64_t *arrive;  // chunks x 9: fused decision's chunk word and 8 group words
   int32_t *ctrl;     // [0] next frame of the batch, [1] frames finished
 };
 

@@ -236,10 +236,10 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
 // not live compute on stale values nobody reads.
 // mbuf: this pass's mask buffer (the decision writes the other).  FUSE: the
 // chunk's decision is taken in this launch by the block whose arrival
-// completes the chunk: one 64-bit atomic add per block carries the arrival
-// (bits 0-11) and, per frame f, "a row of this block is unsatisfied" (bits
-// 12(f+1)..); no fence and no waiting (a chunk that is not live decides in
-// its block 0 alone).
+// completes the chunk: 64-bit atomic adds carry the arrival (bits 0-11) and,
+// per frame f, "a row of these blocks is unsatisfied" (bits 12(f+1)..), in
+// two levels (8 group words per chunk, then the chunk's word); no fence and
+// no waiting (a chunk that is not live decides in its block 0 alone).
 template <int PREC, int DC, bool R16, bool FUSE>
 __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int mbuf, int max_iters,
                                                  int et_period, int B, int32_t *synd) {
@@ -296,23 +296,39 @@ __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int mbuf,
     if (lane == 0) s_odd[threadIdx.x >> 6] = odd;
     __syncthreads();
     if (threadIdx.x == 0) {
+      // two levels, so no word sees more than ~16 + 8 arrivals: block bi
+      // arrives at its group's word (bi mod 8); a group's last block
+      // forwards the group's flags to the chunk's word
       const uint32_t bo = s_odd[0] | s_odd[1] | s_odd[2] | s_odd[3];
       uint64_t add = 1;
 #pragma unroll
       for (int f = 0; f < kF; ++f)
         if ((bo >> f) & 1u) add += 1ull << (12 * (f + 1));
-      const uint64_t old = atomicAdd((unsigned long long *)&w.arrive[k], (unsigned long long)add);
+      const int grp = bi & 7, ngrp = (w.nb_check - grp + 7) >> 3, groups = min(8, w.nb_check);
+      unsigned long long *word = (unsigned long long *)&w.arrive[(int64_t)k * 9];
+      const uint64_t old = atomicAdd(word + 1 + grp, (unsigned long long)add);
       const uint64_t tot = old + add;
-      s_last = (int)(old & 0xfffu) == w.nb_check - 1;
+      int last = 0;
       uint32_t o = 0;
+      if ((int)(old & 0xfffu) == ngrp - 1) {
+        atomicExch(word + 1 + grp, 0ull);
+        uint64_t add2 = 1;
 #pragma unroll
-      for (int f = 0; f < kF; ++f)
-        if ((tot >> (12 * (f + 1))) & 0xfffu) o |= 1u << f;
+        for (int f = 0; f < kF; ++f)
+          if ((tot >> (12 * (f + 1))) & 0xfffu) add2 += 1ull << (12 * (f + 1));
+        const uint64_t old2 = atomicAdd(word, (unsigned long long)add2);
+        const uint64_t tot2 = old2 + add2;
+        last = (int)(old2 & 0xfffu) == groups - 1;
+#pragma unroll
+        for (int f = 0; f < kF; ++f)
+          if ((tot2 >> (12 * (f + 1))) & 0xfffu) o |= 1u << f;
+      }
+      s_last = last;
       s_tot = o;
     }
     __syncthreads();
     if (!s_last || threadIdx.x >= 64) return;
-    if (threadIdx.x == 0) atomicExch((unsigned long long *)&w.arrive[k], 0ull);
+    if (threadIdx.x == 0) atomicExch((unsigned long long *)&w.arrive[(int64_t)k * 9], 0ull);
     decide_slots(w, k, s_tot, mbuf ^ 1, max_iters, et_period, B, synd);
   }
 }
@@ -590,7 +606,8 @@ __global__ void msn_init(MsnWork w) {
   }
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < 2 * w.chunks; k += gridDim.x * blockDim.x) {
     w.live[k] = w.run[k] = w.stop[k] = w.fill[k] = 0;
-    if (k < w.chunks) w.arrive[k] = 0;
+    if (k < w.chunks)
+      for (int j = 0; j < 9; ++j) w.arrive[(int64_t)k * 9 + j] = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     w.ctrl[0] = 0;
@@ -659,7 +676,7 @@ size_t msn_work_bytes(const MsnView &g, int chunks, int prec) {
   n += al256(C * g.dc_max * g.M);                                 // alpha
   n += al256(C * nbc * 4);                                        // odd
   n += 5 * al256(C * F * 4);                                      // capsyn, it, frame, out_frame, used
-  n += 4 * al256(2 * C * 4) + al256(C * 8) + al256(64);          // masks x 2, arrive, ctrl
+  n += 4 * al256(2 * C * 4) + al256(C * 9 * 8) + al256(64);      // masks x 2, arrive, ctrl
   return n;
 }
 
@@ -695,7 +712,7 @@ void msn_work_carve(MsnWork &w, void *base, const MsnView &g, int chunks, int pr
   w.run = (uint32_t *)take(2 * C * 4);
   w.stop = (uint32_t *)take(2 * C * 4);
   w.fill = (uint32_t *)take(2 * C * 4);
-  w.arrive = (uint64_t *)take(C * 8);
+  w.arrive = (uint64_t *)take(C * 9 * 8);
   // LDPC_MSN_FUSE=1: the decision in the check pass's last block per chunk
   // (12-bit arrival count).  Exact, but slower on config 4: the 127 blocks of
   // a chunk contend on one atomic word (check pass 53.5 us against 40.8 + 4.9
@@ -834,6 +851,7 @@ void msn_tables(int M, int N, const std::vector<int32_t> &rp0, const std::vector
     }
   t.corig = corig;
   t.cpos = cpos;
+  t.rpos = rpos;
   msn_block_tables(t.rcs, dc, M, t.rblk, t.rtab);
   msn_block_tables(t.crs, dv, N, t.cblk, t.ctab);
   t.r16 = N <= 0xffff;
@@ -860,6 +878,8 @@ void msn_build(int M, int N, const std::vector<int32_t> &rp0, const std::vector<
   const int force = env ? atoi(env) : -1;
   msn_tables(M, N, rp0, ci0, rid, cid, t);
   t.order = 0;
+  t.score[0] = contiguity(t);
+  t.score[1] = -1;
   if (M % 360 != 0 || force == 0) return;
   const int q = M / 360;
   std::vector<int32_t> rpos(M), cpos(cid);
@@ -889,6 +909,9 @@ void msn_build(int M, int N, const std::vector<int32_t> &rp0, const std::vector<
   if (getenv("LDPC_MSN_DEBUG"))
     fprintf(stderr, "msn order: contiguity identity %ld, residue classes %ld (E = %d)\n", s_id, s_qc,
             rp0[M]);
+  qc.score[0] = s_id;
+  qc.score[1] = s_qc;
+  t.score[1] = s_qc;
   if (force == 1 || s_qc > s_id) t = std::move(qc);
 }
 

@@ -27,6 +27,7 @@ ERRORS = {0: "LDPC_OK", -1: "LDPC_EINVAL", -2: "LDPC_EUNSUPPORTED", -3: "LDPC_ED
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _f32p = ctypes.POINTER(ctypes.c_float)
+_i64p = ctypes.POINTER(ctypes.c_int64)
 _i = ctypes.c_int
 _i64 = ctypes.c_int64
 _vp = ctypes.c_void_p
@@ -44,6 +45,7 @@ SIGNATURES = {
     "ldpc_ctx_packed_frames": (_i, [_vp]),
     "ldpc_ctx_layout": (_i, [_vp, _i32p]),
     "ldpc_plan_layout": (_i, [_u8p, _i, _i, _i, _i32p, _i32p, _i32p]),
+    "ldpc_plan_storage_order": (_i, [_i, _i, _i32p, _i32p, _i32p, _i32p, _i64p]),
     "ldpc_set_work_limit": (_i, [_vp, _i64]),
     "ldpc_encode_device": (_i, [_vp, _vp, _i, _vp, _vp]),
     "ldpc_random_bits": (_i, [_vp, _i64, ctypes.c_uint64, _vp]),
@@ -156,6 +158,24 @@ def plan_layout(H, reorder=True, plain=False):
     return dict(cell=cell[:E].copy(), pos=pos,
                 model=dict(zip(("searched", "cc", "ec", "plain_cc", "plain_ec"),
                                (int(v) for v in model))))
+
+
+def plan_storage_order(csr):
+    """The large-code min-sum pipeline's storage order for csr = (M, N,
+    row_ptr, col_idx) (host only, no GPU): dict with order (0 identity, 1
+    DVB-S2 residue classes), rpos (M,) and cpos (N,) = storage position of
+    each original row / column, and score = contiguity of the identity and
+    residue-class orders (-1: not tried)."""
+    M, N, rp, ci = csr
+    rp = np.ascontiguousarray(rp, np.int32)
+    ci = np.ascontiguousarray(ci, np.int32)
+    rpos = np.zeros(M, np.int32)
+    cpos = np.zeros(N, np.int32)
+    score = np.zeros(2, np.int64)
+    order = _check(lib().ldpc_plan_storage_order(M, N, _p(rp, _i32p), _p(ci, _i32p),
+                                                 _p(rpos, _i32p), _p(cpos, _i32p),
+                                                 _p(score, _i64p)))
+    return dict(order=order, rpos=rpos, cpos=cpos, score=(int(score[0]), int(score[1])))
 
 
 class Decoder:

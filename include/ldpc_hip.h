@@ -129,6 +129,17 @@ int ldpc_alist_read(const char *path, int *M_out, int *N_out, int32_t *row_ptr_o
 int ldpc_plan_layout(const uint8_t *H, int M, int N, int flags, int32_t *cell_out_opt,
                      int32_t *pos_out_opt, int32_t *model_out_opt);
 
+/* The large-code min-sum pipeline's storage order for a CSR H (no GPU; the
+ * choice ldpc_create_csr makes, LDPC_MSN_ORDER included): rpos_out (M) and
+ * cpos_out (N) receive the storage position of every original row / column,
+ * score_out (2) the contiguity of the identity and of the DVB-S2
+ * residue-class order (-1 when M is not a multiple of 360).  Returns the
+ * order taken (0 identity, 1 residue classes) or a negative code.  The
+ * kernels still visit each row's edges in ascending original column and each
+ * column's in ascending original row.  Diagnostic / test helper. */
+int ldpc_plan_storage_order(int M, int N, const int32_t *row_ptr, const int32_t *col_idx,
+                            int32_t *rpos_out_opt, int32_t *cpos_out_opt, int64_t *score_out_opt);
+
 /* ---- device context ----------------------------------------------- */
 
 /* Builds the decoder's view of H (reorderHMatrix unless
