@@ -484,7 +484,13 @@ def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
             "Mbit/s": round(B * dec.K * steps / r["wall"] / 1e6, 2), "ms_per_decode": round(k, 4),
             "mean_iters": round(float(it.mean()), 3), "max_iters": int(it.max()),
             "alg_GB/s": round(alg / (k * 1e-3) / 1e9, 1),
+            "alg_GB/s_note": "edge-message byte model (SURVEY 8(d)) per decode time; the "
+                             "narrow pipeline moves ~0.53x those bytes (DESIGN section 5)",
             "frames_decoded_to_sent_data": int((pk == np.packbits(data, axis=1)).all(axis=1).sum())}
+        t = (load_pmc(args.pmc_json, "dvb0_f64_b1024_i50_db2") or {}).get("hbm_bytes_per_launch")
+        if p == 0 and t and args.iters == 50 and args.ebn0 == 2.0:
+            out["min-sum " + name]["measured_GB/s"] = round(t / (k * 1e-3) / 1e9, 1)
+            out["min-sum " + name]["measured_frac_of_8TB/s"] = round(t / (k * 1e-3) / 8e12, 4)
         if p == 0 and cpu_sample:
             kept = dict(y=d_y[:cpu_sample].cpu().numpy(), pk=pk[:cpu_sample],
                         it=it[:cpu_sample], K=dec.K)
@@ -768,16 +774,26 @@ def main():
         "traffic": traffic,
     }
     if dvb:
-        achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
-        line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                            "traffic": traffic, "model": hbm_model["model"]}
+        model_gbs = alg_bytes / (per_launch_ms * 1e-3) / 1e9
         if traffic:
-            # the compressed-message pipeline moves less than the edge-message
-            # model: its measured bytes over the same time, and their source
-            line["roofline"]["traffic_GB/s"] = round(traffic / (per_launch_ms * 1e-3) / 1e9, 1)
-            line["roofline"]["traffic_vs_model"] = round(traffic / alg_bytes, 3)
-            line["roofline"]["traffic_source"] = entry.get("source")
+            # the compressed-message pipeline moves ~half the edge-message
+            # model's bytes (so the model's rate exceeds the peak): the
+            # roofline is the measured memory traffic (PMC, per decode) over
+            # the live decode time; the model's rate is reported beside it
+            achieved = traffic / (per_launch_ms * 1e-3) / 1e9
+            line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                                "achieved_basis": "measured bytes (traffic) / live decode time",
+                                "model_equiv_GB/s": round(model_gbs, 1),
+                                "traffic_vs_model": round(traffic / alg_bytes, 3),
+                                "model": hbm_model["model"], "traffic_source": entry.get("source")}
+        else:
+            line["roofline"] = {"bound": "hbm", "achieved": round(model_gbs, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(model_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                                "achieved_basis": "edge-message byte model (no PMC entry)",
+                                "model": hbm_model["model"]}
     elif pmc and "SQ_INSTS_VALU" in pmc:
         line["roofline"] = valu_roofline(pmc, per_launch_ms,
                                          (entry.get("isa_hot") or {}).get("other_weight"))

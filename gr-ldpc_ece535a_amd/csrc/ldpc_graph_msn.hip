@@ -33,10 +33,11 @@
 // * The uncapped syndrome weight of a frame stopped at the cap is counted by
 //   the check pass of its last pass (atomic adds per wave, only at the cap).
 //
-// Per pass: msn_check -> msn_decide (stop / refill per slot; with
-// LDPC_MSN_FUSE=1 taken in the check pass instead) -> msn_var (outputs of the
-// stopped frames, the vertical step, refills); separate msn_post / msn_cols
-// launches for the outputs only for codes outside that fast path.
+// Per pass: msn_check (the chunk's stop / refill decision taken by the block
+// that completes the chunk; msn_decide as its own launch with
+// LDPC_MSN_FUSE=0) -> msn_var (outputs of the stopped frames, the vertical
+// step, refills); separate msn_post / msn_cols launches for the outputs only
+// for codes outside that fast path.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -713,11 +714,13 @@ void msn_work_carve(MsnWork &w, void *base, const MsnView &g, int chunks, int pr
   w.stop = (uint32_t *)take(2 * C * 4);
   w.fill = (uint32_t *)take(2 * C * 4);
   w.arrive = (uint64_t *)take(C * 9 * 8);
-  // LDPC_MSN_FUSE=1: the decision in the check pass's last block per chunk
-  // (12-bit arrival count).  Exact, but slower on config 4: the 127 blocks of
-  // a chunk contend on one atomic word (check pass 53.5 us against 40.8 + 4.9
-  // for the check and decision launches, profiles/round3/msn/fused_decide.txt)
-  w.fuse = w.nb_check <= 4095 && getenv("LDPC_MSN_FUSE") && getenv("LDPC_MSN_FUSE")[0] == '1';
+  // The decision in the check pass's last block per chunk (12-bit arrival
+  // counts) unless LDPC_MSN_FUSE=0.  One word per chunk made the 127 blocks of
+  // a chunk contend (check pass 53.5 us against 40.8 + 4.9 for the check and
+  // decision launches, profiles/round3/msn/fused_decide.txt); two levels (8
+  // group words, then the chunk's) measure 2 219-2 229 against 2 207-2 212
+  // Mbit/s for the separate launch (profiles/round3/msn/ab_fuse2.txt)
+  w.fuse = w.nb_check <= 4095 && !(getenv("LDPC_MSN_FUSE") && getenv("LDPC_MSN_FUSE")[0] == '0');
   w.ctrl = (int32_t *)take(64);
 }
 

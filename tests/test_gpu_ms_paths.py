@@ -99,15 +99,15 @@ def test_dvbs2_like_vs_sparse_oracle(mode):
 
 @pytest.mark.parametrize("env", [{"LDPC_MSN_POST": "1"}, {"LDPC_MSN_ORDER": "0"},
                                  {"LDPC_MSN_ORDER": "1"}, {"LDPC_MSN_CHUNKS": "5"},
-                                 {"LDPC_MSN_CHUNKS": "8"}, {"LDPC_MSN_FUSE": "1"},
-                                 {"LDPC_MSN_FUSE": "1", "LDPC_MSN_POST": "1"}],
+                                 {"LDPC_MSN_CHUNKS": "8"}, {"LDPC_MSN_FUSE": "0"},
+                                 {"LDPC_MSN_FUSE": "0", "LDPC_MSN_POST": "1"}],
                          ids=["post-kernels", "identity-order", "residue-order", "5-chunks",
-                              "8-chunks", "fused-decision", "fused-decision-post-kernels"])
+                              "8-chunks", "decision-launch", "decision-launch-post-kernels"])
 def test_narrow_variants_dvbs2(env):
     """The narrow-chunk pipeline's alternate paths on the DVB-S2-like code:
     outputs from the separate post / column kernels instead of the variable
-    pass, the decision taken by the check pass's last block per chunk
-    instead of its own launch, the identity storage order instead of the residue-class order (and
+    pass, the decision as its own launch instead of in the check pass's
+    last block per chunk, the identity storage order instead of the residue-class order (and
     the residue order forced), a chunk count that is not a multiple of 8 (no
     XCD placement) and a single chunk per XCD.  Packed bytes, bits,
     iterations and syndromes equal the sparse oracle's; posteriors equal the
