@@ -666,7 +666,10 @@ void msn_pass(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int par, 
 int msn_default_chunks() {
   const char *e = getenv("LDPC_MSN_CHUNKS");  // A/B knob
   const int v = e ? atoi(e) : 0;
-  return v >= 1 ? v : 32;
+  // 40 chunks = 160 frames in flight, 5 per XCD, 222 MB of chunk state (the
+  // 256 MB Infinity Cache holds it): 2 283-2 291 Mbit/s against 2 223-2 235
+  // for 32 and 2 189-2 201 for 48 (profiles/round3/msn/chunks_fused.txt)
+  return v >= 1 ? v : 40;
 }
 
 size_t msn_work_bytes(const MsnView &g, int chunks, int prec) {
