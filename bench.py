@@ -29,13 +29,16 @@ ranks decoded / that max.
 
 roofline (small-code path): the kernel keeps every edge message in LDS /
 VGPRs, so HBM does not bound it; f64 VALU issue does.  achieved = VALU issue
-cycles per launch (rocprofv3 PMC instruction counts, profiles/, weighted by
-the issue cost measured on gfx950 in profiles/round2/ubench_f64.txt: 4
-cycles per f64 add/mul/fma wave-instruction, 16 per f64 transcendental, 2
-per other VALU instruction) / the per-launch time; peak = 1024 SIMDs x
-2.4 GHz.  The SURVEY 8(d) byte model stays as a labelled secondary figure
-(equivalent streaming bandwidth).  Config 4 (--code dvbs2) is HBM-bound and
-uses the byte model against the 8 TB/s peak.
+cycles per launch (rocprofv3 PMC instruction counts, profiles/pmc_counters.json)
+weighted by the issue costs measured on gfx950 at four waves per SIMD
+(tools/ubench_valu.hip, profiles/round3/ubench_valu.txt: 4.31 cycles per f64
+add/mul/fma wave-instruction, 16.3 per f64 transcendental, the kernel's own
+hot-path mix for the other VALU instructions, ~3.5, tools/isa_hot.py) / the
+per-launch time; peak = 1024 SIMDs x 2.4 GHz.  frac_nominal is the same with
+the ISA's nominal costs (4 / 16 / 2).  The SURVEY 8(d) byte model stays as a
+labelled secondary figure (equivalent streaming bandwidth).  Config 4
+(--code dvbs2) is memory-bound: measured traffic (PMC, taken at the bench's
+own chunk count) over the decode time against the 8 TB/s peak.
 cpu_baseline: the C oracle (oracle/, a dense double restatement of the
 reference decoder) decoding the same frames on the host's cores.
 """
@@ -63,6 +66,7 @@ F64_PEAK_TFLOPS = 78.6         # MI355X FP64 vector spec
 # at 4.31) takes the kernel's hot-path mix (tools/isa_hot.py, recorded with
 # the counters) or this default
 ISSUE_F64, ISSUE_TRANS64, ISSUE_OTHER = 4.31, 16.3, 3.5
+NOMINAL_F64, NOMINAL_TRANS64, NOMINAL_OTHER = 4.0, 16.0, 2.0  # the ISA's nominal costs
 METRIC = "decoded info Mbit/s @ 50 BP iters, batch=4096; achieved HBM GB/s vs peak"
 
 
@@ -84,6 +88,7 @@ def parse(argv=None):
     ap.add_argument("--method", type=int, default=None, help="default 1 (0 for dvbs2)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 variant")
     ap.add_argument("--no-block", action="store_true", help="skip the block-throughput variant")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 variant")
     ap.add_argument("--precision", choices=["f64", "f64libm", "f64fast", "f32"], default="f64",
                     help="f64: LDPC_PREC_F64 (default, bit-exact), f64libm: LDPC_PREC_F64_LIBM "
                          "(exact, unbatched divisions), f64fast: LDPC_PREC_F64_FAST (compact "
@@ -351,6 +356,7 @@ def valu_roofline(pmc, per_launch_ms, w_other=None):
     trans = pmc.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
     other = max(0.0, pmc["SQ_INSTS_VALU"] - f64 - trans)
     cycles = ISSUE_F64 * f64 + ISSUE_TRANS64 * trans + w_other * other
+    nominal = NOMINAL_F64 * f64 + NOMINAL_TRANS64 * trans + NOMINAL_OTHER * other
     peak = SIMDS * CLOCK_HZ / 1e9
     ach = cycles / (per_launch_ms * 1e-3) / 1e9
     flop = 64.0 * (2.0 * pmc.get("SQ_INSTS_VALU_FMA_F64", 0.0) +
@@ -358,6 +364,10 @@ def valu_roofline(pmc, per_launch_ms, w_other=None):
     return {"bound": "valu", "achieved": round(ach, 1), "peak": peak,
             "unit": "G SIMD-cycles/s of VALU issue (f64-weighted)", "frac": round(ach / peak, 4),
             "issue_cycles_per_launch": round(cycles),
+            "frac_nominal": round(nominal / (per_launch_ms * 1e-3) / 1e9 / peak, 4),
+            "nominal_weights": "f64 add/mul/fma %g, f64 transcendental %g, other VALU %g cycles "
+                               "per wave64 instruction" % (NOMINAL_F64, NOMINAL_TRANS64,
+                                                          NOMINAL_OTHER),
             "f64_tflops": round(flop / (per_launch_ms * 1e-3) / 1e12, 2),
             "f64_tflops_frac": round(flop / (per_launch_ms * 1e-3) / 1e12 / F64_PEAK_TFLOPS, 4),
             "weights": "issue cycles per wave64 instruction: f64 add/mul/fma %g, f64 "
@@ -448,13 +458,17 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
             gpu_bytes = drive_stream.last_out
             sample = cx[:n_cpu * 64]
             t0 = time.perf_counter()
-            ref = orc.run_stream(1, Hr, sample, iterations=iters)
+            stats = {}
+            ref = orc.run_stream(1, Hr, sample, iterations=iters, stats=stats)
             cpu_s = time.perf_counter() - t0
             out[name]["cpu_baseline"] = {
                 "Mbit/s": round(ref.size * 8 / cpu_s / 1e6, 5), "cores": 1, "kind": "port",
                 "sample": "the stream's first %d frames of samples through the restated "
                           "general_work (oracle Block, :133-234), one thread" % n_cpu,
                 "bytes": int(ref.size),
+                # the yardstick for windows_per_output_frame: the reference
+                # loop's own decodes (one per step, two on a "-tx" retry)
+                "decodes_per_output_frame": round(stats["decodes"] / max(1, ref.size // 4), 3),
                 "bytes_equal_gpu_prefix": bool(gpu_bytes.size >= ref.size and
                                                (gpu_bytes[:ref.size] == ref).all())}
     return out
@@ -516,6 +530,58 @@ def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
     return out, check
 
 
+def config5_variant(L, torch, dec, args, dev, sizes=(1, 16, 256, 4096, 65536), check_b=4096):
+    """Config 5 (BASELINE configs[4]): the syndrome checked every 5
+    iterations (et_period 5, the reference checks every iteration,
+    lib/ldpc_decoder_cb_impl.cc:535-537 / :406-408), each frame at its own
+    Eb/N0 drawn from {0,1,2,3,4} dB, one launch at a time (latency mode):
+    latency per launch and Mbit/s per batch size, sum-product f64 (exact) and
+    min-sum f64.  Returns (results, check): check() compares the first
+    `check_b` frames of the B = check_b and largest launches with the
+    oracle's et_period restatement (CPU, after the GPU work)."""
+    rng = np.random.Generator(np.random.PCG64(args.seed + 5))
+    Bmax = max(sizes)
+    dbs = rng.integers(0, 5, size=Bmax).astype(np.float64)
+    d_y, _ = synth_device(L, torch, dec, Bmax, dbs, args.seed + 100, dev, check_frames=0)
+    dec.set_launch_mode(0)
+    out = {"setup": "et_period 5, Eb/N0 per frame uniform over {0,1,2,3,4} dB, 50-iteration "
+                    "cap, one launch at a time (latency mode); latency = HIP-event span per "
+                    "launch"}
+    kept = {}
+    for name, m in (("sum-product f64 (exact)", 1), ("min-sum f64", 0)):
+        rows = {}
+        for Bs in sizes:
+            r, st = time_variant(time_decoder, dec, torch, [d_y[:Bs]], Bs, m, args.iters, 5, 0,
+                                 10, 3, 1)
+            it = r["iters"]
+            rows["B=%d" % Bs] = {"latency_ms": round(r["per_launch_ms"], 5),
+                                 "Mbit/s": round(Bs * dec.K * st / r["wall"] / 1e6, 2),
+                                 "mean_iters": round(float(it.mean()), 3), "steps": st}
+            if Bs in (check_b, Bmax):
+                kept[(m, Bs)] = (r["outs"][0][0][:check_b].cpu().numpy(), it[:check_b])
+        out[name] = rows
+    dec.set_launch_mode(1)
+
+    def check():
+        if not kept or args.no_cpu_baseline:
+            return
+        from oracle import oracle as orc
+        threads, _ = cpu_share()
+        llr = d_y[:check_b].cpu().numpy()
+        for name, m in (("sum-product f64 (exact)", 1), ("min-sum f64", 0)):
+            ref = orc.decode_batch(m, dec.H, llr, args.iters, nthreads=threads, et_period=5)
+            bad_pk = bad_it = 0
+            for (mm, Bs), (pk, it) in kept.items():
+                if mm == m:
+                    bad_pk += int((ref["packed"] != pk).any(axis=1).sum())
+                    bad_it += int((ref["iters"] != it).sum())
+            out[name]["parity"] = {"frames": check_b, "launches_checked": 2,
+                                   "packed_mismatch_frames": bad_pk,
+                                   "iters_mismatch_frames": bad_it,
+                                   "checker": "oracle decode_batch, et_period 5"}
+    return out, check
+
+
 def time_variant(timer, dec, torch, inputs, B, m, iters, et, p, steps, warmup, D, min_s=0.03):
     """A variant timed over max(steps, enough steps for min_s seconds): a few
     dozen short launches would time the clock ramp and the pipeline's fill and
@@ -534,7 +600,7 @@ def gpu_variants(L, torch, dec, args, dev, inputs, B, D, prec, dvb, world, rank)
     """Everything the line reports beside the headline that runs on the GPU:
     config 4, the block, one batch in flight, the other methods / precisions.
     Returns dict(variants, serial, outs, config4_check)."""
-    res = dict(variants={}, serial=None, outs={}, config4_check=None)
+    res = dict(variants={}, serial=None, outs={}, config4_check=None, config5_check=None)
     if args.no_variants:
         return res
     var = res["variants"]
@@ -542,6 +608,8 @@ def gpu_variants(L, torch, dec, args, dev, inputs, B, D, prec, dvb, world, rank)
         var["config4"], res["config4_check"] = config4_variant(
             L, torch, dev, args, args.seed + 31,
             cpu_sample=0 if (args.no_cpu_baseline or rank != 0) else 1024)
+    if not dvb and not args.no_config5:
+        var["config5"], res["config5_check"] = config5_variant(L, torch, dec, args, dev)
     if not dvb and not args.no_block and world == 1:
         from ldpc_ece535a import blocks
         with _quiet_stdout():
@@ -894,8 +962,9 @@ def main():
         if world > 1:
             line["parity_all_ranks"] = gathered_parity(L, torch, orc, dec, args, dev, full, world,
                                                        Hr, csr, threads)
-    if pre["config4_check"] is not None:
-        pre["config4_check"]()
+    for chk in ("config4_check", "config5_check"):
+        if pre[chk] is not None:
+            pre[chk]()
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

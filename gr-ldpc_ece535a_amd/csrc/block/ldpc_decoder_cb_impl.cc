@@ -4,8 +4,8 @@
  *
  * general_work reproduces the control flow of lib/ldpc_decoder_cb_impl.cc:133-234
  * of gr-ldpc_ece535a for any chunking of the input; its outputs equal the
- * reference's as far as the window decodes do (parity measured, not proven:
- * see the end of this comment and DESIGN.md section 3).  The
+ * reference's as far as the window decodes do (see the end of this comment
+ * and DESIGN.md section 3).  The
  * reference loop decodes one window per step -- the N samples at the
  * current position times +-1 -- and its state machine decides the next
  * position.  Here the loop is replayed exactly over a memo of decoded
@@ -27,10 +27,11 @@
  * its budget (128 positions) widens x4 per launch.  Measured on one MI355X
  * (profiles/round2/block/block_plans.txt): 4 dB stream 32 -> 75 Mbit/s, 2 dB
  * 11 -> 19 Mbit/s against guessing that every frame in sync passes.
- * A launch costs ~63 us (one 50-iteration frame's latency, ~40 us, plus the
- * host round trip), as much as ~2000 extra windows, so optional branch
- * speculation (LDPC_BLOCK_FORK=1: the windows needed if a search position
- * syncs) is off: it saves launches only as fast as it adds windows.
+ * A launch costs one window's latency plus the host round trip
+ * ("The drop-in block's own throughput"), as much as
+ * thousands of extra windows, so optional branch speculation
+ * (LDPC_BLOCK_FORK=1: the windows needed if a search position syncs) is off
+ * at 50 iterations: it saves launches only as fast as it adds windows.
  *
  * The H is the reference's default (make(method)), or a runtime H (dense,
  * reordered like the reference's constructor; CSR; or an alist file).
@@ -39,10 +40,12 @@
  * decode results, so given the window decodes the block emits the same
  * bytes, consumes the same items, prints the same sync messages and leaves
  * the same state as the reference's frame-at-a-time loop.  The window
- * decodes themselves are the reference's arithmetic as DESIGN.md section 3
- * states it: min-sum exact; sum-product in the default f64 mode within 3 ulp
- * per tanh / 1 ulp per log of glibc, with zero decision mismatches measured
- * (not guaranteed) over the parity sweeps.
+ * decodes themselves are the reference's arithmetic bit for bit in the
+ * default f64 mode (min-sum has no transcendentals;
+ * sum-product reproduces glibc's tanh and log -- the __log_fma variant that
+ * glibc >= 2.28 selects on FMA-capable x86-64 -- with correctly rounded
+ * divisions), so the bytes equal those of the reference built against such a
+ * glibc.
  */
 #include "ldpc_decoder_cb_impl.h"
 

@@ -57,12 +57,12 @@ struct ldpc_ctx {
   int64_t *h_win = nullptr;
   size_t h_win_bytes = 0;
   int64_t span_samples = 0;
-  // large-code min-sum: 2 narrow-chunk pipeline (ldpc_graph_msn.hip), 1 the
-  // 64-frame-chunk pipeline (ldpc_graph_ms.hip), 0 the edge-message passes
+  // large-code min-sum: 2 narrow-chunk pipeline (ldpc_graph_msn.hip), 0 the
+  // edge-message passes (ldpc_graph.hip)
   int ms_mode = 2;
   ldpc::MsnTables msn;  // storage order of the narrow pipeline
-  int32_t *d_msn[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  uint16_t *d_msn16 = nullptr;
+  int32_t *d_msn[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // rblk cblk rx cx corig cpos
+  ldpc::MsnDesc *d_msnd[2] = {nullptr, nullptr};                               // rdesc cdesc
   // small-code frame queues: one monotonic counter per stream that has
   // launched on this context (ldpc_kernels.hpp DecodeArgs::ticket)
   uint32_t *d_tickets = nullptr;
@@ -505,11 +505,12 @@ int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int preci
   if (method == 0 && ctx->ms_mode == 2) {
     // min-sum: narrow chunks, gathered state L2-resident per XCD
     ldpc::MsnView v;
-    v.rblk = (const int2 *)ctx->d_msn[0];
-    v.cblk = (const int2 *)ctx->d_msn[1];
-    v.r16 = ctx->msn.r16 ? 1 : 0;
-    v.rtab = v.r16 ? (const void *)ctx->d_msn16 : (const void *)ctx->d_msn[2];
-    v.ctab = (const uint32_t *)ctx->d_msn[3];
+    v.rblk = (const int4 *)ctx->d_msn[0];
+    v.cblk = (const int4 *)ctx->d_msn[1];
+    v.rx = ctx->d_msn[2];
+    v.cx = ctx->d_msn[3];
+    v.rdesc = ctx->d_msnd[0];
+    v.cdesc = ctx->d_msnd[1];
     v.corig = ctx->d_msn[4];
     v.cpos = ctx->d_msn[5];
     v.M = g.M;
@@ -522,6 +523,10 @@ int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int preci
     int C = ldpc::msn_default_chunks();
     const int need_c = (a.B + ldpc::kMsnFrames - 1) / ldpc::kMsnFrames;
     if (need_c < C) C = need_c >= 8 ? (need_c + 7) / 8 * 8 : need_c;
+    // ldpc_set_work_limit caps the chunks in flight (at least one; multiples
+    // of 8 keep the XCD placement)
+    while (C > 1 && ldpc::msn_work_bytes(v, C, precision) > ctx->work_limit)
+      C = C > 8 && C % 8 == 0 ? C - 8 : C - 1;
     const size_t need = ldpc::msn_work_bytes(v, C, precision);
     if (need > ctx->work_bytes) {
       if (ctx->d_work) {
@@ -541,32 +546,6 @@ int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int preci
     ldpc::MsnWork w;
     ldpc::msn_work_carve(w, ctx->d_work, v, C, precision);
     const int rc = ldpc::launch_graph_decode_msn(v, w, a, precision, ctx->h_ctrl, st);
-    if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "code degrees outside the large-code kernels");
-    if (rc != 0) return hip_err(ctx, hipGetLastError(), "graph kernel launch");
-    return LDPC_OK;
-  }
-  if (method == 0 && ctx->ms_mode == 1) {
-    // min-sum: compressed check messages, frames pipelined through S slots
-    const int S = std::min(ldpc::ms_default_slots(), (a.B + 63) / 64 * 64);
-    const size_t need = ldpc::ms_work_bytes(g, S, precision, want_post);
-    if (need > ctx->work_bytes) {
-      if (ctx->d_work) {
-        (void)hipDeviceSynchronize();
-        (void)hipFree(ctx->d_work);
-        ctx->d_work = nullptr;
-        ctx->work_bytes = 0;
-      }
-      hipError_t e = hipMalloc(&ctx->d_work, need);
-      if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(graph workspace)");
-      ctx->work_bytes = need;
-    }
-    if (!ctx->h_ctrl) {
-      hipError_t e = hipHostMalloc((void **)&ctx->h_ctrl, 64, hipHostMallocDefault);
-      if (e != hipSuccess) return hip_err(ctx, e, "hipHostMalloc(ctrl)");
-    }
-    ldpc::MsWork w;
-    ldpc::ms_work_carve(w, ctx->d_work, g, S, precision, want_post);
-    const int rc = ldpc::launch_graph_decode_ms(g, w, a, precision, ctx->h_ctrl, st);
     if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "code degrees outside the large-code kernels");
     if (rc != 0) return hip_err(ctx, hipGetLastError(), "graph kernel launch");
     return LDPC_OK;
@@ -895,13 +874,21 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     return nullptr;
   }
   ctx->device = device;
-  {  // A/B knob: LDPC_MS_PIPELINE=0 edge-message passes, 1 the 64-frame-chunk
-     // pipeline, 2 (default) the narrow-chunk pipeline
+  {  // A/B knob: LDPC_MS_PIPELINE=0 edge-message passes, 2 (default) the
+     // narrow-chunk pipeline
     const char *v = getenv("LDPC_MS_PIPELINE");
-    ctx->ms_mode = v && v[0] >= '0' && v[0] <= '2' ? v[0] - '0' : 2;
+    ctx->ms_mode = v && v[0] == '0' ? 0 : 2;
     // the narrow pipeline packs a row and an edge's place in it in 32 bits
-    if (ctx->graph && ctx->ms_mode == 2 && (ctx->M >= (1 << 24) || ctx->dc_max > 128)) ctx->ms_mode = 1;
-    if (ctx->graph && ctx->ms_mode == 2) ldpc::msn_build(ctx->M, ctx->N, ctx->rp, ctx->ci, ctx->msn);
+    if (ctx->graph && ctx->ms_mode == 2 && (ctx->M >= (1 << 24) || ctx->dc_max > 128)) ctx->ms_mode = 0;
+    if (ctx->graph && ctx->ms_mode == 2) {
+      try {
+        ldpc::msn_build(ctx->M, ctx->N, ctx->rp, ctx->ci, ctx->msn);
+      } catch (const std::exception &ex) {
+        g_create_error = ex.what();
+        delete ctx;
+        return nullptr;
+      }
+    }
   }
   const char *what = nullptr;
   if ((e = hipSetDevice(device)) != hipSuccess) what = "hipSetDevice";
@@ -914,11 +901,11 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     upload(ctx, &ctx->d_ce, ce, "upload(col_edges)", what, e);
     upload(ctx, &ctx->d_cr, cr, "upload(col_rows)", what, e);
     if (ctx->ms_mode == 2) {
-      const std::vector<int32_t> *t[6] = {&ctx->msn.rblk, &ctx->msn.cblk,  &ctx->msn.rtab,
-                                          &ctx->msn.ctab, &ctx->msn.corig, &ctx->msn.cpos};
-      for (int i = 0; i < 6; ++i)
-        if (i != 2 || !ctx->msn.r16) upload(ctx, &ctx->d_msn[i], *t[i], "upload(storage order)", what, e);
-      if (ctx->msn.r16) upload(ctx, &ctx->d_msn16, ctx->msn.rtab16, "upload(storage order)", what, e);
+      const std::vector<int32_t> *t[6] = {&ctx->msn.rblk, &ctx->msn.cblk, &ctx->msn.rx,
+                                          &ctx->msn.cx,   &ctx->msn.corig, &ctx->msn.cpos};
+      for (int i = 0; i < 6; ++i) upload(ctx, &ctx->d_msn[i], *t[i], "upload(storage order)", what, e);
+      upload(ctx, &ctx->d_msnd[0], ctx->msn.rdesc, "upload(edge descriptors)", what, e);
+      upload(ctx, &ctx->d_msnd[1], ctx->msn.cdesc, "upload(edge descriptors)", what, e);
     }
   } else {
     upload(ctx, &ctx->d_erow, erecs, "upload(erow)", what, e);
@@ -1006,7 +993,8 @@ void ldpc_destroy(ldpc_ctx *ctx) {
     if (p) (void)hipFree(p);
   for (int32_t *p : ctx->d_msn)
     if (p) (void)hipFree(p);
-  if (ctx->d_msn16) (void)hipFree(ctx->d_msn16);
+  for (ldpc::MsnDesc *p : ctx->d_msnd)
+    if (p) (void)hipFree(p);
   if (ctx->d_work) {
     (void)hipDeviceSynchronize();  // graph decodes may run on caller streams
     (void)hipFree(ctx->d_work);

@@ -82,26 +82,6 @@ void graph_work_carve(GraphWork &w, void *base, const GraphView &g, int Bp, int 
 int launch_graph_decode(const GraphView &g, const GraphWork &w, const DecodeArgs &args,
                         int method, int prec, void *stream);
 
-// ---- min-sum with compressed check messages and a frame pipeline
-// (ldpc_graph_ms.hip) ------------------------------------------------------
-struct MsWork {
-  int S, chunks, check_waves;  // S slots (frames in flight), multiple of 64
-  float *L;          // N x S: Lci = -tx of the slot's frame
-  void *LQ;          // N x S Real: Lci + sum of the column's L(r)
-  void *m1, *m2;     // M x S Real: smallest / second smallest |L(q)| of the row
-  uint8_t *meta;     // M x S: (P + 1) << 6 | (i1 + 1)
-  uint64_t *alpha;   // (E x chunks) x 2: slots with L(q) < 0, slots with sign 0
-  uint64_t *hard;    // N x chunks: decisions, bit = slot
-  float *post;       // N x S: L(Q) (only with an llr output)
-  uint64_t *odd;     // check waves x chunks: rows seen unsatisfied
-  int32_t *it;       // S: iterations the slot's frame has executed
-  int32_t *frame;    // S: the slot's frame (-1: empty)
-  int32_t *nxt;      // S: frame after this pass's refill
-  int32_t *used;     // S: iterations of a frame that stopped this pass
-  uint64_t *live_w, *run_w, *stop_w, *fill_w, *cap_w;  // per-chunk lane masks
-  int32_t *ctrl;     // [0] next frame of the batch, [1] frames finished
-};
-
 // ---- min-sum with the gathered state in one XCD's L2 (ldpc_graph_msn.hip):
 // chunks of kMsnFrames frames, XCD-aware chunk placement, storage order ------
 #ifndef LDPC_MSN_FRAMES
@@ -109,17 +89,37 @@ struct MsWork {
 #endif
 constexpr int kMsnFrames = LDPC_MSN_FRAMES;
 
+// One wave's t-th edges (64 lanes): in the storage order every circulant of a
+// DVB-S2-style code is a shifted identity, so the 64 values are a few runs of
+// consecutive integers -- value(lane) = b[run] + lane, run 0 for lanes below
+// thr & 0xff, 1 below (thr >> 8) & 0xff, 2 below (thr >> 16) & 0xff, else 3.
+// A negative value means "no edge" (lanes past the item's degree or past n;
+// such a run's base is kMsnNoEdge).  A wave with a slot of more than 4 runs
+// keeps its values explicitly (MsnView rblk / cblk mark it; each
+// descriptor's xoff indexes the explicit table).  32 bytes; a wave's
+// descriptors are adjacent, so one 4-byte load per lane reads 8 slots'
+// (was 8 x 64 table entries).
+struct alignas(32) MsnDesc {
+  int32_t b[4];
+  uint32_t thr;
+  int32_t xoff;
+  int32_t pad[2];
+};
+constexpr int32_t kMsnNoEdge = -(1 << 30);
+
 // H in storage order: rows and columns renumbered (rpos / cpos), each row's
 // edges still in ascending original column, each column's in ascending
 // original row.
 struct MsnView {
-  // edge tables per block of 256 storage rows / columns ({offset, slots}
-  // per block; [t][lane] inside, -1 past an item's degree):
-  const int2 *rblk;      // check blocks
-  const void *rtab;      // storage column of a row's t-th edge (u16 when r16)
-  const int2 *cblk;      // variable blocks
-  const uint32_t *ctab;  // storage row of a column's t-th edge | its place in that row << 24
-  int r16;
+  // per block of 256 storage rows / columns: {first descriptor, slots (the
+  // block's largest degree), explicit-wave mask, 0}; descriptor of slot t,
+  // wave w at first + w slots + t
+  const int4 *rblk;
+  const MsnDesc *rdesc;  // value = storage column of a row's t-th edge
+  const int32_t *rx;     // explicit row values (64 per explicit descriptor)
+  const int4 *cblk;
+  const MsnDesc *cdesc;  // value = storage row of a column's t-th edge | its place in that row << 24
+  const int32_t *cx;
   const int32_t *corig;  // N: original column of a storage column
   const int32_t *cpos;   // N: storage column of an original column
   int M, N, E, KB, dc_max, dv_max;
@@ -130,9 +130,8 @@ struct MsnTables {  // host copies of MsnView's arrays
   // full slot-major tables (D x n, -1 past the degree): rcs[t][p] storage
   // column of row p's t-th edge, crs[t][x] storage row | place << 24
   std::vector<int32_t> rp, cp, rcs, crs, corig, cpos;
-  std::vector<int32_t> rblk, rtab, cblk, ctab;  // per-block tables (MsnView)
-  std::vector<uint16_t> rtab16;
-  bool r16 = false;
+  std::vector<int32_t> rblk, cblk, rx, cx;  // per-block offsets, explicit values (MsnView)
+  std::vector<MsnDesc> rdesc, cdesc;
   std::vector<int32_t> rpos;  // storage row of each original row
   int order = 0;         // 0 identity, 1 DVB-S2 residue classes
   long score[2] = {0, 0};  // contiguity of the identity / residue-class order (-1: not tried)
@@ -167,13 +166,5 @@ size_t msn_work_bytes(const MsnView &g, int chunks, int prec);
 void msn_work_carve(MsnWork &w, void *base, const MsnView &g, int chunks, int prec);
 int launch_graph_decode_msn(const MsnView &g, const MsnWork &w, const DecodeArgs &args, int prec,
                             int32_t *h_ctrl, void *stream);
-
-int ms_default_slots();
-size_t ms_work_bytes(const GraphView &g, int S, int prec, bool want_post);
-void ms_work_carve(MsWork &w, void *base, const GraphView &g, int S, int prec, bool want_post);
-// Min-sum decode of args.B frames through S slots; waits on the device between
-// rounds of passes (h_ctrl: 4 ints of pinned host memory).  0, -2 or -1.
-int launch_graph_decode_ms(const GraphView &g, const MsWork &w, const DecodeArgs &args, int prec,
-                           int32_t *h_ctrl, void *stream);
 
 }  // namespace ldpc

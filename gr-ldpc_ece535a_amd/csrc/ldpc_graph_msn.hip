@@ -19,13 +19,13 @@
 // * Storage order.  Rows and columns are stored in an order chosen on the
 //   host (ldpc_msn_build): for codes with the DVB-S2 structure (IRA, 360-
 //   column groups, row r = x + s q mod M) rows by residue class mod q, which
-//   makes every circulant a shifted identity, so the 16 rows of a wave read
-//   16 consecutive columns for each of their edges and the 16 columns of a
-//   wave read 16 consecutive rows -- 512 contiguous bytes per wave
-//   instruction.  The arithmetic still visits a row's edges in ascending
+//   makes every circulant a shifted identity, so the 64 rows of a wave read
+//   (runs of) consecutive columns for each of their edges and the 64 columns
+//   of a wave read consecutive rows.  The arithmetic still visits a row's edges in ascending
 //   original column and a column's edges in ascending original row (the
 //   reference's scan order); the order only moves where values are stored.
-// * A lane is (item, frame): 16 rows / columns x 4 frames per wave.  The
+// * One row (column) per lane, 64 per wave, 256 per block; the chunk's F
+//   frames sit in the lane as one vector (Vec).  The
 //   decisions are the signs of LQ (vhat = LQ < 0, :398-402), so the check
 //   pass forms the parities of the last decisions from the LQ values it
 //   gathers anyway (no separate hard-decision array), and outputs (packed
@@ -41,6 +41,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <stdexcept>
 #include <vector>
 
 #include <stdio.h>
@@ -144,8 +145,80 @@ __device__ __forceinline__ int alpha_of(uint32_t byte, int f) {
   return (b & 2u) ? 0 : ((b & 1u) ? -1 : 1);
 }
 
-__device__ void decide_slots(const MsnWork &w, int k, uint32_t odd, int nb, int max_iters,
-                             int et_period, int B, int32_t *synd);
+__device__ __forceinline__ void decide_slots(const MsnWork &w, int k, uint32_t odd, int nb,
+                                             int max_iters, int et_period, int B, int32_t *synd);
+
+__device__ __forceinline__ int wave_of_block() {
+  return __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+}
+
+// A wave's descriptors sit together (slot t of wave w at first + w * slots +
+// t), so one 4-byte load per lane fetches 8 of them: lane l gets dword l & 7
+// of slot 8 g + (l >> 3).  The lane's word of group g.
+__device__ __forceinline__ int desc_group(const MsnDesc *desc, int4 blk, int g) {
+  const int lane = threadIdx.x & 63;
+  const int deg = __builtin_amdgcn_readfirstlane(blk.y);
+  const int d0 = __builtin_amdgcn_readfirstlane(blk.x) + wave_of_block() * deg;
+  const int t = 8 * g + (lane >> 3);
+  return t < deg ? ((const int32_t *)(desc + d0 + 8 * g))[lane] : 0;
+}
+
+// The lane's value of slot T from its group's word: b[run] + lane (runs and
+// bases read across the wave), or the explicit table's value.
+template <int T>
+__device__ __forceinline__ int slot_value(int word) {
+  constexpr int q = 8 * (T & 7);
+  const int lane = threadIdx.x & 63;
+  const uint32_t thr = (uint32_t)__builtin_amdgcn_readlane(word, q + 4);
+  const int b0 = __builtin_amdgcn_readlane(word, q), b1 = __builtin_amdgcn_readlane(word, q + 1),
+            b2 = __builtin_amdgcn_readlane(word, q + 2), b3 = __builtin_amdgcn_readlane(word, q + 3);
+  int base = lane >= (int)(thr & 0xffu) ? b1 : b0;  // s1 <= s2 <= s3
+  base = lane >= (int)((thr >> 8) & 0xffu) ? b2 : base;
+  base = lane >= (int)((thr >> 16) & 0xffu) ? b3 : base;
+  return base + lane;
+}
+template <int T>
+__device__ __forceinline__ int slot_explicit(int word, const int32_t *x) {
+  return x[__builtin_amdgcn_readlane(word, 8 * (T & 7) + 5) + (int)(threadIdx.x & 63)];
+}
+
+template <int T0, int I, bool EXPL>
+__device__ __forceinline__ void slot_values(const int *word, const int32_t *x, int deg, int *v) {
+  if constexpr (I > 0) {
+    slot_values<T0, I - 1, EXPL>(word, x, deg, v);
+    constexpr int t = T0 + I - 1;
+    const int wd = word[t / 8];
+    if constexpr (EXPL)
+      v[I - 1] = t < deg ? slot_explicit<t>(wd, x) : -1;
+    else
+      v[I - 1] = t < deg ? slot_value<t>(wd) : -1;
+  }
+}
+
+// The block's descriptor words, groups 0 .. NW - 1 (desc_group).  Must run
+// with every lane of the wave active: slot_value reads the words across the
+// wave, so lanes that exit early (items past n) must have loaded theirs.
+template <int NW>
+__device__ __forceinline__ void desc_words(const MsnDesc *desc, int4 blk, int (&word)[NW]) {
+  const int deg = __builtin_amdgcn_readfirstlane(blk.y);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) word[i] = 8 * i < deg ? desc_group(desc, blk, i) : 0;
+}
+
+// The lane's values of slots T0 .. T0 + D - 1 of its item (negative: no
+// edge) from the block's table blk = {first descriptor, slots, explicit-wave
+// mask} and its descriptor words (desc_words).
+template <int T0, int D, int NW>
+__device__ __forceinline__ void edge_values(const int (&word)[NW], const int32_t *x, int4 blk,
+                                            int (&v)[D]) {
+  static_assert((T0 + D - 1) / 8 < NW, "descriptor group not loaded");
+  const int deg = __builtin_amdgcn_readfirstlane(blk.y);
+  if ((__builtin_amdgcn_readfirstlane(blk.z) >> wave_of_block()) & 1)
+    slot_values<T0, D, true>(word, x, deg, v);
+  else
+    slot_values<T0, D, false>(word, x, deg, v);
+}
+
 
 // ---------------------------------------------------------------------------
 // Horizontal step (:340-376) of one row (storage position p) for the chunk's
@@ -154,24 +227,21 @@ __device__ void decide_slots(const MsnWork &w, int k, uint32_t odd, int nb, int 
 // and are masked).  L(q) of each edge is LQ - L(r_old) (:387-392); a frame's
 // first step takes L(q) = Lci (LQ = Lci, no old message).  The parity of the
 // last decisions (checkFrame, :236-253) comes from the signs of the same LQ.
-template <int PREC, int D, bool R16>
-__device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, int k, int p, int off,
-                                          const int (&itf)[kF], bool (&par)[kF]) {
+// blk = the block's table (edge_values); its degree is <= D: the
+// straight-line bodies are instantiated at the block degree, the body for
+// degrees above 8 at D = DC with slots past the block degree masked.
+template <int PREC, int D, int NW>
+__device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, int k, int p, int4 blk,
+                                          const int (&word)[NW], const int (&itf)[kF],
+                                          bool (&par)[kF]) {
   typedef typename Math<PREC>::Real Real;
   int cs[D];
   bool ok[D];
+  edge_values<0, D>(word, g.rx, blk, cs);
 #pragma unroll
   for (int t = 0; t < D; ++t) {
-    const int64_t i = off + t * kIB + (int)threadIdx.x;
-    int v;
-    if constexpr (R16) {
-      v = ((const uint16_t *)g.rtab)[i];
-      ok[t] = v != 0xffff;
-    } else {
-      v = ((const int32_t *)g.rtab)[i];
-      ok[t] = v >= 0;
-    }
-    cs[t] = ok[t] ? v : 0;
+    ok[t] = cs[t] >= 0;
+    cs[t] = ok[t] ? cs[t] : 0;
   }
   Real *m1 = (Real *)w.m1, *m2 = (Real *)w.m2;
   const Real *LQ = (const Real *)w.LQ;
@@ -181,10 +251,11 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
   uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M + p;  // [t][p]
   Vec<Real> lq[D];
   uint32_t ab[D];
+  const int deg = __builtin_amdgcn_readfirstlane(blk.y);
 #pragma unroll
   for (int t = 0; t < D; ++t) {
     lq[t] = ldv(LQ + el(k, g.N, cs[t]));
-    ab[t] = alpha[(int64_t)t * g.M];
+    ab[t] = t < deg ? alpha[(int64_t)t * g.M] : 0u;
   }
   // per frame: L(q) in ascending original column, sign product, smallest and
   // second smallest |L(q)| (strict <, first occurrence, DBL_MAX seeds; NaN
@@ -241,7 +312,7 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
 // per frame f, "a row of these blocks is unsatisfied" (bits 12(f+1)..), in
 // two levels (8 group words per chunk, then the chunk's word); no fence and
 // no waiting (a chunk that is not live decides in its block 0 alone).
-template <int PREC, int DC, bool R16, bool FUSE>
+template <int PREC, int DC, bool FUSE>
 __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int mbuf, int max_iters,
                                                  int et_period, int B, int32_t *synd) {
   int k, bi;
@@ -259,18 +330,20 @@ __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int mbuf,
   bool par[kF];
 #pragma unroll
   for (int f = 0; f < kF; ++f) par[f] = false;
+  const int4 rb = g.rblk[bi];  // the block's descriptors, largest degree, explicit waves
+  int word[(DC + 7) / 8];
+  desc_words(g.rdesc, rb, word);  // every lane, before rows past M drop out
   if (p < g.M) {
-    const int2 rb = g.rblk[bi];  // the block's table offset and largest degree
     switch (rb.y) {
 #define LDPC_MSN_ROW(n) \
   case n:               \
-    if constexpr (n <= DC) check_row<PREC, (n <= DC ? n : 1), R16>(g, w, k, p, rb.x, itf, par); \
+    if constexpr (n <= DC) check_row<PREC, (n <= DC ? n : 1)>(g, w, k, p, rb, word, itf, par); \
     break;
       LDPC_MSN_ROW(1) LDPC_MSN_ROW(2) LDPC_MSN_ROW(3) LDPC_MSN_ROW(4) LDPC_MSN_ROW(5)
       LDPC_MSN_ROW(6) LDPC_MSN_ROW(7) LDPC_MSN_ROW(8)
 #undef LDPC_MSN_ROW
       default:
-        if constexpr (DC > 8) check_row<PREC, DC, R16>(g, w, k, p, rb.x, itf, par);
+        if constexpr (DC > 8) check_row<PREC, DC>(g, w, k, p, rb, word, itf, par);
         break;
     }
   }
@@ -339,8 +412,8 @@ __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int mbuf,
 // every check is satisfied (bit f of odd: frame f saw an unsatisfied row);
 // freed (and empty) slots take the next frames of the batch.  The new masks
 // go to mask buffer `nb` (the pass's check read the other one).
-__device__ void decide_slots(const MsnWork &w, int k, uint32_t odd, int nb, int max_iters,
-                             int et_period, int B, int32_t *synd) {
+__device__ __forceinline__ void decide_slots(const MsnWork &w, int k, uint32_t odd, int nb,
+                                             int max_iters, int et_period, int B, int32_t *synd) {
   const int lane = threadIdx.x;
   const bool on = lane < kF;
   const int slot = k * kF + lane;
@@ -461,21 +534,22 @@ __global__ void __launch_bounds__(256) msn_cols(MsnView g, MsnWork w, uint8_t *b
 // Every load of the group is issued before the first is used (m1 and m2 both,
 // rather than selecting by meta first: one load level less); edges past the
 // column's own degree read row 0 and are masked.
-template <typename Real, int T0, int D>
-__device__ __forceinline__ void var_edges(const MsnView &g, const MsnWork &w, int k, int off,
-                                          Vec<Real> &s) {
+template <typename Real, int T0, int D, int NW>
+__device__ __forceinline__ void var_edges(const MsnView &g, const MsnWork &w, int k, int4 blk,
+                                          const int (&word)[NW], Vec<Real> &s) {
   const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
   const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M;
+  int v[D];
+  edge_values<T0, D>(word, g.cx, blk, v);
   bool ok[D];
   int place[D];
   int64_t ro[D];
   uint32_t ai[D];
 #pragma unroll
   for (int t = 0; t < D; ++t) {
-    const uint32_t v = g.ctab[off + (T0 + t) * kIB + (int)threadIdx.x];
-    ok[t] = v != 0xffffffffu;
-    const int rp = ok[t] ? (int)(v & 0xffffffu) : 0;
-    place[t] = ok[t] ? (int)(v >> 24) : 0;
+    ok[t] = v[t] >= 0;
+    const int rp = ok[t] ? (v[t] & 0xffffff) : 0;
+    place[t] = ok[t] ? (v[t] >> 24) : 0;
     ro[t] = el(k, g.M, rp);
     ai[t] = (uint32_t)place[t] * (uint32_t)g.M + (uint32_t)rp;
   }
@@ -501,26 +575,13 @@ __device__ __forceinline__ void var_edges(const MsnView &g, const MsnWork &w, in
     }
 }
 
-// the same for n <= 4 edges from t0 (columns of degree > 8)
+// the same for columns of degree > 8: edges 8 .. deg - 1, four at a time
 template <typename Real>
-__device__ void var_edges_rt(const MsnView &g, const MsnWork &w, int k, int off, int t0, int n,
-                             Vec<Real> &s) {
-  const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
-  const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M;
-  for (int t = t0; t < t0 + n; ++t) {
-    const uint32_t v = g.ctab[off + t * kIB + (int)threadIdx.x];
-    if (v == 0xffffffffu) continue;
-    const int rp = (int)(v & 0xffffffu), place = (int)(v >> 24);
-    const int64_t ro = el(k, g.M, rp);
-    const MetaWord mt = ld_meta(w.meta + ro);
-    const uint32_t ab = alpha[(int64_t)place * g.M + rp];
-#pragma unroll
-    for (int f = 0; f < kF; ++f) {
-      const int m = (int)((mt >> (8 * f)) & 0xffu);
-      const Real *src = place == (m & 63) - 1 ? m2 : m1;
-      s.v[f] = s.v[f] + (Real)(((m >> 6) - 1) * alpha_of(ab, f)) * src[ro + f];
-    }
-  }
+__device__ void var_edges_rt(const MsnView &g, const MsnWork &w, int k, int4 blk,
+                             const int (&word)[2], Vec<Real> &s) {
+  const int deg = __builtin_amdgcn_readfirstlane(blk.y);
+  if (deg > 8) var_edges<Real, 8, 4>(g, w, k, blk, word, s);
+  if (deg > 12) var_edges<Real, 12, 4>(g, w, k, blk, word, s);
 }
 
 // Vertical step (:379-403), one column per lane, the chunk's F frames in the
@@ -559,6 +620,9 @@ __global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs 
       if (bi == 0 && threadIdx.x == 0 && a.iters) a.iters[fr] = w.used[k * kF + f];
     }
   }
+  const int4 cb = g.cblk[bi];  // the block's descriptors, largest degree, explicit waves
+  int word[(DV + 7) / 8];
+  if (run) desc_words(g.cdesc, cb, word);  // every lane, before columns past N drop out
   if (!(run | fill) || x >= g.N) return;
   Vec<float> lci = ldv_nt(w.L + ci);
   if (fill) {
@@ -573,21 +637,20 @@ __global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs 
 #pragma unroll
   for (int f = 0; f < kF; ++f) s.v[f] = Real(0);
   if (run) {
-    const int2 cb = g.cblk[bi];  // the block's table offset and largest degree
     switch (cb.y) {
 #define LDPC_MSN_COL(n)                                                    \
   case n:                                                                  \
-    if constexpr (n <= DV) var_edges<Real, 0, (n < 4 ? n : 4)>(g, w, k, cb.x, s); \
-    if constexpr (n > 4 && n <= DV) var_edges<Real, 4, (n > 4 ? n - 4 : 1)>(g, w, k, cb.x, s); \
+    if constexpr (n <= DV) var_edges<Real, 0, (n < 4 ? n : 4)>(g, w, k, cb, word, s); \
+    if constexpr (n > 4 && n <= DV) var_edges<Real, 4, (n > 4 ? n - 4 : 1)>(g, w, k, cb, word, s); \
     break;
       LDPC_MSN_COL(1) LDPC_MSN_COL(2) LDPC_MSN_COL(3) LDPC_MSN_COL(4) LDPC_MSN_COL(5)
       LDPC_MSN_COL(6) LDPC_MSN_COL(7) LDPC_MSN_COL(8)
 #undef LDPC_MSN_COL
       default:
         if constexpr (DV > 8) {
-          var_edges<Real, 0, 4>(g, w, k, cb.x, s);
-          var_edges<Real, 4, 4>(g, w, k, cb.x, s);
-          for (int t0 = 8; t0 < cb.y; t0 += 4) var_edges_rt<Real>(g, w, k, cb.x, t0, min(4, cb.y - t0), s);
+          var_edges<Real, 0, 4>(g, w, k, cb, word, s);
+          var_edges<Real, 4, 4>(g, w, k, cb, word, s);
+          var_edges_rt<Real>(g, w, k, cb, word, s);
         }
         break;
     }
@@ -624,18 +687,14 @@ void msn_pass_f(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int par
   typedef typename Math<PREC>::Real Real;
   const int rblocks = w.nb_check * w.chunks, cblocks = w.nb_var * w.chunks, nb = par ^ 1;
   static_assert(kMsnFrames == kF, "");
-#define LDPC_MSN_CHECK(DC, R16) \
-  msn_check<PREC, DC, R16, FUSE><<<rblocks, 256, 0, st>>>(g, w, par, a.max_iters, a.et_period, a.B, a.synd)
-  if (g.dc_max <= 8) {
-    if (g.r16)
-      LDPC_MSN_CHECK(8, true);
-    else
-      LDPC_MSN_CHECK(8, false);
-  } else if (g.dc_max <= 16) {
-    LDPC_MSN_CHECK(16, false);
-  } else {
-    LDPC_MSN_CHECK(32, false);
-  }
+#define LDPC_MSN_CHECK(DC) \
+  msn_check<PREC, DC, FUSE><<<rblocks, 256, 0, st>>>(g, w, par, a.max_iters, a.et_period, a.B, a.synd)
+  if (g.dc_max <= 8)
+    LDPC_MSN_CHECK(8);
+  else if (g.dc_max <= 16)
+    LDPC_MSN_CHECK(16);
+  else
+    LDPC_MSN_CHECK(32);
 #undef LDPC_MSN_CHECK
   if (!FUSE) msn_decide<<<w.chunks, 256, 0, st>>>(w, par, a.max_iters, a.et_period, a.B, a.synd);
   if (!w.out_var) {
@@ -796,28 +855,87 @@ long contiguity(const MsnTables &t) {
 
 // A slot-major table full[t][x] (D x n, -1 past each item's degree) cut in
 // blocks of the kernels' 256 items: block b keeps only its largest degree's
-// slots, [t][lane] at blk[2b] with blk[2b+1] slots.
+// slots, one descriptor per (slot, wave) (MsnDesc: up to 4 runs of
+// consecutive values), a wave's slots together.  A wave with a slot of more
+// than 4 runs keeps every slot's 64 values in `x` instead (at each
+// descriptor's xoff).  blk[4b ..] = {first descriptor, slots, explicit-wave
+// mask, 0}.
 void msn_block_tables(const std::vector<int32_t> &full, int D, int n, std::vector<int32_t> &blk,
-                      std::vector<int32_t> &tab) {
-  const int nb = (n + kIB - 1) / kIB;
-  blk.assign((size_t)2 * nb, 0);
-  tab.clear();
+                      std::vector<MsnDesc> &desc, std::vector<int32_t> &x) {
+  const int nb = (n + kIB - 1) / kIB, nw = kIB / 64;
+  blk.assign((size_t)4 * nb, 0);
+  desc.clear();
+  x.clear();
   for (int b = 0; b < nb; ++b) {
     int deg = 0;
     for (int i = 0; i < kIB; ++i) {
-      const int x = b * kIB + i;
-      if (x >= n) break;
+      const int c = b * kIB + i;
+      if (c >= n) break;
       for (int t = 0; t < D; ++t)
-        if (full[(size_t)t * n + x] != -1) deg = std::max(deg, t + 1);
+        if (full[(size_t)t * n + c] != -1) deg = std::max(deg, t + 1);
     }
-    blk[2 * b] = (int32_t)tab.size();
-    blk[2 * b + 1] = deg;
-    for (int t = 0; t < deg; ++t)
-      for (int i = 0; i < kIB; ++i) {
-        const int x = b * kIB + i;
-        tab.push_back(x < n ? full[(size_t)t * n + x] : -1);
+    const size_t d0 = desc.size();
+    blk[4 * b] = (int32_t)d0;
+    blk[4 * b + 1] = deg;
+    desc.resize(d0 + (size_t)deg * nw);
+    for (int w = 0; w < nw; ++w) {
+      std::vector<MsnDesc> mine((size_t)deg);
+      std::vector<int32_t> vals((size_t)deg * 64);
+      bool explicit_wave = false;
+      for (int t = 0; t < deg; ++t) {
+        int32_t *v = &vals[(size_t)t * 64];
+        for (int l = 0; l < 64; ++l) {
+          const int c = b * kIB + w * 64 + l;
+          v[l] = c < n ? full[(size_t)t * n + c] : -1;
+        }
+        int start[64], runs = 0;
+        for (int l = 0; l < 64; ++l) {
+          const bool cont = l > 0 && ((v[l - 1] < 0 && v[l] < 0) || (v[l - 1] >= 0 && v[l] == v[l - 1] + 1));
+          if (!cont) start[runs++] = l;
+        }
+        MsnDesc &d = mine[t];
+        d = MsnDesc{};
+        d.xoff = -1;
+        explicit_wave |= runs > 4;
+        uint32_t thr = 0;
+        for (int r = 0; r < 4; ++r) {
+          const int a = r < runs ? start[r] : 64;
+          d.b[r] = r < runs ? (v[a] < 0 ? kMsnNoEdge : v[a] - a) : kMsnNoEdge;
+          if (r >= 1) thr |= (uint32_t)a << (8 * (r - 1));
+        }
+        d.thr = thr;
       }
+      if (explicit_wave && deg > 0) {
+        blk[4 * b + 2] |= 1 << w;
+        for (int t = 0; t < deg; ++t) mine[t].xoff = (int32_t)(x.size() + (size_t)t * 64);
+        x.insert(x.end(), vals.begin(), vals.end());
+      }
+      for (int t = 0; t < deg; ++t) desc[d0 + (size_t)w * deg + t] = mine[t];
+    }
   }
+  // self-check: decode every (block, wave, slot, lane) as the kernels do
+  // (desc_group / slot_value / slot_explicit) and compare with the table
+  for (int b = 0; b < nb; ++b)
+    for (int w = 0; w < nw; ++w)
+      for (int t = 0; t < blk[4 * b + 1]; ++t) {
+        const MsnDesc &d = desc[(size_t)blk[4 * b] + (size_t)w * blk[4 * b + 1] + t];
+        const bool expl = (blk[4 * b + 2] >> w) & 1;
+        for (int l = 0; l < 64; ++l) {
+          const int c = b * kIB + w * 64 + l;
+          const int32_t want = c < n ? full[(size_t)t * n + c] : -1;
+          int32_t got;
+          if (expl) {
+            got = x[(size_t)d.xoff + l];
+          } else {
+            int base = l >= (int)(d.thr & 0xffu) ? d.b[1] : d.b[0];
+            base = l >= (int)((d.thr >> 8) & 0xffu) ? d.b[2] : base;
+            base = l >= (int)((d.thr >> 16) & 0xffu) ? d.b[3] : base;
+            got = base + l;
+          }
+          if ((want < 0) != (got < 0) || (want >= 0 && want != got))
+            throw std::runtime_error("msn_block_tables: descriptor self-check failed");
+        }
+      }
 }
 
 // Storage-ordered tables of H (rows rpos, columns cpos): row offsets and
@@ -858,13 +976,8 @@ void msn_tables(int M, int N, const std::vector<int32_t> &rp0, const std::vector
   t.corig = corig;
   t.cpos = cpos;
   t.rpos = rpos;
-  msn_block_tables(t.rcs, dc, M, t.rblk, t.rtab);
-  msn_block_tables(t.crs, dv, N, t.cblk, t.ctab);
-  t.r16 = N <= 0xffff;
-  if (t.r16) {
-    t.rtab16.resize(t.rtab.size());
-    for (size_t i = 0; i < t.rtab.size(); ++i) t.rtab16[i] = (uint16_t)(t.rtab[i] < 0 ? 0xffff : t.rtab[i]);
-  }
+  msn_block_tables(t.rcs, dc, M, t.rblk, t.rdesc, t.rx);
+  msn_block_tables(t.crs, dv, N, t.cblk, t.cdesc, t.cx);
   // outputs from the variable pass need the info columns in place, 8 per byte
   t.out_var = M % 8 == 0;
   for (int c = M; c < N && t.out_var; ++c) t.out_var = cpos[c] == c;

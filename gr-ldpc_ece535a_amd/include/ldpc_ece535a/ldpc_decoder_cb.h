@@ -36,8 +36,11 @@ class LDPC_ECE535A_API ldpc_decoder_cb : virtual public gr::block {
   static sptr make(const int method);
 
   /*! Additive overload: iteration cap (the reference hard-codes 5) and
-   *  arithmetic precision (0 = f64 parity mode, 1 = f32, 2 = f64 with
-   *  glibc-identical tanh). */
+   *  arithmetic precision (include/ldpc_hip.h LDPC_PREC_*): 0 = f64, the
+   *  reference's arithmetic bit for bit (glibc's tanh / log reproduced,
+   *  correctly rounded divisions); 1 = f32; 2 = the same f64 functions one
+   *  value at a time (also exact); 3 = f64 with compact tanh / log (within
+   *  3 / 1 ulp of glibc, not exact). */
   static sptr make(const int method, const int iterations, const int precision = 0);
 
   /*! Additive overload: a runtime H in place of the compiled-in matrix

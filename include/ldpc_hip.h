@@ -59,7 +59,10 @@ extern "C" {
  *                  operations in its order, glibc's tanh(m/2) and
  *                  log((1+T)/(1-T)) reproduced exactly, correctly rounded
  *                  divisions -- hard decisions, posteriors and iteration
- *                  counts identical to the reference CPU decoder's
+ *                  counts identical to the reference CPU decoder's as built
+ *                  against glibc >= 2.28 on an FMA-capable x86-64 host (the
+ *                  __log_fma variant of log; an older glibc's log, or the
+ *                  non-FMA variant, could differ in the last bit)
  *   F64_LIBM       the same results, each tanh / log / division evaluated on
  *                  its own (no shared reciprocal): a second evaluation of F64
  *   F64_FAST       double with compact tanh/log (within 3 / 1 ulp of glibc):
@@ -247,8 +250,7 @@ int ldpc_decode_windows(ldpc_ctx *ctx, int method, int max_iters, int et_period,
  * (hipStream_t, NULL = the context's own stream) and returns without
  * synchronising -- except min-sum on a large-code context, whose pass loop
  * stops on a progress counter the host reads back: that call returns when
- * its decode has finished (LDPC_MS_ASYNC=1 enqueues the worst-case number of
- * passes instead and returns at once, ~11 % slower on config 4).  One host
+ * its decode has finished.  One host
  * thread may enqueue on several streams: small-code launches on different
  * streams run concurrently (each stream has its own frame queue), large-code
  * launches share the context's workspace and are ordered after the previous

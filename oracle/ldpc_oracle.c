@@ -714,14 +714,16 @@ void orc_block_init(orc_block *blk, int method, int iterations,
   blk->M = M;
   blk->N = N;
   blk->H = Hr;
+  blk->decodes = 0;
 }
 
 /* One window's decode and frame check for the loop below: dense H (the
  * block's own, :155-166) or, for large codes, the sparse restatement of the
  * same decoders (g != NULL).  Returns checkFrame's count. */
-static int block_decode_check(const orc_block *blk, const orc_graph *g, const int32_t *rp,
+static int block_decode_check(orc_block *blk, const orc_graph *g, const int32_t *rp,
                               const int32_t *ci, const double *tx, int *v) {
   const int threshold = blk->M / 8; /* :142 */
+  blk->decodes++;
   if (g) {
     orc_decode_graph(blk->method, g, tx, blk->iterations, 1, v, NULL);
     return orc_check_frame_sparse(rp, ci, blk->M, v, threshold);

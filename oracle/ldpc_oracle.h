@@ -125,6 +125,8 @@ typedef struct orc_block {
   unsigned errors; /* d_errors */
   int M, N;
   const uint8_t *H; /* reordered H, M x N */
+  long long decodes; /* windows decoded so far (the retry's "-tx" included; a
+                        measurement counter, not reference state) */
 } orc_block;
 
 void orc_block_init(orc_block *blk, int method, int iterations,

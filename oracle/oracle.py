@@ -193,7 +193,8 @@ def dense_to_csr(H):
 class _OrcBlock(ctypes.Structure):
     _fields_ = [("method", ctypes.c_int), ("iterations", ctypes.c_int),
                 ("state", ctypes.c_int), ("errors", ctypes.c_uint),
-                ("M", ctypes.c_int), ("N", ctypes.c_int), ("H", ctypes.c_void_p)]
+                ("M", ctypes.c_int), ("N", ctypes.c_int), ("H", ctypes.c_void_p),
+                ("decodes", ctypes.c_longlong)]
 
 
 class Block:
@@ -226,6 +227,11 @@ class Block:
     def errors(self):
         return self.s.errors
 
+    @property
+    def decodes(self):
+        """Windows decoded so far, each "-tx" retry counted (a measurement)."""
+        return self.s.decodes
+
     def general_work(self, noutput_items, in_complex):
         """in_complex: complex64 array (ninput_items long).  Returns
         (out_bytes, consumed)."""
@@ -247,12 +253,14 @@ class Block:
         return out[:made].copy(), used.value
 
 
-def run_stream(method, Hr, samples, iterations=5, chunks=None, out_space=1 << 30, csr=None):
+def run_stream(method, Hr, samples, iterations=5, chunks=None, out_space=1 << 30, csr=None,
+               stats=None):
     """Feed a complex stream through the restated block the way the GR
     scheduler does: input arrives in `chunks` (sizes), unconsumed input is
     kept, and general_work is called again until it consumes nothing.
     Returns the concatenated output bytes.  csr: a large code's (M, N,
-    row_ptr, col_idx) instead of Hr (sparse window decodes)."""
+    row_ptr, col_idx) instead of Hr (sparse window decodes).  stats: a dict
+    that receives the number of windows the loop decoded ("decodes")."""
     blk = Block(method, Hr, iterations, csr=csr)
     samples = np.asarray(samples, np.complex64)
     ends = list(np.cumsum(chunks)) if chunks is not None else []
@@ -265,4 +273,6 @@ def run_stream(method, Hr, samples, iterations=5, chunks=None, out_space=1 << 30
             pos += used
             if used == 0:
                 break
+    if stats is not None:
+        stats["decodes"] = int(blk.decodes)
     return np.concatenate(outs) if outs else np.zeros(0, np.uint8)

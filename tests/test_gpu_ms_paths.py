@@ -1,8 +1,8 @@
-"""Large-code min-sum has three implementations (ldpc_capi.hip decode_graph):
-the narrow-chunk frame pipeline (ldpc_graph_msn.hip, the default,
-LDPC_MS_PIPELINE=2), the 64-frame-chunk pipeline with compressed check
-messages (ldpc_graph_ms.hip, LDPC_MS_PIPELINE=1) and the edge-message passes
-(ldpc_graph.hip, LDPC_MS_PIPELINE=0), chosen at context creation.  Both must reproduce the oracle exactly: the reference's
+"""Large-code min-sum has two implementations (ldpc_capi.hip decode_graph):
+the narrow-chunk frame pipeline with compressed check messages
+(ldpc_graph_msn.hip, the default, LDPC_MS_PIPELINE=2) and the edge-message
+passes (ldpc_graph.hip, LDPC_MS_PIPELINE=0), chosen at context creation.
+Both must reproduce the oracle exactly: the reference's
 fixtures on its own H forced onto the large-code path (hard decisions, packed
 bytes, iterations, syndromes, posteriors), the DVB-S2-like code against the
 sparse restatement, non-finite samples, et_period 5, and batches far larger
@@ -15,8 +15,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-MODES = ["2", "1", "0"]
-IDS = ["narrow", "pipeline", "edge"]
+MODES = ["2", "0"]
+IDS = ["narrow", "edge"]
 
 
 def _decoder(mode, **kw):
@@ -136,3 +136,37 @@ def test_narrow_variants_dvbs2(env):
         np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
     edge = _decoder("0", csr=csr).decode(y, method=0, max_iters=30, want_llr=True)
     np.testing.assert_array_equal(out["llr"].view(np.uint32), edge["llr"].view(np.uint32))
+
+
+@pytest.mark.parametrize("hi_groups,hi_deg,dc", [(3, 8, 14), (5, 12, 20)],
+                         ids=["dc14", "dc20"])
+@pytest.mark.parametrize("mode", MODES, ids=IDS)
+def test_high_check_degree_vs_sparse_oracle(mode, hi_groups, hi_deg, dc):
+    """Rate-3/4 IRA codes in the DVB-S2 style (N = 7200, 360-column groups)
+    whose rows have 13-14 and 19-20 edges: the narrow pipeline's check pass
+    then runs its 16- and 32-slot bodies with the slots past each block's
+    degree masked, and its variable pass the degree-12 columns; every f64
+    output equals the sparse oracle's, at an Eb/N0 beyond the code's reach
+    and at one within it."""
+    from ldpc_ece535a import codes
+    from oracle import oracle as orc
+    table = codes.dvbs2_like_table(3, K=5400, N=7200, hi_groups=hi_groups, hi_deg=hi_deg,
+                                   lo_deg=3)
+    csr = codes.ira_from_table(table, 5400, 7200)
+    M, N, rp, ci = csr
+    assert int(np.diff(rp).max()) == dc
+    d = _decoder(mode, csr=csr)
+    rng = np.random.Generator(np.random.PCG64(hi_deg))
+    info = rng.integers(0, 2, size=(200, N - M), dtype=np.uint8)
+    x = 2.0 * codes.ira_encode(csr, info) - 1.0
+    n = rng.standard_normal(x.shape)
+    for db in (3.0, 6.0):  # beyond / within the rate-3/4 code's reach
+        y = (x + np.sqrt(10 ** (-db / 10)) * n).astype(np.float32)
+        out = d.decode(y, method=0, max_iters=40, precision=0)
+        ref = orc.decode_batch_sparse(0, rp, ci, M, N, y, 40, nthreads=16)
+        for k in ("bits", "packed", "iters", "synd"):
+            np.testing.assert_array_equal(out[k], ref[k], err_msg="%s %g dB" % (k, db))
+    # f32: decisions only (6 dB: most frames decode)
+    assert (ref["synd"] == 0).mean() > 0.5
+    out = d.decode(y, method=0, max_iters=40, precision=1)
+    assert ((out["packed"] == np.packbits(info, axis=1)).all(axis=1)).mean() > 0.5

@@ -77,3 +77,20 @@ def test_forced_identity():
             os.environ["LDPC_MSN_ORDER"] = old
     assert r["order"] == 0
     assert np.array_equal(r["rpos"], np.arange(csr[0]))
+
+
+def test_edge_descriptor_self_check_high_degree_codes():
+    """The edge tables are run-length descriptors per (wave, slot)
+    (ldpc_graph.hpp MsnDesc) built with a host self-check that decodes every
+    entry the way the kernels do and throws on a mismatch; plan_storage_order
+    runs that build.  Codes with row degrees 6-20 and column degrees 1-12,
+    in both storage orders."""
+    for hg, hd in ((3, 8), (5, 12)):
+        csr = codes.ira_from_table(codes.dvbs2_like_table(3, K=5400, N=7200, hi_groups=hg,
+                                                          hi_deg=hd, lo_deg=3), 5400, 7200)
+        for force in ("0", "1"):
+            os.environ["LDPC_MSN_ORDER"] = force
+            try:
+                assert L._capi.plan_storage_order(csr)["order"] == int(force)
+            finally:
+                del os.environ["LDPC_MSN_ORDER"]
