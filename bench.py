@@ -123,6 +123,22 @@ def sigma_of(ebn0):
     return float(np.sqrt(10.0 ** (-ebn0 / 10.0)))
 
 
+_STREAMS = {}
+
+
+def bench_streams(torch, dev, n):
+    """The process's first n HIP streams, created once and reused by every
+    measurement: torch hands out streams round-robin from a pool, and the
+    streams created later in a process can share hardware queues with one
+    another -- measured: after ~10 extra streams, four batches in flight ran
+    at 800 instead of 1 120 Mbit/s (profiles/round4/headline/streams_ab.txt)."""
+    key = (str(dev),)
+    have = _STREAMS.setdefault(key, [])
+    while len(have) < n:
+        have.append(torch.cuda.Stream(dev))
+    return have[:n]
+
+
 def synth_device(L, torch, dec, B, ebn0, seed, dev, check_frames=64):
     """Frames made on the GPU: Philox bits -> ldpc_encode_device -> BPSK +
     AWGN.  ebn0 may be a scalar or a per-frame array (config 5).  Returns
@@ -131,7 +147,7 @@ def synth_device(L, torch, dec, B, ebn0, seed, dev, check_frames=64):
     K, N = dec.K, dec.N
     # one explicit (non-null) stream for every step: a NULL stream argument
     # would mean the context's own stream for ldpc_encode_device
-    st = torch.cuda.Stream(dev)
+    st = bench_streams(torch, dev, 1)[0]
     sp = ctypes.c_void_p(st.cuda_stream)
     with torch.cuda.stream(st):
         d_bits = torch.empty((B, K), dtype=torch.uint8, device=dev)
@@ -257,7 +273,7 @@ def plan_batch(B, world, rank, strong):
 
 
 def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, dist=None,
-                 inflight=1):
+                 inflight=1, streams=None):
     """Decode `steps` batches with `inflight` batches in flight: step k
     decodes inputs[k % D] on stream k % D into that stream's output buffers.
     Returns dict(wall, span_ms, per_launch_ms, iters, outs) where span_ms is
@@ -267,7 +283,8 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
     synd) of the last decode of batch d."""
     D = max(1, inflight)
     dev = inputs[0].device
-    streams = [torch.cuda.Stream(dev) for _ in range(D)]
+    if streams is None:
+        streams = bench_streams(torch, dev, D)
     sps = [ctypes.c_void_p(s.cuda_stream) for s in streams]
     outs = [(torch.empty((B, dec.KB), dtype=torch.uint8, device=dev),
              torch.empty(B, dtype=torch.int32, device=dev),
@@ -483,6 +500,7 @@ def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
     from ldpc_ece535a import codes
     csr = codes.dvbs2_like(0)
     dec = L.Decoder(csr=csr, device=dev.index or 0)
+    pipe = dec.pipeline()
     B = 1024
     d_y, d_bits = synth_device(L, torch, dec, B, args.ebn0, seed, dev)
     data = d_bits.cpu().numpy()
@@ -501,15 +519,22 @@ def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
             "alg_GB/s_note": "edge-message byte model (SURVEY 8(d)) per decode time; the "
                              "narrow pipeline moves ~0.53x those bytes (DESIGN section 5)",
             "frames_decoded_to_sent_data": int((pk == np.packbits(data, axis=1)).all(axis=1).sum())}
-        t = (load_pmc(args.pmc_json, "dvb0_f64_b1024_i50_db2") or {}).get("hbm_bytes_per_launch")
-        if p == 0 and t and args.iters == 50 and args.ebn0 == 2.0:
+        ent = load_pmc(args.pmc_json, "dvb0_f64_b1024_i50_db2") or {}
+        t = ent.get("hbm_bytes_per_launch")
+        # the measured traffic applies only to the pipeline configuration it
+        # was taken at (frames per chunk, chunks in flight)
+        if p == 0 and t and args.iters == 50 and args.ebn0 == 2.0 and ent.get("pipeline") == pipe:
             out["min-sum " + name]["measured_GB/s"] = round(t / (k * 1e-3) / 1e9, 1)
             out["min-sum " + name]["measured_frac_of_8TB/s"] = round(t / (k * 1e-3) / 8e12, 4)
+            out["min-sum " + name]["measured_MB_per_frame_iteration"] = round(
+                t / float(it.sum()) / 1e6, 3)
+            out["min-sum " + name]["pmc_source"] = ent.get("source")
         if p == 0 and cpu_sample:
             kept = dict(y=d_y[:cpu_sample].cpu().numpy(), pk=pk[:cpu_sample],
                         it=it[:cpu_sample], K=dec.K)
     out["code"] = ("DVB-S2-like N=64800 K=32400 E=226799 (synthetic rate-1/2 address table, "
                    "ldpc_ece535a.codes.dvbs2_like(0)), B=1024, %d-iteration cap" % args.iters)
+    out["pipeline"] = pipe
     dec.close()
 
     def check():
@@ -530,7 +555,7 @@ def config4_variant(L, torch, dev, args, seed, steps=5, warmup=1, cpu_sample=0):
     return out, check
 
 
-def config5_variant(L, torch, dec, args, dev, sizes=(1, 16, 256, 4096, 65536), check_b=4096):
+def config5_variant(L, torch, args, dev, sizes=(1, 16, 256, 4096, 65536), check_b=4096):
     """Config 5 (BASELINE configs[4]): the syndrome checked every 5
     iterations (et_period 5, the reference checks every iteration,
     lib/ldpc_decoder_cb_impl.cc:535-537 / :406-408), each frame at its own
@@ -539,6 +564,9 @@ def config5_variant(L, torch, dec, args, dev, sizes=(1, 16, 256, 4096, 65536), c
     min-sum f64.  Returns (results, check): check() compares the first
     `check_b` frames of the B = check_b and largest launches with the
     oracle's et_period restatement (CPU, after the GPU work)."""
+    # its own context (frame queues, streams): the headline's decoder is
+    # left exactly as the other variants leave it
+    dec = L.Decoder(device=dev.index or 0)
     rng = np.random.Generator(np.random.PCG64(args.seed + 5))
     Bmax = max(sizes)
     dbs = rng.integers(0, 5, size=Bmax).astype(np.float64)
@@ -560,7 +588,8 @@ def config5_variant(L, torch, dec, args, dev, sizes=(1, 16, 256, 4096, 65536), c
             if Bs in (check_b, Bmax):
                 kept[(m, Bs)] = (r["outs"][0][0][:check_b].cpu().numpy(), it[:check_b])
         out[name] = rows
-    dec.set_launch_mode(1)
+    Hr = dec.H.copy()
+    dec.close()
 
     def check():
         if not kept or args.no_cpu_baseline:
@@ -569,7 +598,7 @@ def config5_variant(L, torch, dec, args, dev, sizes=(1, 16, 256, 4096, 65536), c
         threads, _ = cpu_share()
         llr = d_y[:check_b].cpu().numpy()
         for name, m in (("sum-product f64 (exact)", 1), ("min-sum f64", 0)):
-            ref = orc.decode_batch(m, dec.H, llr, args.iters, nthreads=threads, et_period=5)
+            ref = orc.decode_batch(m, Hr, llr, args.iters, nthreads=threads, et_period=5)
             bad_pk = bad_it = 0
             for (mm, Bs), (pk, it) in kept.items():
                 if mm == m:
@@ -582,17 +611,19 @@ def config5_variant(L, torch, dec, args, dev, sizes=(1, 16, 256, 4096, 65536), c
     return out, check
 
 
-def time_variant(timer, dec, torch, inputs, B, m, iters, et, p, steps, warmup, D, min_s=0.03):
+def time_variant(timer, dec, torch, inputs, B, m, iters, et, p, steps, warmup, D, min_s=0.03,
+                 streams=None):
     """A variant timed over max(steps, enough steps for min_s seconds): a few
     dozen short launches would time the clock ramp and the pipeline's fill and
     drain rather than the decoder, and the last variant's run is what the GPU
     was doing just before the headline's warmup (its clock has ramped).
     Returns (result, steps timed)."""
-    r = timer(dec, torch, inputs, B, m, iters, et, p, steps, warmup, inflight=D)
+    r = timer(dec, torch, inputs, B, m, iters, et, p, steps, warmup, inflight=D, streams=streams)
     need = int(np.ceil(min_s / max(r["wall"] / steps, 1e-6)))
     if need > steps:
         steps = need
-        r = timer(dec, torch, inputs, B, m, iters, et, p, steps, warmup, inflight=D)
+        r = timer(dec, torch, inputs, B, m, iters, et, p, steps, warmup, inflight=D,
+                  streams=streams)
     return r, steps
 
 
@@ -609,7 +640,7 @@ def gpu_variants(L, torch, dec, args, dev, inputs, B, D, prec, dvb, world, rank)
             L, torch, dev, args, args.seed + 31,
             cpu_sample=0 if (args.no_cpu_baseline or rank != 0) else 1024)
     if not dvb and not args.no_config5:
-        var["config5"], res["config5_check"] = config5_variant(L, torch, dec, args, dev)
+        var["config5"], res["config5_check"] = config5_variant(L, torch, args, dev)
     if not dvb and not args.no_block and world == 1:
         from ldpc_ece535a import blocks
         with _quiet_stdout():
@@ -795,6 +826,8 @@ def main():
     workload_key = "%s%d_%s_b%d_i%d_db%g" % ("dvb" if dvb else "sp", args.method, args.precision,
                                             args.batch, args.iters, args.ebn0)
     entry = load_pmc(args.pmc_json, workload_key) or {}
+    if dvb and entry.get("pipeline") != dec.pipeline():
+        entry = {}  # taken at another pipeline configuration: not this run's traffic
     pmc = entry.get("pmc")
     traffic = entry.get("hbm_bytes_per_launch")
 

@@ -39,11 +39,6 @@ struct ldpc_ctx {
   uint16_t *d_lane_col = nullptr;  // small-code LDS layout (ldpc_layout.hpp)
   uint8_t *d_col_lane = nullptr;
   uint64_t dpos[2] = {0, 0};
-  // packed sum-product kernel (ldpc_kernels.hpp PackedCell); pF = 0: not used
-  ldpc::PackedCell *d_pcells = nullptr;
-  ldpc::PackedColRec *d_pcols = nullptr;
-  uint64_t *d_prowmask = nullptr;
-  int pF = 0, pfull = 0;
   int layout_model[5] = {0, 0, 0, 0, 0};  // searched?, modelled cc / ec, plain cc / ec
   void *d_stage = nullptr;
   size_t stage_bytes = 0;
@@ -61,7 +56,7 @@ struct ldpc_ctx {
   // edge-message passes (ldpc_graph.hip)
   int ms_mode = 2;
   ldpc::MsnTables msn;  // storage order of the narrow pipeline
-  int32_t *d_msn[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // rblk cblk rx cx corig cpos
+  int32_t *d_msn[4] = {nullptr, nullptr, nullptr, nullptr};  // rx cx corig cpos
   ldpc::MsnDesc *d_msnd[2] = {nullptr, nullptr};                               // rdesc cdesc
   // small-code frame queues: one monotonic counter per stream that has
   // launched on this context (ldpc_kernels.hpp DecodeArgs::ticket)
@@ -288,66 +283,6 @@ int build_tables(ldpc_ctx *ctx, std::vector<EdgeRowRec> &erecs, std::vector<Edge
   return LDPC_OK;
 }
 
-// Tables of the packed sum-product kernel (ldpc_kernels.hpp PackedCell) for
-// codes with N, M <= 64, dc <= 6, dv <= 3 and room for F >= 2 frames in 512
-// cells with each frame's whole slots aligned: F full + ceil(F rem / 64) <= 8
-// (full = E / 64, rem = E % 64), F <= 4.  Returns F (0: the code does not fit).
-int build_packed(const ldpc_ctx *ctx, std::vector<ldpc::PackedCell> &pc,
-                 std::vector<ldpc::PackedColRec> &pcol, std::vector<uint64_t> &prow,
-                 int &full_out) {
-  const int M = ctx->M, N = ctx->N, E = ctx->E;
-  if (N > 64 || M > 64 || ctx->dc_max > 6 || ctx->dv_max > 3 || E <= 0) return 0;
-  const int full = E / 64, rem = E % 64;
-  int F = ldpc::kPackedFramesMax;
-  while (F >= 2 && F * full + (F * rem + 63) / 64 > ldpc::kPackedCells) --F;
-  if (F < 2) return 0;
-  full_out = full;
-  const uint8_t *H = ctx->H.data();
-  std::vector<int> erow, ecol;
-  std::vector<std::vector<int>> row_edges(M), col_edges(N);
-  for (int j = 0; j < M; ++j)
-    for (int i = 0; i < N; ++i)
-      if (H[(size_t)j * N + i]) {
-        const int e = (int)erow.size();
-        erow.push_back(j);
-        ecol.push_back(i);
-        row_edges[j].push_back(e);
-        col_edges[i].push_back(e);
-      }
-  // cell of frame f's edge e
-  auto cell = [&](int f, int e) {
-    return e < 64 * full ? 64 * full * f + e : 64 * full * F + rem * f + (e - 64 * full);
-  };
-  pc.assign(64 * ldpc::kPackedCells, ldpc::PackedCell{});
-  for (auto &c : pc) {
-    std::fill(std::begin(c.nbr), std::end(c.nbr), kNone);
-    std::fill(std::begin(c.oth), std::end(c.oth), kNone);
-    c.rcell = kNone;
-  }
-  for (int f = 0; f < F; ++f)
-    for (int e = 0; e < E; ++e) {
-      ldpc::PackedCell &c = pc[cell(f, e)];
-      int k = 0;
-      for (int n : row_edges[erow[e]])
-        if (n != e) c.nbr[k++] = (uint16_t)cell(f, n);  // ascending column
-      k = 0;
-      for (int n : col_edges[ecol[e]])
-        if (n != e) c.oth[k++] = (uint16_t)cell(f, n);  // ascending row
-      c.rcell = (uint16_t)(f * 64 + ecol[e]);
-    }
-  pcol.assign(64, ldpc::PackedColRec{});
-  for (int l = 0; l < 64; ++l)
-    for (int f = 0; f < ldpc::kPackedFramesMax; ++f)
-      for (int k = 0; k < 3; ++k)
-        pcol[l].e[f][k] = (l < N && f < F && k < (int)col_edges[l].size())
-                              ? (uint16_t)cell(f, col_edges[l][k])
-                              : kNone;
-  prow.assign((size_t)M, 0);
-  for (int j = 0; j < M; ++j)
-    for (int i = 0; i < N; ++i)
-      if (H[(size_t)j * N + i]) prow[j] |= 1ull << i;
-  return F;
-}
 
 int ensure_stage(ldpc_ctx *ctx, size_t bytes) {
   if (bytes <= ctx->stage_bytes) return LDPC_OK;
@@ -489,11 +424,6 @@ ldpc::CodeView code_view(const ldpc_ctx *ctx) {
   v.dc_max = ctx->dc_max;
   v.dv_max = ctx->dv_max;
   v.dc_min = ctx->dc_min;
-  v.pcells = ctx->d_pcells;
-  v.pcols = ctx->d_pcols;
-  v.prowmask = ctx->d_prowmask;
-  v.pF = ctx->pF;
-  v.pfull = ctx->pfull;
   return v;
 }
 
@@ -505,14 +435,14 @@ int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int preci
   if (method == 0 && ctx->ms_mode == 2) {
     // min-sum: narrow chunks, gathered state L2-resident per XCD
     ldpc::MsnView v;
-    v.rblk = (const int4 *)ctx->d_msn[0];
-    v.cblk = (const int4 *)ctx->d_msn[1];
-    v.rx = ctx->d_msn[2];
-    v.cx = ctx->d_msn[3];
+    v.rx = ctx->d_msn[0];
+    v.cx = ctx->d_msn[1];
     v.rdesc = ctx->d_msnd[0];
     v.cdesc = ctx->d_msnd[1];
-    v.corig = ctx->d_msn[4];
-    v.cpos = ctx->d_msn[5];
+    v.rs = ctx->msn.rs;
+    v.cs = ctx->msn.cs;
+    v.corig = ctx->d_msn[2];
+    v.cpos = ctx->d_msn[3];
     v.M = g.M;
     v.N = g.N;
     v.E = g.E;
@@ -840,21 +770,10 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
   std::vector<uint16_t> lane_col;
   std::vector<uint8_t> col_lane;
   std::vector<int32_t> cp, ce, cr;
-  std::vector<ldpc::PackedCell> pcells;
-  std::vector<ldpc::PackedColRec> pcols;
-  std::vector<uint64_t> prow;
   int rc = LDPC_EUNSUPPORTED;
   if (!(flags & LDPC_FLAG_GRAPH) && !ctx->H.empty())
     rc = build_tables(ctx, erecs, crecs, cols, rowmask, lane_col, col_lane,
                       !(flags & LDPC_FLAG_PLAIN_LAYOUT));
-  if (rc == LDPC_OK) {
-    // LDPC_PACKED=1: the packed sum-product kernel (F frames per wave) in
-    // throughput mode.  Exact, but slower than one frame per wave so far
-    // (919 vs 1158 Mbit/s, profiles/round3/ab_packed.txt): it saves the
-    // padding's f64 work but spends more on bookkeeping and SGPR spills.
-    const char *v = getenv("LDPC_PACKED");
-    ctx->pF = (v && v[0] == '1') ? build_packed(ctx, pcells, pcols, prow, ctx->pfull) : 0;
-  }
   if (rc == LDPC_EUNSUPPORTED) {
     ctx->err.clear();
     rc = build_graph(ctx, cp, ce, cr);
@@ -901,9 +820,9 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     upload(ctx, &ctx->d_ce, ce, "upload(col_edges)", what, e);
     upload(ctx, &ctx->d_cr, cr, "upload(col_rows)", what, e);
     if (ctx->ms_mode == 2) {
-      const std::vector<int32_t> *t[6] = {&ctx->msn.rblk, &ctx->msn.cblk, &ctx->msn.rx,
-                                          &ctx->msn.cx,   &ctx->msn.corig, &ctx->msn.cpos};
-      for (int i = 0; i < 6; ++i) upload(ctx, &ctx->d_msn[i], *t[i], "upload(storage order)", what, e);
+      const std::vector<int32_t> *t[4] = {&ctx->msn.rx, &ctx->msn.cx, &ctx->msn.corig,
+                                          &ctx->msn.cpos};
+      for (int i = 0; i < 4; ++i) upload(ctx, &ctx->d_msn[i], *t[i], "upload(storage order)", what, e);
       upload(ctx, &ctx->d_msnd[0], ctx->msn.rdesc, "upload(edge descriptors)", what, e);
       upload(ctx, &ctx->d_msnd[1], ctx->msn.cdesc, "upload(edge descriptors)", what, e);
     }
@@ -914,11 +833,6 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     upload(ctx, &ctx->d_rowmask, rowmask, "upload(rowmask)", what, e);
     upload(ctx, &ctx->d_lane_col, lane_col, "upload(lane_col)", what, e);
     upload(ctx, &ctx->d_col_lane, col_lane, "upload(col_lane)", what, e);
-    if (ctx->pF > 0) {
-      upload(ctx, &ctx->d_pcells, pcells, "upload(packed cells)", what, e);
-      upload(ctx, &ctx->d_pcols, pcols, "upload(packed columns)", what, e);
-      upload(ctx, &ctx->d_prowmask, prow, "upload(packed rows)", what, e);
-    }
     std::vector<uint32_t> zeros(LDPC_TICKET_SLOTS, 0);
     upload(ctx, &ctx->d_tickets, zeros, "upload(tickets)", what, e);
   }
@@ -980,9 +894,6 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->d_rowmask) (void)hipFree(ctx->d_rowmask);
   if (ctx->d_lane_col) (void)hipFree(ctx->d_lane_col);
   if (ctx->d_col_lane) (void)hipFree(ctx->d_col_lane);
-  if (ctx->d_pcells) (void)hipFree(ctx->d_pcells);
-  if (ctx->d_pcols) (void)hipFree(ctx->d_pcols);
-  if (ctx->d_prowmask) (void)hipFree(ctx->d_prowmask);
   if (ctx->d_stage) (void)hipFree(ctx->d_stage);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
@@ -1042,9 +953,12 @@ int ldpc_ctx_path(const ldpc_ctx *ctx) {
   return ctx->graph ? 1 : 0;
 }
 
-int ldpc_ctx_packed_frames(const ldpc_ctx *ctx) {
+int ldpc_ctx_pipeline(const ldpc_ctx *ctx, int *frames_per_chunk, int *chunks) {
   if (!ctx) return LDPC_EINVAL;
-  return ctx->pF;
+  const bool narrow = ctx->graph && ctx->ms_mode == 2;
+  if (frames_per_chunk) *frames_per_chunk = narrow ? ldpc::kMsnFrames : 0;
+  if (chunks) *chunks = narrow ? ldpc::msn_default_chunks() : 0;
+  return narrow ? 1 : 0;
 }
 
 int ldpc_ctx_layout(const ldpc_ctx *ctx, int32_t *model_out) {

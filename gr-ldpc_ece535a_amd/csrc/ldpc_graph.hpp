@@ -85,7 +85,7 @@ int launch_graph_decode(const GraphView &g, const GraphWork &w, const DecodeArgs
 // ---- min-sum with the gathered state in one XCD's L2 (ldpc_graph_msn.hip):
 // chunks of kMsnFrames frames, XCD-aware chunk placement, storage order ------
 #ifndef LDPC_MSN_FRAMES
-#define LDPC_MSN_FRAMES 4
+#define LDPC_MSN_FRAMES 2
 #endif
 constexpr int kMsnFrames = LDPC_MSN_FRAMES;
 
@@ -94,11 +94,12 @@ constexpr int kMsnFrames = LDPC_MSN_FRAMES;
 // consecutive integers -- value(lane) = b[run] + lane, run 0 for lanes below
 // thr & 0xff, 1 below (thr >> 8) & 0xff, 2 below (thr >> 16) & 0xff, else 3.
 // A negative value means "no edge" (lanes past the item's degree or past n;
-// such a run's base is kMsnNoEdge).  A wave with a slot of more than 4 runs
-// keeps its values explicitly (MsnView rblk / cblk mark it; each
-// descriptor's xoff indexes the explicit table).  32 bytes; a wave's
-// descriptors are adjacent, so one 4-byte load per lane reads 8 slots'
-// (was 8 x 64 table entries).
+// such a run's base is kMsnNoEdge).  pad[0] = the item block's largest
+// degree, pad[1] = 1 when the wave's values are explicit (a slot of more
+// than 4 runs): then xoff indexes its 64 values.  32 bytes; the descriptors
+// of a wave are adjacent at a fixed stride, so one 4-byte load per lane
+// reads 8 slots' at an address known from the block index (was a block
+// table, then 8 x 64 table entries).
 struct alignas(32) MsnDesc {
   int32_t b[4];
   uint32_t thr;
@@ -111,18 +112,15 @@ constexpr int32_t kMsnNoEdge = -(1 << 30);
 // edges still in ascending original column, each column's in ascending
 // original row.
 struct MsnView {
-  // per block of 256 storage rows / columns: {first descriptor, slots (the
-  // block's largest degree), explicit-wave mask, 0}; descriptor of slot t,
-  // wave w at first + w slots + t
-  const int4 *rblk;
+  // descriptors (MsnDesc): slot t of wave w of 256-item block b at
+  // (4 b + w) S + t, S = rs (rows: dc_max) or cs (columns: dv_max)
   const MsnDesc *rdesc;  // value = storage column of a row's t-th edge
   const int32_t *rx;     // explicit row values (64 per explicit descriptor)
-  const int4 *cblk;
   const MsnDesc *cdesc;  // value = storage row of a column's t-th edge | its place in that row << 24
   const int32_t *cx;
   const int32_t *corig;  // N: original column of a storage column
   const int32_t *cpos;   // N: storage column of an original column
-  int M, N, E, KB, dc_max, dv_max;
+  int M, N, E, KB, dc_max, dv_max, rs, cs;
   int out_var;           // outputs written by the variable pass (MsnTables::out_var)
 };
 
@@ -130,8 +128,9 @@ struct MsnTables {  // host copies of MsnView's arrays
   // full slot-major tables (D x n, -1 past the degree): rcs[t][p] storage
   // column of row p's t-th edge, crs[t][x] storage row | place << 24
   std::vector<int32_t> rp, cp, rcs, crs, corig, cpos;
-  std::vector<int32_t> rblk, cblk, rx, cx;  // per-block offsets, explicit values (MsnView)
+  std::vector<int32_t> rx, cx;  // explicit values (MsnView)
   std::vector<MsnDesc> rdesc, cdesc;
+  int rs = 0, cs = 0;
   std::vector<int32_t> rpos;  // storage row of each original row
   int order = 0;         // 0 identity, 1 DVB-S2 residue classes
   long score[2] = {0, 0};  // contiguity of the identity / residue-class order (-1: not tried)

@@ -152,15 +152,33 @@ __device__ __forceinline__ int wave_of_block() {
   return __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
 }
 
-// A wave's descriptors sit together (slot t of wave w at first + w * slots +
-// t), so one 4-byte load per lane fetches 8 of them: lane l gets dword l & 7
-// of slot 8 g + (l >> 3).  The lane's word of group g.
-__device__ __forceinline__ int desc_group(const MsnDesc *desc, int4 blk, int g) {
+// Uniform loads (chunk masks, iteration counts) through the scalar cache:
+// issued at the top of a kernel, in parallel with its vector loads, and never
+// written by the kernel that reads them (the previous launch's decision wrote
+// them).
+template <typename T>
+__device__ __forceinline__ T ld_uniform(const T *p) {
+  return *(const __attribute__((address_space(4))) T *)p;
+}
+
+// Descriptor words.  The S descriptors of wave w of item block b sit at
+// (4 b + w) S, so one 4-byte load per lane reads 8 of them -- lane l gets
+// dword l & 7 of slot 8 g + (l >> 3) -- at an address known from blockIdx
+// alone.  Groups 0 .. NW - 1.  Runs with every lane of the wave active:
+// slot_value reads the words across the wave, so lanes whose item is past n
+// must have loaded theirs.
+template <int NW>
+__device__ __forceinline__ void desc_words(const MsnDesc *desc, int bi, int S, int (&word)[NW]) {
   const int lane = threadIdx.x & 63;
-  const int deg = __builtin_amdgcn_readfirstlane(blk.y);
-  const int d0 = __builtin_amdgcn_readfirstlane(blk.x) + wave_of_block() * deg;
-  const int t = 8 * g + (lane >> 3);
-  return t < deg ? ((const int32_t *)(desc + d0 + 8 * g))[lane] : 0;
+  const MsnDesc *d = desc + (int64_t)(4 * bi + wave_of_block()) * S;
+#pragma unroll
+  for (int i = 0; i < NW; ++i)
+    word[i] = 8 * i < S && 8 * i + (lane >> 3) < S ? ((const int32_t *)(d + 8 * i))[lane] : 0;
+}
+// the block's largest degree and whether this wave's values are explicit
+__device__ __forceinline__ int desc_degree(int word0) { return __builtin_amdgcn_readlane(word0, 6); }
+__device__ __forceinline__ bool desc_explicit(int word0) {
+  return __builtin_amdgcn_readlane(word0, 7) != 0;
 }
 
 // The lane's value of slot T from its group's word: b[run] + lane (runs and
@@ -195,25 +213,13 @@ __device__ __forceinline__ void slot_values(const int *word, const int32_t *x, i
   }
 }
 
-// The block's descriptor words, groups 0 .. NW - 1 (desc_group).  Must run
-// with every lane of the wave active: slot_value reads the words across the
-// wave, so lanes that exit early (items past n) must have loaded theirs.
-template <int NW>
-__device__ __forceinline__ void desc_words(const MsnDesc *desc, int4 blk, int (&word)[NW]) {
-  const int deg = __builtin_amdgcn_readfirstlane(blk.y);
-#pragma unroll
-  for (int i = 0; i < NW; ++i) word[i] = 8 * i < deg ? desc_group(desc, blk, i) : 0;
-}
-
 // The lane's values of slots T0 .. T0 + D - 1 of its item (negative: no
-// edge) from the block's table blk = {first descriptor, slots, explicit-wave
-// mask} and its descriptor words (desc_words).
+// edge) from its wave's descriptor words (desc_words).
 template <int T0, int D, int NW>
-__device__ __forceinline__ void edge_values(const int (&word)[NW], const int32_t *x, int4 blk,
-                                            int (&v)[D]) {
+__device__ __forceinline__ void edge_values(const int (&word)[NW], const int32_t *x, int (&v)[D]) {
   static_assert((T0 + D - 1) / 8 < NW, "descriptor group not loaded");
-  const int deg = __builtin_amdgcn_readfirstlane(blk.y);
-  if ((__builtin_amdgcn_readfirstlane(blk.z) >> wave_of_block()) & 1)
+  const int deg = desc_degree(word[0]);
+  if (desc_explicit(word[0]))
     slot_values<T0, D, true>(word, x, deg, v);
   else
     slot_values<T0, D, false>(word, x, deg, v);
@@ -227,17 +233,22 @@ __device__ __forceinline__ void edge_values(const int (&word)[NW], const int32_t
 // and are masked).  L(q) of each edge is LQ - L(r_old) (:387-392); a frame's
 // first step takes L(q) = Lci (LQ = Lci, no old message).  The parity of the
 // last decisions (checkFrame, :236-253) comes from the signs of the same LQ.
-// blk = the block's table (edge_values); its degree is <= D: the
+// The row's state (om1, om2, omt) and alpha bytes (ab) were loaded by the
+// caller with the descriptor words; the block's degree is <= D: the
 // straight-line bodies are instantiated at the block degree, the body for
 // degrees above 8 at D = DC with slots past the block degree masked.
-template <int PREC, int D, int NW>
-__device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, int k, int p, int4 blk,
-                                          const int (&word)[NW], const int (&itf)[kF],
+template <int PREC, int D, int NW, int NA>
+__device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, int k, int p,
+                                          const int (&word)[NW],
+                                          const Vec<typename Math<PREC>::Real> &om1,
+                                          const Vec<typename Math<PREC>::Real> &om2, MetaWord omt,
+                                          const uint32_t (&ab)[NA], const int (&itf)[kF],
                                           bool (&par)[kF]) {
+  static_assert(D <= NA, "alpha bytes not loaded");
   typedef typename Math<PREC>::Real Real;
   int cs[D];
   bool ok[D];
-  edge_values<0, D>(word, g.rx, blk, cs);
+  edge_values<0, D>(word, g.rx, cs);
 #pragma unroll
   for (int t = 0; t < D; ++t) {
     ok[t] = cs[t] >= 0;
@@ -246,17 +257,10 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
   Real *m1 = (Real *)w.m1, *m2 = (Real *)w.m2;
   const Real *LQ = (const Real *)w.LQ;
   const int64_t ro = el(k, g.M, p);
-  const Vec<Real> om1 = ldv_nt(m1 + ro), om2 = ldv_nt(m2 + ro);
-  const MetaWord omt = ld_meta(w.meta + ro);
   uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M + p;  // [t][p]
   Vec<Real> lq[D];
-  uint32_t ab[D];
-  const int deg = __builtin_amdgcn_readfirstlane(blk.y);
 #pragma unroll
-  for (int t = 0; t < D; ++t) {
-    lq[t] = ldv(LQ + el(k, g.N, cs[t]));
-    ab[t] = t < deg ? alpha[(int64_t)t * g.M] : 0u;
-  }
+  for (int t = 0; t < D; ++t) lq[t] = ldv(LQ + el(k, g.N, cs[t]));
   // per frame: L(q) in ascending original column, sign product, smallest and
   // second smallest |L(q)| (strict <, first occurrence, DBL_MAX seeds; NaN
   // never passes), the new alpha bits
@@ -315,35 +319,45 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
 template <int PREC, int DC, bool FUSE>
 __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int mbuf, int max_iters,
                                                  int et_period, int B, int32_t *synd) {
+  typedef typename Math<PREC>::Real Real;
   int k, bi;
   map_block(blockIdx.x, w.chunks, w.nb_check, k, bi);
-  const uint32_t live = w.live[mbuf * w.chunks + k];
+  // every load that does not depend on the descriptors goes out with them:
+  // one memory round trip before the gathers (rows past M load row M - 1)
+  const int p = bi * kIB + threadIdx.x;  // row storage position
+  const int pl = min(p, g.M - 1);
+  int word[(DC + 7) / 8];
+  desc_words(g.rdesc, bi, g.rs, word);
+  const uint32_t live = ld_uniform(&w.live[mbuf * w.chunks + k]);
+  int itf[kF];
+#pragma unroll
+  for (int f = 0; f < kF; ++f) itf[f] = ld_uniform(&w.it[k * kF + f]);
+  const int64_t ro = el(k, g.M, pl);
+  const Vec<Real> om1 = ldv_nt((const Real *)w.m1 + ro), om2 = ldv_nt((const Real *)w.m2 + ro);
+  const MetaWord omt = ld_meta(w.meta + ro);
+  uint32_t ab[DC];
+  const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M + pl;  // [t][p]
+#pragma unroll
+  for (int t = 0; t < DC; ++t) ab[t] = t < g.dc_max ? alpha[(int64_t)t * g.M] : 0u;
   if (!live) {
     if (FUSE && bi == 0 && threadIdx.x < 64)
       decide_slots(w, k, 0u, mbuf ^ 1, max_iters, et_period, B, synd);
     return;
   }
-  const int p = bi * kIB + threadIdx.x;  // row storage position
-  int itf[kF];
-#pragma unroll
-  for (int f = 0; f < kF; ++f) itf[f] = w.it[k * kF + f];
   bool par[kF];
 #pragma unroll
   for (int f = 0; f < kF; ++f) par[f] = false;
-  const int4 rb = g.rblk[bi];  // the block's descriptors, largest degree, explicit waves
-  int word[(DC + 7) / 8];
-  desc_words(g.rdesc, rb, word);  // every lane, before rows past M drop out
   if (p < g.M) {
-    switch (rb.y) {
+    switch (desc_degree(word[0])) {
 #define LDPC_MSN_ROW(n) \
   case n:               \
-    if constexpr (n <= DC) check_row<PREC, (n <= DC ? n : 1)>(g, w, k, p, rb, word, itf, par); \
+    if constexpr (n <= DC) check_row<PREC, (n <= DC ? n : 1)>(g, w, k, p, word, om1, om2, omt, ab, itf, par); \
     break;
       LDPC_MSN_ROW(1) LDPC_MSN_ROW(2) LDPC_MSN_ROW(3) LDPC_MSN_ROW(4) LDPC_MSN_ROW(5)
       LDPC_MSN_ROW(6) LDPC_MSN_ROW(7) LDPC_MSN_ROW(8)
 #undef LDPC_MSN_ROW
       default:
-        if constexpr (DC > 8) check_row<PREC, DC>(g, w, k, p, rb, word, itf, par);
+        if constexpr (DC > 8) check_row<PREC, DC>(g, w, k, p, word, om1, om2, omt, ab, itf, par);
         break;
     }
   }
@@ -535,12 +549,12 @@ __global__ void __launch_bounds__(256) msn_cols(MsnView g, MsnWork w, uint8_t *b
 // rather than selecting by meta first: one load level less); edges past the
 // column's own degree read row 0 and are masked.
 template <typename Real, int T0, int D, int NW>
-__device__ __forceinline__ void var_edges(const MsnView &g, const MsnWork &w, int k, int4 blk,
+__device__ __forceinline__ void var_edges(const MsnView &g, const MsnWork &w, int k,
                                           const int (&word)[NW], Vec<Real> &s) {
   const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
   const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M;
   int v[D];
-  edge_values<T0, D>(word, g.cx, blk, v);
+  edge_values<T0, D>(word, g.cx, v);
   bool ok[D];
   int place[D];
   int64_t ro[D];
@@ -577,11 +591,11 @@ __device__ __forceinline__ void var_edges(const MsnView &g, const MsnWork &w, in
 
 // the same for columns of degree > 8: edges 8 .. deg - 1, four at a time
 template <typename Real>
-__device__ void var_edges_rt(const MsnView &g, const MsnWork &w, int k, int4 blk,
-                             const int (&word)[2], Vec<Real> &s) {
-  const int deg = __builtin_amdgcn_readfirstlane(blk.y);
-  if (deg > 8) var_edges<Real, 8, 4>(g, w, k, blk, word, s);
-  if (deg > 12) var_edges<Real, 12, 4>(g, w, k, blk, word, s);
+__device__ void var_edges_rt(const MsnView &g, const MsnWork &w, int k, const int (&word)[2],
+                             Vec<Real> &s) {
+  const int deg = desc_degree(word[0]);
+  if (deg > 8) var_edges<Real, 8, 4>(g, w, k, word, s);
+  if (deg > 12) var_edges<Real, 12, 4>(g, w, k, word, s);
 }
 
 // Vertical step (:379-403), one column per lane, the chunk's F frames in the
@@ -597,10 +611,16 @@ __global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs 
   int k, bi;
   map_block(blockIdx.x, w.chunks, w.nb_var, k, bi);
   const int m = nb * w.chunks + k;  // the decision's mask buffer
-  const uint32_t run = w.run[m], fill = w.fill[m], stop = w.stop[m];
+  const uint32_t run = ld_uniform(&w.run[m]), fill = ld_uniform(&w.fill[m]),
+                 stop = ld_uniform(&w.stop[m]);
   const int x = bi * kIB + threadIdx.x;  // column storage position
   const int64_t ci = el(k, g.N, x);
   Real *LQ = (Real *)w.LQ;
+  // the descriptor words and Lci go out together (columns past N load the
+  // last column's)
+  int word[(DV + 7) / 8];
+  desc_words(g.cdesc, bi, g.cs, word);
+  Vec<float> lci = ldv_nt(w.L + el(k, g.N, min(x, g.N - 1)));
   if (w.out_var && stop) {
     const int lane = threadIdx.x & 63;
     const bool in = x < g.N;
@@ -620,11 +640,7 @@ __global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs 
       if (bi == 0 && threadIdx.x == 0 && a.iters) a.iters[fr] = w.used[k * kF + f];
     }
   }
-  const int4 cb = g.cblk[bi];  // the block's descriptors, largest degree, explicit waves
-  int word[(DV + 7) / 8];
-  if (run) desc_words(g.cdesc, cb, word);  // every lane, before columns past N drop out
   if (!(run | fill) || x >= g.N) return;
-  Vec<float> lci = ldv_nt(w.L + ci);
   if (fill) {
     const int64_t src = (int64_t)g.corig[x] * a.elem_stride;
 #pragma unroll
@@ -637,20 +653,20 @@ __global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs 
 #pragma unroll
   for (int f = 0; f < kF; ++f) s.v[f] = Real(0);
   if (run) {
-    switch (cb.y) {
+    switch (desc_degree(word[0])) {
 #define LDPC_MSN_COL(n)                                                    \
   case n:                                                                  \
-    if constexpr (n <= DV) var_edges<Real, 0, (n < 4 ? n : 4)>(g, w, k, cb, word, s); \
-    if constexpr (n > 4 && n <= DV) var_edges<Real, 4, (n > 4 ? n - 4 : 1)>(g, w, k, cb, word, s); \
+    if constexpr (n <= DV) var_edges<Real, 0, (n < 4 ? n : 4)>(g, w, k, word, s); \
+    if constexpr (n > 4 && n <= DV) var_edges<Real, 4, (n > 4 ? n - 4 : 1)>(g, w, k, word, s); \
     break;
       LDPC_MSN_COL(1) LDPC_MSN_COL(2) LDPC_MSN_COL(3) LDPC_MSN_COL(4) LDPC_MSN_COL(5)
       LDPC_MSN_COL(6) LDPC_MSN_COL(7) LDPC_MSN_COL(8)
 #undef LDPC_MSN_COL
       default:
         if constexpr (DV > 8) {
-          var_edges<Real, 0, 4>(g, w, k, cb, word, s);
-          var_edges<Real, 4, 4>(g, w, k, cb, word, s);
-          var_edges_rt<Real>(g, w, k, cb, word, s);
+          var_edges<Real, 0, 4>(g, w, k, word, s);
+          var_edges<Real, 4, 4>(g, w, k, word, s);
+          var_edges_rt<Real>(g, w, k, word, s);
         }
         break;
     }
@@ -728,7 +744,7 @@ int msn_default_chunks() {
   // 40 chunks = 160 frames in flight, 5 per XCD, 222 MB of chunk state (the
   // 256 MB Infinity Cache holds it): 2 283-2 291 Mbit/s against 2 223-2 235
   // for 32 and 2 189-2 201 for 48 (profiles/round3/msn/chunks_fused.txt)
-  return v >= 1 ? v : 40;
+  return v >= 1 ? v : 80;
 }
 
 size_t msn_work_bytes(const MsnView &g, int chunks, int prec) {
@@ -853,18 +869,21 @@ long contiguity(const MsnTables &t) {
 
 }  // namespace
 
-// A slot-major table full[t][x] (D x n, -1 past each item's degree) cut in
-// blocks of the kernels' 256 items: block b keeps only its largest degree's
-// slots, one descriptor per (slot, wave) (MsnDesc: up to 4 runs of
-// consecutive values), a wave's slots together.  A wave with a slot of more
-// than 4 runs keeps every slot's 64 values in `x` instead (at each
-// descriptor's xoff).  blk[4b ..] = {first descriptor, slots, explicit-wave
-// mask, 0}.
-void msn_block_tables(const std::vector<int32_t> &full, int D, int n, std::vector<int32_t> &blk,
-                      std::vector<MsnDesc> &desc, std::vector<int32_t> &x) {
-  const int nb = (n + kIB - 1) / kIB, nw = kIB / 64;
-  blk.assign((size_t)4 * nb, 0);
-  desc.clear();
+// A slot-major table full[t][x] (D x n, -1 past each item's degree) as
+// descriptors (MsnDesc: up to 4 runs of consecutive values): S = D per wave
+// of the kernels' 256-item blocks, slot t of wave w of block b at
+// (4 b + w) S + t; slots past the block's largest degree hold no edge.  Each
+// descriptor also carries that degree (pad[0]) and whether its wave's values
+// are explicit (pad[1]): a wave with a slot of more than 4 runs keeps every
+// slot's 64 values in `x` (at each descriptor's xoff).
+void msn_block_tables(const std::vector<int32_t> &full, int D, int n, std::vector<MsnDesc> &desc,
+                      std::vector<int32_t> &x) {
+  const int nb = (n + kIB - 1) / kIB, nw = kIB / 64, S = D;
+  MsnDesc none{};
+  for (int r = 0; r < 4; ++r) none.b[r] = kMsnNoEdge;
+  none.thr = 64u | 64u << 8 | 64u << 16;
+  none.xoff = -1;
+  desc.assign((size_t)nb * nw * S, none);
   x.clear();
   for (int b = 0; b < nb; ++b) {
     int deg = 0;
@@ -874,12 +893,8 @@ void msn_block_tables(const std::vector<int32_t> &full, int D, int n, std::vecto
       for (int t = 0; t < D; ++t)
         if (full[(size_t)t * n + c] != -1) deg = std::max(deg, t + 1);
     }
-    const size_t d0 = desc.size();
-    blk[4 * b] = (int32_t)d0;
-    blk[4 * b + 1] = deg;
-    desc.resize(d0 + (size_t)deg * nw);
     for (int w = 0; w < nw; ++w) {
-      std::vector<MsnDesc> mine((size_t)deg);
+      MsnDesc *mine = &desc[((size_t)b * nw + w) * S];
       std::vector<int32_t> vals((size_t)deg * 64);
       bool explicit_wave = false;
       for (int t = 0; t < deg; ++t) {
@@ -894,8 +909,6 @@ void msn_block_tables(const std::vector<int32_t> &full, int D, int n, std::vecto
           if (!cont) start[runs++] = l;
         }
         MsnDesc &d = mine[t];
-        d = MsnDesc{};
-        d.xoff = -1;
         explicit_wave |= runs > 4;
         uint32_t thr = 0;
         for (int r = 0; r < 4; ++r) {
@@ -905,26 +918,31 @@ void msn_block_tables(const std::vector<int32_t> &full, int D, int n, std::vecto
         }
         d.thr = thr;
       }
-      if (explicit_wave && deg > 0) {
-        blk[4 * b + 2] |= 1 << w;
+      if (explicit_wave)
         for (int t = 0; t < deg; ++t) mine[t].xoff = (int32_t)(x.size() + (size_t)t * 64);
-        x.insert(x.end(), vals.begin(), vals.end());
+      if (explicit_wave) x.insert(x.end(), vals.begin(), vals.end());
+      for (int t = 0; t < S; ++t) {
+        mine[t].pad[0] = deg;
+        mine[t].pad[1] = explicit_wave ? 1 : 0;
       }
-      for (int t = 0; t < deg; ++t) desc[d0 + (size_t)w * deg + t] = mine[t];
     }
   }
   // self-check: decode every (block, wave, slot, lane) as the kernels do
-  // (desc_group / slot_value / slot_explicit) and compare with the table
+  // (desc_words / slot_value / slot_explicit) and compare with the table
   for (int b = 0; b < nb; ++b)
     for (int w = 0; w < nw; ++w)
-      for (int t = 0; t < blk[4 * b + 1]; ++t) {
-        const MsnDesc &d = desc[(size_t)blk[4 * b] + (size_t)w * blk[4 * b + 1] + t];
-        const bool expl = (blk[4 * b + 2] >> w) & 1;
+      for (int t = 0; t < S; ++t) {
+        const MsnDesc *mine = &desc[((size_t)b * nw + w) * S];
+        const MsnDesc &d = mine[t];
+        const int deg = mine[0].pad[0];
+        const bool expl = mine[0].pad[1] != 0;
         for (int l = 0; l < 64; ++l) {
           const int c = b * kIB + w * 64 + l;
           const int32_t want = c < n ? full[(size_t)t * n + c] : -1;
           int32_t got;
-          if (expl) {
+          if (t >= deg) {
+            got = -1;
+          } else if (expl) {
             got = x[(size_t)d.xoff + l];
           } else {
             int base = l >= (int)(d.thr & 0xffu) ? d.b[1] : d.b[0];
@@ -976,8 +994,10 @@ void msn_tables(int M, int N, const std::vector<int32_t> &rp0, const std::vector
   t.corig = corig;
   t.cpos = cpos;
   t.rpos = rpos;
-  msn_block_tables(t.rcs, dc, M, t.rblk, t.rdesc, t.rx);
-  msn_block_tables(t.crs, dv, N, t.cblk, t.cdesc, t.cx);
+  msn_block_tables(t.rcs, dc, M, t.rdesc, t.rx);
+  msn_block_tables(t.crs, dv, N, t.cdesc, t.cx);
+  t.rs = dc;
+  t.cs = dv;
   // outputs from the variable pass need the info columns in place, 8 per byte
   t.out_var = M % 8 == 0;
   for (int c = M; c < N && t.out_var; ++c) t.out_var = cpos[c] == c;

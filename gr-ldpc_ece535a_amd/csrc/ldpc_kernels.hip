@@ -1144,308 +1144,6 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
 }
 
 // ---------------------------------------------------------------------------
-// Packed sum-product kernel: F frames per wave (ldpc_kernels.hpp PackedCell).
-//
-// One frame per wave leaves a code's E edges padded to 64 S cells: 168 of
-// the reference's edges in 192, and the column-centric pass computes a third
-// tanh for each of its 24 degree-2 columns -- 12.5 % of the f64 work spent on
-// nothing.  Here frame f of the wave's F owns cells f E .. f E + E - 1 of its
-// 512 (3 x 168 = 504 for the reference's H), and every cell does the same
-// work: its bit message M(j,i) = sum_{k != j} (E(k,i) + r(i)) in ascending k
-// (:540-553; r(i) itself while the frame is fresh, :489-496), tanh(M/2) into
-// tb (:509), the product of its row neighbours' tanh values in ascending
-// column and the check message log((1+T)/(1-T)) into eb (:506-513).  Then
-// each frame's column lanes form the posterior, hard decision and syndrome
-// (:519-537) and the frame either goes on or is written out and replaced by
-// the next frame of the launch's queue.  Frames advance in lockstep but each
-// at its own iteration count; a finished frame's slot refills at once.
-// Same operations, same order, same arithmetic (ldpc_exact.hpp) as the
-// one-frame kernel and the reference.
-//
-// LDS per wave (doubles): tb[512] + identity 1.0 + zero 0.0, eb[512] + zero,
-// rb[F 64] r = -tx per frame column + 1.0 (padding cells' r), nr[F 64] = tx
-// (a missing column entry's term -r + r is exactly +0.0, as in decode_frame's
-// FIN form; frames with a non-finite sample take the select form instead).
-// Cell records are relocated once into 16-bit LDS byte addresses (the
-// block's LDS stays below 64 KiB), two per VGPR.
-// ---------------------------------------------------------------------------
-#ifndef LDPC_PACKED_MINB
-#define LDPC_PACKED_MINB 3  // packed kernel: waves per SIMD the register budget allows
-#endif
-template <int F>
-struct PackedLds {
-  static constexpr int kCells = 64 * kPackedCells;
-  static constexpr int tb = 0, tb_one = kCells, tb_zero = kCells + 1;
-  static constexpr int eb = kCells + 2, eb_zero = eb + kCells;
-  static constexpr int rb = eb_zero + 1, rb_one = rb + 64 * F;
-  static constexpr int nr = rb_one + 1;
-  static constexpr int end = nr + 64 * F;
-  static constexpr size_t per_wave = align16((size_t)end * 8);
-};
-
-__device__ __forceinline__ uint32_t lo16(uint32_t w) { return w & 0xffffu; }
-__device__ __forceinline__ uint32_t hi16(uint32_t w) { return w >> 16; }
-
-template <int F, int PREC, int MINB>
-__global__ void __launch_bounds__(kThreads, MINB) decode_packed_kernel(CodeView code, DecodeArgs a) {
-  typedef double Real;
-  constexpr int C = kPackedCells;
-  typedef PackedLds<F> L;
-  static_assert(kWavesPerBlock * L::per_wave + sizeof(typename Math<PREC>::Tab) < 65536,
-                "16-bit LDS addresses");
-  extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
-  stage_tab<PREC>(logtab);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wg = blockIdx.x * kWavesPerBlock + wave;
-  if (wg >= a.waves) return;
-  const int M = code.M, N = code.N, full = code.pfull;
-  Real *slice = reinterpret_cast<Real *>(smem + (size_t)wave * L::per_wave);
-  Real *tb = slice + L::tb, *eb = slice + L::eb, *rb = slice + L::rb, *nr = slice + L::nr;
-  const uint32_t s0 = lds_addr(slice);
-  auto at = [&](int idx) { return s0 + 8u * (uint32_t)idx; };
-
-  // ---- cell records -> LDS byte addresses, two per VGPR -------------------
-  // w[s][0] = nbr0 | nbr1, [1] = nbr2 | nbr3, [2] = nbr4 | oth0, [3] = oth1 | r
-  uint32_t w[C][4];
-  uint32_t cellmask[F];  // bit s: cell s of this lane belongs to frame f
-  uint32_t valid = 0;    // select form: bit 2 s + k: cell s has a k-th other edge
-#pragma unroll
-  for (int f = 0; f < F; ++f) cellmask[f] = 0;
-#pragma unroll
-  for (int s = 0; s < C; ++s) {
-    const int g = lane + 64 * s;
-    const PackedCell pc = code.pcells[g];
-    uint32_t ad[8];
-    if (pc.rcell == kNone) {  // padding: T = 0 (first factor the zero cell), M = 2
-      ad[0] = at(L::tb_zero);
-#pragma unroll
-      for (int k = 1; k < 5; ++k) ad[k] = at(L::tb_one);
-      ad[5] = ad[6] = at(L::eb_zero);
-      ad[7] = at(L::rb_one);
-    } else {
-      const int f = pc.rcell >> 6;
-#pragma unroll
-      for (int f2 = 0; f2 < F; ++f2) cellmask[f2] |= (f == f2 ? 1u : 0u) << s;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) ad[k] = pc.nbr[k] == kNone ? at(L::tb_one) : at(L::tb + pc.nbr[k]);
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        ad[5 + k] = pc.oth[k] == kNone ? at(L::nr + pc.rcell) : at(L::eb + pc.oth[k]);
-        valid |= (pc.oth[k] == kNone ? 0u : 1u) << (2 * s + k);
-      }
-      ad[7] = at(L::rb + pc.rcell);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) w[s][k] = ad[2 * k] | (ad[2 * k + 1] << 16);
-  }
-  // column lane (column `lane` of every frame): its edges' eb cells, missing
-  // entries (and lanes >= N) -> the frame column's -r cell
-  uint32_t pe[F][2];
-  uint32_t pvalid = 0;  // select form: bit 3 f + k
-  {
-    const PackedColRec cr = code.pcols[lane];
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-      uint32_t ad[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const bool ok = cr.e[f][k] != kNone;
-        ad[k] = ok ? at(L::eb + cr.e[f][k]) : at(L::nr + 64 * f + lane);
-        pvalid |= (ok ? 1u : 0u) << (3 * f + k);
-      }
-      pe[f][0] = ad[0] | (ad[1] << 16);
-      pe[f][1] = ad[2];
-    }
-  }
-  const uint64_t prow = lane < M ? code.prowmask[lane] : 0ull;
-  const uint64_t col_ok = __ballot(lane < N);
-  const uint64_t row_ok = __ballot(lane < M);
-  if (lane == 0) {
-    tb[L::tb_one] = Real(1);
-    tb[L::tb_zero] = Real(0);
-    eb[L::eb_zero - L::eb] = Real(0);
-    rb[L::rb_one - L::rb] = Real(1);
-  }
-
-  // ---- frame slots --------------------------------------------------------
-  const int64_t first = (int64_t)a.waves * F;  // frames handed out before the queue
-  int64_t fb[F];                               // frame in slot f, -1: empty
-  int fh[F];                                   // iterations done
-  uint32_t fresh = 0, nonfin = 0;              // per slot
-  // loads frame b into slot f (b < 0: empty slot, benign values)
-  auto load = [&](int f, int64_t b) {
-    float x = 1.0f;
-    if (b >= 0 && lane < N) {
-      float pol;
-      const float *src = frame_src(a, b, pol);
-      x = src[(int64_t)lane * a.elem_stride] * pol;
-    }
-    if (b >= 0 && lane >= N) x = 0.0f;
-    rb[64 * f + lane] = -(Real)x;  // r = -tx (:486)
-    nr[64 * f + lane] = (Real)x;
-    const bool bad = b >= 0 && !__builtin_isfinite(x);
-    nonfin = (nonfin & ~(1u << f)) | ((__ballot(bad) != 0 ? 1u : 0u) << f);
-    fb[f] = b;
-    fh[f] = 0;
-    fresh |= 1u << f;
-  };
-#pragma unroll
-  for (int f = 0; f < F; ++f) {
-    const int64_t b = (int64_t)wg * F + f;
-    load(f, b < a.B ? b : -1);
-  }
-
-  while (true) {
-    bool any = false;
-#pragma unroll
-    for (int f = 0; f < F; ++f) any |= fb[f] >= 0;
-    if (!any) break;
-    wave_lds_sync();
-    // ---- A: bit messages (:540-553, :489-496) and tanh(M/2) (:509) --------
-    uint32_t freshcells = 0;
-#pragma unroll
-    for (int f = 0; f < F; ++f) freshcells |= (fresh >> f) & 1u ? cellmask[f] : 0u;
-    const bool sel_form = nonfin != 0;
-    // the slots a frame owns whole (full f .. full f + full - 1) are skipped
-    // while that frame slot is empty; shared slots always run
-    auto skip = [&](int s) {
-      const int f = full > 0 ? s / full : F;
-      bool empty = false;
-#pragma unroll
-      for (int f2 = 0; f2 < F; ++f2) empty |= f2 == f && fb[f2] < 0;
-      return s < F * full && empty;
-    };
-#pragma unroll
-    for (int h2 = 0; h2 < C; h2 += 2) {
-      constexpr int G = 2;
-      if (skip(h2) && skip(h2 + 1)) continue;
-      Real m[G];
-#pragma unroll
-      for (int s2 = 0; s2 < G; ++s2) {
-        const int s = h2 + s2;
-        const Real r = lds_ld<Real>(hi16(w[s][3]));
-        const Real e0 = lds_ld<Real>(hi16(w[s][2]));
-        const Real e1 = lds_ld<Real>(lo16(w[s][3]));
-        Real sum;
-        if (!sel_form) {
-          // a missing entry reads -r: (-r + r) is exactly +0.0 and adding it
-          // changes nothing (no term is -0.0); the first term seeds the sum
-          sum = (e0 + r) + (e1 + r);
-        } else {
-          sum = Real(0);
-          sum = (valid >> (2 * s)) & 1u ? sum + (e0 + r) : sum;
-          sum = (valid >> (2 * s + 1)) & 1u ? sum + (e1 + r) : sum;
-        }
-        m[s2] = (freshcells >> s) & 1u ? r : sum;
-      }
-      Real th[G];
-      Math<PREC>::template tanh_half_n<G>(m, th, logtab);
-#pragma unroll
-      for (int s2 = 0; s2 < G; ++s2) tb[lane + 64 * (h2 + s2)] = th[s2];
-    }
-    wave_lds_sync();
-    // ---- B: check messages (:503-516) --------------------------------------
-#pragma unroll
-    for (int h2 = 0; h2 < C; h2 += 2) {
-      if (skip(h2) && skip(h2 + 1)) continue;
-      Real nb[2][5];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int s = h2 + s2;
-        nb[s2][0] = lds_ld<Real>(lo16(w[s][0]));
-        nb[s2][1] = lds_ld<Real>(hi16(w[s][0]));
-        nb[s2][2] = lds_ld<Real>(lo16(w[s][1]));
-        nb[s2][3] = lds_ld<Real>(hi16(w[s][1]));
-        nb[s2][4] = lds_ld<Real>(lo16(w[s][2]));
-      }
-      Real T[2], Es[2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        Real t = nb[s2][0];  // 1.0 * x == x: the reference's T = 1.0 seed
-#pragma unroll
-        for (int k = 1; k < 5; ++k) t = t * nb[s2][k];
-        T[s2] = t;
-      }
-      // scratch of the near-1 packing (128 cells): eb[384..511] for slot
-      // pairs 0..2 (last iteration's messages there were consumed by A and C;
-      // pair 3 rewrites them), tb[0..127] for pair 3 (every gather of the
-      // iteration has completed; A rewrites tb)
-      log_ratio_n_packed<2>(T, logtab, Es, h2 < C - 2 ? eb + 64 * (C - 2) : tb, lane);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) eb[lane + 64 * (h2 + s2)] = Es[s2];
-    }
-    wave_lds_sync();
-    // ---- C: posterior, hard decision, syndrome, exit (:519-537) ------------
-#pragma unroll
-    for (int f = 0; f < F; ++f) {
-      if (fb[f] < 0) continue;
-      const Real r = rb[64 * f + lane];
-      const Real e0 = lds_ld<Real>(lo16(pe[f][0]));
-      const Real e1 = lds_ld<Real>(hi16(pe[f][0]));
-      const Real e2 = lds_ld<Real>(pe[f][1]);
-      Real Lc;
-      if (!((nonfin >> f) & 1u)) {
-        Lc = ((e0 + r) + (e1 + r)) + (e2 + r);
-      } else {
-        Lc = Real(0);
-        Lc = (pvalid >> (3 * f)) & 1u ? Lc + (e0 + r) : Lc;
-        Lc = (pvalid >> (3 * f + 1)) & 1u ? Lc + (e1 + r) : Lc;
-        Lc = (pvalid >> (3 * f + 2)) & 1u ? Lc + (e2 + r) : Lc;
-      }
-      const uint64_t hard = __builtin_amdgcn_ballot_w64(Lc <= Real(0)) & col_ok;
-      const int odd = __popcll(prow & hard) & 1;
-      const int weight = __popcll(__builtin_amdgcn_ballot_w64(odd != 0) & row_ok);
-      const int used = fh[f] + 1;
-      const bool stop = used == a.max_iters || (used % a.et_period == 0 && weight == 0);
-      if (!stop) {
-        fh[f] = used;
-        fresh &= ~(1u << f);
-        continue;
-      }
-      // ---- frame done: outputs, then the next frame of the queue ----------
-      const int64_t b = fb[f];
-      if (lane == 0) {
-        if (a.iters) a.iters[b] = used;
-        if (a.synd) a.synd[b] = weight;
-      }
-      if (lane < N) {
-        if (a.bits) a.bits[b * N + lane] = (uint8_t)((hard >> lane) & 1);
-        if (a.llr) a.llr[b * N + lane] = (float)Lc;
-      }
-      if (lane < code.KB) {  // info bits M.., MSB first (:207-219)
-        uint32_t o = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int c = M + 8 * lane + j;
-          if (c < N) o |= (uint32_t)((hard >> c) & 1) << (7 - j);
-        }
-        a.packed[b * code.KB + lane] = (uint8_t)o;
-      }
-      uint32_t t = 0;
-      if (lane == 0) t = atomicAdd(a.ticket, 1u) - a.ticket_base;
-      const int64_t nb2 = first + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
-      wave_lds_sync();  // this frame's rb / nr reads above are done
-      load(f, nb2 < a.B ? nb2 : -1);
-    }
-  }
-}
-
-template <int F, int PREC>
-static int launch_packed(const CodeView &code, const DecodeArgs &a, hipStream_t st) {
-  const size_t lds = (size_t)kWavesPerBlock * PackedLds<F>::per_wave;
-  constexpr int kMinb = LDPC_PACKED_MINB;
-  if (lds > 65536 &&
-      hipFuncSetAttribute((const void *)decode_packed_kernel<F, PREC, kMinb>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return -3;
-  const dim3 grid((unsigned)((a.waves + kWavesPerBlock - 1) / kWavesPerBlock));
-  hipLaunchKernelGGL((decode_packed_kernel<F, PREC, kMinb>), grid, dim3(kThreads), lds, st, code,
-                     a);
-  return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
-// ---------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------
 template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax,
@@ -1581,21 +1279,6 @@ int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int 
   constexpr int kMwAutoMax = 512;
   const bool mw = schedule == 2 || (schedule == 0 && method == 1 && (prec == 0 || prec == 2) &&
                                     a.B <= kMwAutoMax);
-  // sum-product f64 in throughput mode on a code the packed kernel takes:
-  // F frames per wave (waves_per_cu waves per CU, each with F frames)
-#ifndef LDPC_NO_PACKED  // A/B only
-  if (method == 1 && prec == 0 && code.pF >= 2 && a.fair_cycles == 0 && !mw) {
-    const int F = code.pF;
-    const int64_t w = std::min<int64_t>(((int64_t)a.B + F - 1) / F, (int64_t)waves_per_cu * cus);
-    a.waves = (int)((w + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock);
-    switch (F) {
-      case 2: return launch_packed<2, 0>(code, a, st);
-      case 3: return launch_packed<3, 0>(code, a, st);
-      case 4: return launch_packed<4, 0>(code, a, st);
-      default: return -2;
-    }
-  }
-#endif
   if (mw) {
     const int64_t frames_in_flight = std::max<int64_t>(1, (int64_t)waves_per_cu * cus / slots);
     a.waves = (int)std::min<int64_t>((int64_t)a.B, frames_in_flight);

@@ -47,28 +47,6 @@ struct alignas(16) ColRec {
   uint16_t r[kDvMax];
 };  // 16 bytes
 
-// Packed sum-product kernel (decode_packed_kernel): F frames share one wave's
-// 512 cells (lane g % 64, slot g / 64 of cell g) -- e.g. 3 x 168 edges of the
-// reference's H in 512 cells, where one frame per wave pads 168 edges to 192.
-// Frame f's first 64 full edges (CSR order) fill whole slots full f ..
-// full f + full - 1 (full = E / 64), so a wave can skip the slots of a frame
-// slot that is empty; its remaining E - 64 full edges share the slots after
-// F full with the other frames' (padding cells after them).  Per cell: its
-// row neighbours' cells (ascending column, kNone: none), its column's other
-// edges' cells (ascending row, kNone: none) and its frame-column f 64 + i
-// (kNone: padding cell).  Per lane l < N (column l, identity positions) and
-// frame f: the cells of the column's edges (ascending row).
-constexpr int kPackedCells = 8;  // cells per lane: 512 per wave
-constexpr int kPackedFramesMax = 4;
-struct alignas(16) PackedCell {
-  uint16_t nbr[5];  // dc <= 6
-  uint16_t oth[2];  // dv <= 3
-  uint16_t rcell;   // f * 64 + column, kNone for padding
-};  // 16 bytes
-struct alignas(8) PackedColRec {
-  uint16_t e[kPackedFramesMax][3];  // cells of column l's edges in frame f, ascending row
-};  // 24 bytes
-
 // Edge records live at their edge's cell (lane slot 64 s + lane) and column
 // records at their column's lane position (lane + 64 q), both chosen per H by
 // plan_layout (ldpc_layout.hpp) so the kernel's LDS gathers are free of bank
@@ -85,12 +63,6 @@ struct CodeView {
   int M, N, E, KB, rs;       // rs = ceil(M / 64)
   int dc_max, dv_max;        // largest check / variable degree
   int dc_min;                // smallest check degree
-  // packed kernel tables (pF == 0: the code does not fit it)
-  const PackedCell *pcells;      // 64 kPackedCells, by cell
-  const PackedColRec *pcols;     // 64, by lane (column)
-  const uint64_t *prowmask;      // M: bit i <=> H(j, i) (identity positions)
-  int pF;                        // frames per wave
-  int pfull;                     // whole slots per frame (slots 0 .. pF pfull - 1)
 };
 
 struct DecodeArgs {

@@ -42,7 +42,7 @@ SIGNATURES = {
     "ldpc_create_csr": (_vp, [_i, _i, _i32p, _i32p, _i, _i]),
     "ldpc_ctx_csr": (_i, [_vp, _i32p, _i32p]),
     "ldpc_ctx_path": (_i, [_vp]),
-    "ldpc_ctx_packed_frames": (_i, [_vp]),
+    "ldpc_ctx_pipeline": (_i, [_vp, _i32p, _i32p]),
     "ldpc_ctx_layout": (_i, [_vp, _i32p]),
     "ldpc_plan_layout": (_i, [_u8p, _i, _i, _i, _i32p, _i32p, _i32p]),
     "ldpc_plan_storage_order": (_i, [_i, _i, _i32p, _i32p, _i32p, _i32p, _i64p]),
@@ -217,10 +217,12 @@ class Decoder:
                self._ctx)
         self._H = None
 
-    def packed_frames_per_wave(self):
-        """ldpc_ctx_packed_frames: frames per wave of the packed sum-product
-        kernel (throughput mode, f64), 0 if the code does not fit it."""
-        return _check(lib().ldpc_ctx_packed_frames(self._ctx), self._ctx)
+    def pipeline(self):
+        """ldpc_ctx_pipeline: {frames_per_chunk, chunks} of the large-code
+        min-sum pipeline (both 0 when this context does not use it)."""
+        f, c = ctypes.c_int32(0), ctypes.c_int32(0)
+        _check(lib().ldpc_ctx_pipeline(self._ctx, ctypes.byref(f), ctypes.byref(c)), self._ctx)
+        return {"frames_per_chunk": f.value, "chunks": c.value}
 
     @property
     def layout_model(self):

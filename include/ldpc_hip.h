@@ -173,10 +173,11 @@ int ldpc_ctx_csr(const ldpc_ctx *ctx, int32_t *row_ptr_out, int32_t *col_idx_out
 /* 0: small-code kernel (frame per wave / workgroup, registers + LDS);
  * 1: large-code kernels (messages in HBM). */
 int ldpc_ctx_path(const ldpc_ctx *ctx);
-/* Frames per wave of the packed sum-product kernel that throughput mode uses
- * for LDPC_PREC_F64 on this code (0: the code does not fit it; one frame per
- * wave then). */
-int ldpc_ctx_packed_frames(const ldpc_ctx *ctx);
+/* The large-code min-sum pipeline's configuration: 1 and the
+ * frames per chunk and the chunks in flight (LDPC_MSN_CHUNKS, else the
+ * default) when min-sum decodes on this context use the narrow-chunk
+ * pipeline; 0 (both 0) otherwise.  Either pointer may be NULL. */
+int ldpc_ctx_pipeline(const ldpc_ctx *ctx, int *frames_per_chunk, int *chunks);
 /* The context's layout model (5 ints, as ldpc_plan_layout's model_out);
  * LDPC_EUNSUPPORTED for a large-code context. */
 int ldpc_ctx_layout(const ldpc_ctx *ctx, int32_t *model_out);

@@ -31,6 +31,12 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--decodes", type=int, default=0,
                     help="divide totals by this many decodes (default: dispatches of *_init)")
+    ap.add_argument("--update-json", default="",
+                    help="write the msn_* kernels' memory traffic per decode into this PMC json "
+                         "(key --key) with --pipeline F,C and --source")
+    ap.add_argument("--key", default="dvb0_f64_b1024_i50_db2")
+    ap.add_argument("--pipeline", default="")
+    ap.add_argument("--source", default="")
     a = ap.parse_args()
     kt = rows(os.path.join(a.dir, "kt", "**", "*kernel_trace.csv"))
     dur = collections.defaultdict(list)
@@ -66,6 +72,23 @@ def main():
             h, m = c["TCC_HIT_sum"], c["TCC_MISS_sum"]
             parts.append("L2 hit %.3f" % (h / max(1.0, h + m)))
         print("  %-60s %s" % (k, ", ".join(parts)))
+    if a.update_json:
+        import json
+        fetch = write = kns = 0.0
+        for k, c in cnt.items():
+            if k.startswith("msn_"):
+                fetch += 2 * c.get("FETCH_SIZE", 0.0) * 1024 / nd
+                write += c.get("WRITE_SIZE", 0.0) * 1024 / nd
+                kns += sum(dur.get(k, [0])) / nd
+        f, ch = (int(x) for x in a.pipeline.split(","))
+        db = json.load(open(a.update_json))
+        db[a.key] = {"hbm_bytes_per_launch": fetch + write,
+                     "per_decode": {"decodes": nd, "fetch_bytes": fetch, "write_bytes": write,
+                                    "kernel_ns_per_decode": kns},
+                     "pipeline": {"frames_per_chunk": f, "chunks": ch},
+                     "source": a.source}
+        json.dump(db, open(a.update_json, "w"), indent=1)
+        print("updated %s[%s]: %.1f GB per decode" % (a.update_json, a.key, (fetch + write) / 1e9))
 
 
 if __name__ == "__main__":
