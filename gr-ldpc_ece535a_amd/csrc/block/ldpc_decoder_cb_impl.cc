@@ -183,6 +183,11 @@ void ldpc_decoder_cb_impl::adopt(ldpc_ctx *ctx) {
         "ldpc_decoder_cb: the block emits M/8 bytes of information bits per frame "
         "(lib/ldpc_decoder_cb_impl.cc:141, :209-219); this H has N - M < 8 (M/8)");
   }
+  // A/B knobs for the window launches: LDPC_BLOCK_TP=1 the throughput build
+  // (four waves per SIMD), LDPC_BLOCK_WPC waves per CU
+  if (getenv("LDPC_BLOCK_TP") && getenv("LDPC_BLOCK_TP")[0] == '1')
+    (void)ldpc_set_launch_mode(ctx, LDPC_MODE_THROUGHPUT);
+  if (getenv("LDPC_BLOCK_WPC")) (void)ldpc_set_waves_per_cu(ctx, atoi(getenv("LDPC_BLOCK_WPC")));
   d_ctx = ctx;
   d_M = (unsigned)M;
   d_N = (unsigned)N;
@@ -467,6 +472,15 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   d_rpacked.clear();
 
   Replay r{d_state, d_errors, 0, 0};
+  // the span goes to the device while the first dry run plans (every launch
+  // of this call then reuses it)
+  bool staged = false;
+  if (!d_backend && nin >= N && noutput_items >= d_out_bytes) {
+    if (ldpc_stage_span(d_ctx, in, 2 * (int64_t)nin, 2, max_windows(d_N)) < 0)
+      throw std::runtime_error(std::string("ldpc_decoder_cb: staging failed: ") +
+                               ldpc_last_error(d_ctx));
+    staged = true;
+  }
   const int search_first = std::min(std::max(d_search_first, 1), max_windows(d_N));
   int out_budget = search_first;  // out-of-sync positions one launch may guess past
   bool first = true, last_out = false;
@@ -515,7 +529,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       d_prof[2] += t1 - t0;
       t0 = t1;
     }
-    decode_wanted(in, nin, first);
+    decode_wanted(in, nin, first && !staged);
     if (d_profile) {
       const double t1 = now_s();
       d_prof[3] += t1 - t0;
@@ -526,6 +540,14 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   if (d_profile) {
     d_prof[1] += now_s() - t0;
     d_prof[0] += now_s() - t_call;
+    if (getenv("LDPC_BLOCK_PROFILE")[0] == '2') {  // a line per call
+      static double last[4] = {0, 0, 0, 0};
+      fprintf(stderr,
+              "general_work call: %.1f us = replay %.1f + dry runs %.1f + decode launches %.1f\n",
+              1e6 * (d_prof[0] - last[0]), 1e6 * (d_prof[1] - last[1]),
+              1e6 * (d_prof[2] - last[2]), 1e6 * (d_prof[3] - last[3]));
+      for (int i = 0; i < 4; ++i) last[i] = d_prof[i];
+    }
   }
   d_state = r.state;
   d_errors = r.errors;

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <exception>
 #include <string>
 #include <vector>
@@ -27,6 +28,12 @@ using ldpc::EdgeRowRec;
 using ldpc::kNone;
 
 struct ldpc_ctx {
+  // LDPC_WIN_PROFILE=1: host time split of ldpc_decode_windows, printed by
+  // ldpc_destroy (span staging, window list + launch, wait, result copy)
+  bool win_profile = getenv("LDPC_WIN_PROFILE") != nullptr;
+  bool win_trace = getenv("LDPC_WIN_PROFILE") && getenv("LDPC_WIN_PROFILE")[0] == '2';  // a line per call
+  double win_prof[5] = {0, 0, 0, 0, 0};
+  long long win_calls = 0, win_windows = 0;
   int M = 0, N = 0, E = 0, K = 0, KB = 0, dc_max = 0, dv_max = 0, dc_min = 0;
   int slots = 0, nw = 0, rs = 0;
   int device = 0;
@@ -44,6 +51,7 @@ struct ldpc_ctx {
   size_t stage_bytes = 0;
   float *h_stage = nullptr;  // pinned host staging of host-buffer decodes
   size_t h_stage_bytes = 0;
+  bool h_stage_busy = false;  // a copy out of h_stage may still be running (ldpc_stage_span)
   int32_t *h_ctrl = nullptr;  // pinned progress words of the min-sum pipeline
   // ldpc_decode_windows: the staged sample span (device), window list and
   // frames; span_samples > 0 while the staged span may be reused
@@ -92,6 +100,9 @@ struct ldpc_ctx {
 };
 
 #define LDPC_TICKET_SLOTS 64
+// one counter per 256 bytes: the streams' queues never share a cache line
+// (atomics on one line serialise in its L2 channel)
+#define LDPC_TICKET_STRIDE 64
 
 namespace {
 
@@ -300,6 +311,10 @@ int ensure_stage(ldpc_ctx *ctx, size_t bytes) {
 }
 
 int ensure_host_stage(ldpc_ctx *ctx, size_t bytes) {
+  if (ctx->h_stage_busy) {  // every writer of h_stage comes through here
+    (void)hipStreamSynchronize(ctx->stream);
+    ctx->h_stage_busy = false;
+  }
   if (bytes <= ctx->h_stage_bytes) return LDPC_OK;
   if (ctx->h_stage) {
     (void)hipStreamSynchronize(ctx->stream);
@@ -833,7 +848,7 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     upload(ctx, &ctx->d_rowmask, rowmask, "upload(rowmask)", what, e);
     upload(ctx, &ctx->d_lane_col, lane_col, "upload(lane_col)", what, e);
     upload(ctx, &ctx->d_col_lane, col_lane, "upload(col_lane)", what, e);
-    std::vector<uint32_t> zeros(LDPC_TICKET_SLOTS, 0);
+    std::vector<uint32_t> zeros((size_t)LDPC_TICKET_SLOTS * LDPC_TICKET_STRIDE, 0);
     upload(ctx, &ctx->d_tickets, zeros, "upload(tickets)", what, e);
   }
   if (what) {
@@ -887,6 +902,12 @@ ldpc_ctx *ldpc_create_csr(int M, int N, const int32_t *row_ptr, const int32_t *c
 
 void ldpc_destroy(ldpc_ctx *ctx) {
   if (!ctx) return;
+  if (ctx->win_profile && ctx->win_calls)
+    fprintf(stderr,
+            "ldpc_decode_windows profile: %lld calls, %lld windows; staging %.3f ms, window list + "
+            "launch %.3f ms, wait %.3f ms, results %.3f ms\n",
+            ctx->win_calls, ctx->win_windows, 1e3 * ctx->win_prof[0], 1e3 * ctx->win_prof[1],
+            1e3 * ctx->win_prof[2], 1e3 * ctx->win_prof[3]);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->d_erow) (void)hipFree(ctx->d_erow);
   if (ctx->d_ecol) (void)hipFree(ctx->d_ecol);
@@ -1084,7 +1105,7 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   if (rc != LDPC_OK) return rc;
   if (B == 0) return LDPC_OK;
   if (!d_in || !d_out_packed) return set_err(ctx, LDPC_EINVAL, "null device buffer");
-  ldpc::DecodeArgs a;
+  ldpc::DecodeArgs a{};
   a.in = d_in;
   a.cw_stride = cw_stride;
   a.elem_stride = elem_stride;
@@ -1142,7 +1163,9 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
       // The memset runs on the null stream, which non-blocking streams are
       // not ordered after: wait for it before any stream launches again.
       if ((e = hipDeviceSynchronize()) != hipSuccess ||
-          (e = hipMemset(ctx->d_tickets, 0, LDPC_TICKET_SLOTS * sizeof(uint32_t))) != hipSuccess ||
+          (e = hipMemset(ctx->d_tickets, 0,
+                         (size_t)LDPC_TICKET_SLOTS * LDPC_TICKET_STRIDE * sizeof(uint32_t))) !=
+              hipSuccess ||
           (e = hipDeviceSynchronize()) != hipSuccess)
         return hip_err(ctx, e, "ticket reset");
       ctx->queues.clear();
@@ -1151,15 +1174,20 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
     // slots are handed out in order from zeroed memory (creation, reset)
     ctx->queues.push_back({st, 0u});
   }
-  a.ticket = ctx->d_tickets + q;
+  a.ticket = ctx->d_tickets + q * LDPC_TICKET_STRIDE;
   a.ticket_base = ctx->queues[q].base;
   a.waves = 0;
+  // short frames (iteration cap <= 10): fixed frame stride, no queue atomics
+  // (ldpc_kernels.hpp DecodeArgs::static_stride; LDPC_STATIC_ITERS overrides)
+  static const int static_iters =
+      getenv("LDPC_STATIC_ITERS") ? atoi(getenv("LDPC_STATIC_ITERS")) : 10;
+  a.static_stride = max_iters <= static_iters ? 1 : 0;
   a.fair_cycles = ctx->fair_cycles;
   rc = ldpc::launch_decode(code_view(ctx), a, method, precision, ctx->slots, ctx->nw,
                            ctx->waves_per_cu, ctx->schedule, st);
   if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no kernel for this code shape");
   if (rc != 0) return hip_err(ctx, hipGetLastError(), "kernel launch");
-  ctx->queues[q].base += (uint32_t)B;  // the launch adds exactly B to its counter
+  if (!a.static_stride) ctx->queues[q].base += (uint32_t)B;  // the launch adds exactly B to its counter
   return LDPC_OK;
 }
 
@@ -1236,6 +1264,43 @@ int decode_host_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, in
 
 // ldpc_decode_windows: span in ctx->d_wstage [0, span), then the window list,
 // the gathered frames and the outputs.
+// The window-launch staging area: the span at its start, window lists and
+// outputs at its end.  A bigger area moves everything: the staged span is gone.
+int ensure_window_stage(ldpc_ctx *ctx, size_t need) {
+  if (need <= ctx->wstage_bytes) return LDPC_OK;
+  if (ctx->d_wstage) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->d_wstage);
+    ctx->d_wstage = nullptr;
+    ctx->wstage_bytes = 0;
+  }
+  ctx->span_samples = 0;
+  const size_t want = std::max(need + need / 2, (size_t)4 << 20);
+  hipError_t e = hipMalloc(&ctx->d_wstage, want);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(window staging)");
+  ctx->wstage_bytes = want;
+  return LDPC_OK;
+}
+
+// S samples in[i * elem_stride] -> pinned host stage -> d_span (enqueued on
+// the context's stream; the launches that read it follow on the same stream).
+int copy_span(ldpc_ctx *ctx, const float *in, int64_t S, int elem_stride, float *d_span) {
+  int rc = ensure_host_stage(ctx, (size_t)S * 4);
+  if (rc != LDPC_OK) return rc;
+  float *h = ctx->h_stage;
+  if (elem_stride == 1)
+    memcpy(h, in, (size_t)S * 4);
+  else if (elem_stride == 2)  // gr_complex real parts (the block): a constant stride vectorises
+    for (int64_t i = 0; i < S; ++i) h[i] = in[2 * i];
+  else
+    for (int64_t i = 0; i < S; ++i) h[i] = in[i * elem_stride];
+  hipError_t e = hipMemcpyAsync(d_span, h, (size_t)S * 4, hipMemcpyHostToDevice, ctx->stream);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipMemcpyAsync(span)");
+  ctx->h_stage_busy = true;
+  ctx->span_samples = S;
+  return LDPC_OK;
+}
+
 int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
                         const float *in, int64_t n_in_floats, int elem_stride, int reuse_span,
                         const int64_t *win, int B, uint8_t *out_packed, int32_t *syn_weight_opt) {
@@ -1256,21 +1321,8 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
                b_sy = al((size_t)B * 4);
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  const size_t need = b_span + b_win + b_fr + b_pk + b_sy;
-  if (need > ctx->wstage_bytes) {
-    // a bigger span moves everything: the staged span is gone
-    if (ctx->d_wstage) {
-      (void)hipStreamSynchronize(ctx->stream);
-      (void)hipFree(ctx->d_wstage);
-      ctx->d_wstage = nullptr;
-      ctx->wstage_bytes = 0;
-    }
-    ctx->span_samples = 0;
-    const size_t want = std::max(need + need / 2, (size_t)4 << 20);
-    if ((e = hipMalloc(&ctx->d_wstage, want)) != hipSuccess)
-      return hip_err(ctx, e, "hipMalloc(window staging)");
-    ctx->wstage_bytes = want;
-  }
+  rc = ensure_window_stage(ctx, b_span + b_win + b_fr + b_pk + b_sy);
+  if (rc != LDPC_OK) return rc;
   // pinned: the window list in, then the packed words and syndrome weights
   // out in one copy (d_pk .. d_sy are adjacent in the staging area), so no
   // transfer goes through a pageable bounce
@@ -1298,20 +1350,18 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   float *d_fr = (float *)(base + span_cap + b_win);
   uint8_t *d_pk = (uint8_t *)(base + span_cap + b_win + b_fr);
   int32_t *d_sy = (int32_t *)(base + span_cap + b_win + b_fr + b_pk);
+  const auto tnow = []() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  double t0 = ctx->win_profile ? tnow() : 0.0;
   if (!(reuse_span && ctx->span_samples == S)) {
-    rc = ensure_host_stage(ctx, (size_t)S * 4);
+    rc = copy_span(ctx, in, S, elem_stride, d_span);
     if (rc != LDPC_OK) return rc;
-    float *h = ctx->h_stage;
-    if (elem_stride == 1)
-      memcpy(h, in, (size_t)S * 4);
-    else if (elem_stride == 2)  // gr_complex real parts (the block): a constant stride vectorises
-      for (int64_t i = 0; i < S; ++i) h[i] = in[2 * i];
-    else
-      for (int64_t i = 0; i < S; ++i) h[i] = in[i * elem_stride];
-    if ((e = hipMemcpyAsync(d_span, h, (size_t)S * 4, hipMemcpyHostToDevice, ctx->stream)) !=
-        hipSuccess)
-      return hip_err(ctx, e, "hipMemcpyAsync(span)");
-    ctx->span_samples = S;
+  }
+  if (ctx->win_profile) {
+    const double t1 = tnow();
+    ctx->win_prof[0] += t1 - t0;
+    t0 = t1;
   }
   // the previous call's copy out of h_win has completed (it synchronised)
   memcpy(ctx->h_win, win, (size_t)B * 8);
@@ -1349,6 +1399,11 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   if (!direct && (e = hipMemcpyAsync(h_out, d_pk, out_bytes, hipMemcpyDeviceToHost,
                                      ctx->stream)) != hipSuccess)
     return hip_err(ctx, e, "hipMemcpyAsync(out)");
+  if (ctx->win_profile) {
+    const double t1 = tnow();
+    ctx->win_prof[1] += t1 - t0;
+    t0 = t1;
+  }
   // wait for the launch; polling instead of hipStreamSynchronize
   // (LDPC_WIN_SPIN=1) measured no faster (profiles/round2/block/window_latency.txt)
   static const bool no_spin = !(getenv("LDPC_WIN_SPIN") && getenv("LDPC_WIN_SPIN")[0] == '1');
@@ -1360,14 +1415,49 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
     }
     if (e != hipSuccess) return hip_err(ctx, e, "hipStreamQuery");
   }
+  if (ctx->win_profile) {
+    const double t1 = tnow();
+    ctx->win_prof[2] += t1 - t0;
+    t0 = t1;
+  }
   memcpy(out_packed, h_out, (size_t)B * ctx->KB);
   if (syn_weight_opt) memcpy(syn_weight_opt, h_out + b_pk, (size_t)B * 4);
+  if (ctx->win_profile) {
+    ctx->win_prof[3] += tnow() - t0;
+    ctx->win_calls += 1;
+    ctx->win_windows += B;
+    if (ctx->win_trace) {
+      static double last[4] = {0, 0, 0, 0};
+      fprintf(stderr, "decode_windows B=%d stage %.1f list+launch %.1f wait %.1f results %.1f us\n",
+              B, 1e6 * (ctx->win_prof[0] - last[0]), 1e6 * (ctx->win_prof[1] - last[1]),
+              1e6 * (ctx->win_prof[2] - last[2]), 1e6 * (ctx->win_prof[3] - last[3]));
+      for (int i = 0; i < 4; ++i) last[i] = ctx->win_prof[i];
+    }
+  }
   return LDPC_OK;
 }
 
 }  // namespace
 
 extern "C" {
+
+int ldpc_stage_span(ldpc_ctx *ctx, const float *in, int64_t n_in_floats, int elem_stride,
+                    int max_windows) {
+  if (!ctx) return LDPC_EINVAL;
+  if (!in || elem_stride < 1 || n_in_floats < 0 || max_windows < 0)
+    return set_err(ctx, LDPC_EINVAL, "bad span");
+  const int64_t S = (n_in_floats + elem_stride - 1) / elem_stride;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t B = (size_t)max_windows;
+  // room for that many windows' lists and outputs behind the span
+  const size_t extra = al(B * 8) + (ctx->graph ? al(B * (size_t)ctx->N * 4) : 0) +
+                       al(B * (size_t)ctx->KB) + al(B * 4);
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  int rc = ensure_window_stage(ctx, al((size_t)S * 4) + extra);
+  if (rc != LDPC_OK) return rc;
+  return copy_span(ctx, in, S, elem_stride, (float *)ctx->d_wstage);
+}
 
 int ldpc_decode_windows(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
                         const float *in, int64_t n_in_floats, int elem_stride, int reuse_span,

@@ -922,9 +922,13 @@ __global__ void __launch_bounds__(kThreads, MINB)
       g_timeline[4 * b + 3] = __builtin_amdgcn_s_memtime() - c_start;  // core clocks
     }
 #endif
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(a.ticket, 1u) - a.ticket_base;
-    b = (int64_t)a.waves + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
+    if (a.static_stride) {
+      b += a.waves;
+    } else {
+      uint32_t t = 0;
+      if (lane == 0) t = atomicAdd(a.ticket, 1u) - a.ticket_base;
+      b = (int64_t)a.waves + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
+    }
   }
 }
 
@@ -1137,9 +1141,14 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
       }
     }
     wave_lds_sync();  // this wave's rb reads done before the next frame's writes
-    if (tid == 0) *fslot = (int)(atomicAdd(a.ticket, 1u) - a.ticket_base);
-    __syncthreads();
-    b = (int64_t)a.waves + (int64_t)*fslot;
+    if (a.static_stride) {
+      __syncthreads();
+      b += a.waves;
+    } else {
+      if (tid == 0) *fslot = (int)(atomicAdd(a.ticket, 1u) - a.ticket_base);
+      __syncthreads();
+      b = (int64_t)a.waves + (int64_t)*fslot;
+    }
   }
 }
 
@@ -1257,9 +1266,15 @@ int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (args.B <= 0) return 0;
   DecodeArgs a = args;
+  // CUs of the current device, looked up once per device
+  static int cus_of[64] = {0};
   int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+    if (!cus_of[dev] &&
+        hipDeviceGetAttribute(&cus_of[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus_of[dev] = 256;
+    cus = cus_of[dev];
+  }
 #ifndef LDPC_SMALL_WPC
 #define LDPC_SMALL_WPC 12
 #endif

@@ -97,6 +97,13 @@ struct DecodeArgs {
   uint32_t *ticket;
   uint32_t ticket_base;
   int waves;
+  // 1: no queue -- wave (workgroup) w takes frames w, w + waves, w + 2 waves,
+  // ... and the counter is untouched.  For launches of short frames (small
+  // iteration caps: the block's windows at the reference's 5 iterations) the
+  // one counter's atomics were the bottleneck -- one word serves ~88 adds per
+  // us (MI355X_MICROARCH.md), 8 192 frames ~93 us -- while frames of similar
+  // length need no balancing.
+  int static_stride;
   // issue-priority threshold in core clocks for waves whose last iteration
   // was slow (0: off); see decode_frame
   uint32_t fair_cycles;

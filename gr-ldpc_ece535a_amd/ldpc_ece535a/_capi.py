@@ -64,6 +64,7 @@ SIGNATURES = {
                                      ctypes.c_float, _i, _u8p, _i32p]),
     "ldpc_decode_windows": (_i, [_vp, _i, _i, _i, _i, _f32p, _i64, _i, _i,
                                  ctypes.POINTER(ctypes.c_int64), _i, _u8p, _i32p]),
+    "ldpc_stage_span": (_i, [_vp, _f32p, _i64, _i, _i]),
     "ldpc_alist_read": (_i, [ctypes.c_char_p, _i32p, _i32p, _i32p, _i32p, _i64]),
     "ldpc_set_waves_per_cu": (_i, [_vp, _i]),
     "ldpc_set_launch_mode": (_i, [_vp, _i]),
@@ -299,6 +300,14 @@ class Decoder:
                                               float(polarity), int(B), _p(packed, _u8p),
                                               _p(synd, _i32p)), self._ctx)
         return dict(packed=packed, synd=synd)
+
+    def stage_span(self, samples, elem_stride=1, max_windows=0):
+        """ldpc_stage_span: copy a sample span to the device for the
+        decode_windows(..., reuse_span=True) calls that follow."""
+        x = np.ascontiguousarray(samples, np.float32).reshape(-1)
+        self._span = x  # the copy is asynchronous: keep the source alive
+        _check(lib().ldpc_stage_span(self._ctx, _p(x, _f32p), x.size, int(elem_stride),
+                                     int(max_windows)), self._ctx)
 
     def decode_windows(self, samples, windows, method=METHOD_SUMPRODUCT, max_iters=50,
                        et_period=1, precision=PREC_F64, elem_stride=1, reuse_span=False):

@@ -247,6 +247,14 @@ int ldpc_decode_windows(ldpc_ctx *ctx, int method, int max_iters, int et_period,
                         int elem_stride, int reuse_span, const int64_t *windows, int B,
                         uint8_t *out_packed, int32_t *syn_weight_opt);
 
+/* Stages a span for the ldpc_decode_windows calls that follow (reuse_span =
+ * 1, same span length), with room for up to max_windows windows per launch:
+ * the copy to the device is enqueued and the call returns, so the caller can
+ * plan its first launch while the span moves.  (The block's general_work
+ * calls it before its first dry run.) */
+int ldpc_stage_span(ldpc_ctx *ctx, const float *in, int64_t n_in_floats, int elem_stride,
+                    int max_windows);
+
 /* Device-resident buffers (already in HBM); enqueues on `hip_stream`
  * (hipStream_t, NULL = the context's own stream) and returns without
  * synchronising -- except min-sum on a large-code context, whose pass loop

@@ -200,6 +200,17 @@ def test_decode_windows_any_positions(graph, method):
         assert out["synd"][b] == ref["synd"][0], b
     assert (again["packed"][::-1] == out["packed"]).all()
     assert (again["synd"][::-1] == out["synd"]).all()
+    # a span staged ahead (ldpc_stage_span, the block's first step) serves
+    # the launches that reuse it; a host-buffer decode in between waits for
+    # its copy before touching the pinned stage
+    other = dec.decode(span[37:37 + 4 * N], method=method, max_iters=20)
+    dec.stage_span(cx, elem_stride=2, max_windows=win.size)
+    mid = dec.decode(span[37:37 + 4 * N], method=method, max_iters=20)
+    assert (mid["packed"] == other["packed"]).all()
+    dec.stage_span(cx, elem_stride=2, max_windows=win.size)
+    pre = dec.decode_windows(cx, win, method=method, max_iters=20, elem_stride=2,
+                             reuse_span=True)
+    assert (pre["packed"] == out["packed"]).all() and (pre["synd"] == out["synd"]).all()
 
 
 def test_decode_windows_rejects_out_of_span():

@@ -65,6 +65,8 @@ def run_plan(env, cache):
     e = dict(os.environ)
     e.update(env)
     out = subprocess.run(cmd, env=e, capture_output=True, text=True, check=True)
+    if out.stderr.strip():
+        sys.stderr.write(out.stderr)
     return [l for l in out.stdout.splitlines() if l.startswith("plan:")][0][5:]
 
 
@@ -113,8 +115,18 @@ def child(cache):
     l, w, i, b = (blk.launches - l0, st["windows"] - w0, st["iters"] - i0,
                   sum(m.size for m in made[m0:]))
     # GPU time model: a launch costs its fixed overhead plus one 50-iteration
-    # frame latency per round of wave slots its windows fill
-    t = sum(MODEL_LAUNCH_US + -(-W // MODEL_SLOTS) * MODEL_ROUND_US for W in per_launch.values())
+    # frame latency per round of wave slots its windows fill; or, with
+    # LDPC_SIM_MODEL="launch_us,window_ns", a fixed cost per launch (host gap +
+    # kernel floor) plus a cost per window (5 iterations on one MI355X:
+    # "56,12.8", profiles/round4/block/)
+    lin = os.environ.get("LDPC_SIM_MODEL")
+    if lin:
+        lu, wn = (float(v) for v in lin.split(","))
+        t = sum(lu + W * wn / 1e3 for W in per_launch.values())
+    else:
+        t = sum(MODEL_LAUNCH_US + -(-W // MODEL_SLOTS) * MODEL_ROUND_US for W in per_launch.values())
+    if os.environ.get("LDPC_SIM_PER_LAUNCH"):
+        sys.stderr.write("windows per launch: %s\n" % [per_launch[k] for k in sorted(per_launch)])
     print("plan:launches %d windows %d iters %d out_frames %d model %.2f ms (%.1f Mbit/s)" % (
         l, w, i, b // 4, t / 1e3, b * 8 / t))
 
