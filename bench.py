@@ -127,11 +127,14 @@ _STREAMS = {}
 
 
 def bench_streams(torch, dev, n):
-    """The process's first n HIP streams, created once and reused by every
-    measurement: torch hands out streams round-robin from a pool, and the
-    streams created later in a process can share hardware queues with one
-    another -- measured: after ~10 extra streams, four batches in flight ran
-    at 800 instead of 1 120 Mbit/s (profiles/round4/headline/streams_ab.txt)."""
+    """n streams for one measurement: fresh ones (default, as every round so
+    far), or with LDPC_BENCH_STREAMS=shared one set created at startup and
+    reused.  Which hardware queues (GPU_MAX_HW_QUEUES = 4) the in-flight
+    batches' streams share depends on the streams the process made before
+    them: measured four batches in flight at 800 instead of 1 120 Mbit/s after
+    ten extra streams, and with the shared set (profiles/round4/headline/)."""
+    if os.environ.get("LDPC_BENCH_STREAMS", "fresh") == "fresh":
+        return [torch.cuda.Stream(dev) for _ in range(n)]
     key = (str(dev),)
     have = _STREAMS.setdefault(key, [])
     while len(have) < n:
@@ -576,11 +579,14 @@ def config5_variant(L, torch, args, dev, sizes=(1, 16, 256, 4096, 65536), check_
                     "cap, one launch at a time (latency mode); latency = HIP-event span per "
                     "launch"}
     kept = {}
+    # one stream for all of it: every stream a process creates shifts which
+    # hardware queues the headline's streams get (profiles/round4/headline/)
+    c5_stream = [torch.cuda.Stream(dev)]
     for name, m in (("sum-product f64 (exact)", 1), ("min-sum f64", 0)):
         rows = {}
         for Bs in sizes:
             r, st = time_variant(time_decoder, dec, torch, [d_y[:Bs]], Bs, m, args.iters, 5, 0,
-                                 10, 3, 1)
+                                 10, 3, 1, streams=c5_stream)
             it = r["iters"]
             rows["B=%d" % Bs] = {"latency_ms": round(r["per_launch_ms"], 5),
                                  "Mbit/s": round(Bs * dec.K * st / r["wall"] / 1e6, 2),
@@ -766,6 +772,8 @@ def main():
     if args.batch is None:
         args.batch = 1024 if dvb else 4096
     D = max(1, args.inflight)
+    if os.environ.get("LDPC_BENCH_STREAMS", "fresh") != "fresh":
+        bench_streams(torch, dev, max(4, D))
 
     csr = None
     if dvb:

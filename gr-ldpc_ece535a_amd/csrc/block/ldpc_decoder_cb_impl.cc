@@ -256,7 +256,7 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
       throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
                                ldpc_last_error(d_ctx));
   }
-  for (int b = 0; b < B; ++b) d_memo[d_want[b] & 1][d_want[b] >> 1] = (int32_t)(base + b);
+  for (int b = 0; b < B; ++b) d_memo[d_want[b] & 1][slot(d_want[b] >> 1)] = (int32_t)(base + b);
   d_touched.insert(d_touched.end(), d_want.begin(), d_want.end());
   d_frames_decoded += B;
   d_launches += 1;
@@ -264,7 +264,7 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
 
 void ldpc_decoder_cb_impl::want(int64_t pos, int pol, int nin) {
   if (pos < 0 || pos + (int64_t)d_N > nin || d_want.size() >= (size_t)max_windows(d_N)) return;
-  int32_t &m = d_memo[pol][pos];
+  int32_t &m = d_memo[pol][slot(pos)];
   if (m == -1) {
     m = -2;  // pending: wanted by this launch
     d_want.push_back((pos << 1) | pol);
@@ -302,14 +302,16 @@ int ldpc_decoder_cb_impl::pass_run(int pol, int pos, int nin) {
   const int32_t *memo = d_memo[pol].data();
   int p = pos;
   while (p + N <= nin) {
-    const int32_t u = memo[p];
+    const int64_t s = slot(p);
+    const int32_t u = memo[s];
     if (u < 0 || d_rsynd[u] > thr) break;
-    p = skip[p] > p ? skip[p] : p + N;
+    p = skip[s] > p ? skip[s] : p + N;
   }
   for (int q = pos; q < p;) {
-    const int nx = skip[q] > q ? skip[q] : q + N;
-    if (skip[q] == 0) d_skip_touched.push_back(((int64_t)q << 1) | pol);
-    skip[q] = p;
+    const int64_t s = slot(q);
+    const int nx = skip[s] > q ? skip[s] : q + N;
+    if (skip[s] == 0) d_skip_touched.push_back(((int64_t)q << 1) | pol);
+    skip[s] = p;
     q = nx;
   }
   return (p - pos) / N;
@@ -336,7 +338,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
           d_grid_frames += k;
           for (int i = 0; i < k; ++i)
             std::memcpy(out + r.produced + (size_t)i * mo,
-                        &d_rpacked[(size_t)d_memo[pol][pos + i * N] * KB], (size_t)mo);
+                        &d_rpacked[(size_t)d_memo[pol][slot(pos + i * N)] * KB], (size_t)mo);
           // two frames in a row pass in sync: their grid is the stream's
           if (k > 1 || d_last_pass == d_abs + pos - N) d_anchor = (int)((d_abs + pos) % N);
           d_last_pass = d_abs + pos + (int64_t)(k - 1) * N;
@@ -351,7 +353,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
     bool guessed_out = false, lost = false, inverted = false, synced = false;
     // checkFrame(vhat, M/8) > M/8 (:166-168); it stops counting past the
     // threshold, so comparing the full weight gives the same decision
-    int32_t use = d_memo[pol][pos];
+    int32_t use = d_memo[pol][slot(pos)];
     // the dry run's guess: a window on the grid the stream was last seen in
     // sync on passes, any other fails (a misaligned window passes ~1 % of the
     // time); with no grid seen yet, frames in sync pass
@@ -368,7 +370,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       // (the complement of a codeword leaves every odd-weight row unsatisfied:
       // 20 of the default H's 32)
       if (pass && d_opposite) {
-        const int32_t o = d_memo[pol ^ 1][pos];
+        const int32_t o = d_memo[pol ^ 1][slot(pos)];
         if (o >= 0 && d_rsynd[o] <= thr) pass = false;
       }
       guessed_out = !pass;
@@ -402,7 +404,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
         }
       }
       if (n.state == STATE_OUT_OF_SYNC) {  // the "-tx" retry, :178-198
-        const int32_t i2 = d_memo[pol ^ 1][pos];
+        const int32_t i2 = d_memo[pol ^ 1][slot(pos)];
         bool pass2 = false;
         if (i2 >= 0) {
           pass2 = d_rsynd[i2] <= thr;
@@ -460,13 +462,22 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   // the memo and the jump table keep their size between calls: only the
   // entries the last call set go back to "not decoded" (a full reset was
   // 2 x 4 bytes per input sample per call)
-  for (int64_t key : d_touched) d_memo[key & 1][key >> 1] = -1;
-  for (int64_t key : d_skip_touched) d_skip[key & 1][key >> 1] = 0;
+  for (int64_t key : d_touched) d_memo[key & 1][slot(key >> 1)] = -1;
+  for (int64_t key : d_skip_touched) d_skip[key & 1][slot(key >> 1)] = 0;
   d_touched.clear();
   d_skip_touched.clear();
-  for (int pl = 0; pl < 2; ++pl) {
-    if (d_memo[pl].size() < npos) d_memo[pl].resize(npos, -1);
-    if (d_skip[pl].size() < npos) d_skip[pl].resize(npos, 0);
+  // every entry is clean again; grow the grid-major tables if this call's
+  // positions need more rows (a larger layout moves every slot)
+  const int64_t rows = (int64_t)npos / N + 2;
+  if (rows > d_rows) {
+    d_rows = std::max(rows, 2 * d_rows);
+    d_nshift = -1;
+    for (int sh = 0; sh < 31; ++sh)
+      if ((1 << sh) == N) d_nshift = sh;
+    for (int pl = 0; pl < 2; ++pl) {
+      d_memo[pl].assign((size_t)N * (size_t)d_rows, -1);
+      d_skip[pl].assign((size_t)N * (size_t)d_rows, 0);
+    }
   }
   d_rsynd.clear();
   d_rpacked.clear();

@@ -82,12 +82,21 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
 
   // general_work's decode memo for the current call: the result of window
   // (position p, polarity) -- p in samples from the call's first input item,
-  // polarity 0 = +tx, 1 = -tx -- is entry d_memo[pol][p] of d_rsynd /
+  // polarity 0 = +tx, 1 = -tx -- is entry d_memo[pol][slot(p)] of d_rsynd /
   // d_rpacked (-1: not decoded, -2: wanted by the launch being planned).  Keys are (p << 1) | pol.
   std::vector<int32_t> d_memo[2];
   std::vector<int32_t> d_rsynd;
-  // d_skip[pol][p] > p: frames p, p + N, ... before it are decoded and pass
+  // d_skip[pol][slot(p)] > p: frames p, p + N, ... before it are decoded and pass
   std::vector<int32_t> d_skip[2];
+  // memo and jump entries are stored grid-major -- position p at
+  // (p mod N) * d_rows + p / N -- so a run of frames on one grid reads
+  // consecutive words instead of one word every N
+  int64_t d_rows = 0;
+  int d_nshift = -1;  // log2(N) when N is a power of two
+  int64_t slot(int64_t p) const {
+    return d_nshift >= 0 ? (p & (((int64_t)1 << d_nshift) - 1)) * d_rows + (p >> d_nshift)
+                         : (p % (int64_t)d_N) * d_rows + p / (int64_t)d_N;
+  }
   // keys whose memo / jump entries this call set (reset at the next call)
   std::vector<int64_t> d_touched, d_skip_touched;
   std::vector<uint8_t> d_rpacked;

@@ -144,7 +144,7 @@ struct MsnWork {
   void *LQ;          // chunks x N x F Real: Lci + sum of the column's L(r)
   void *m1, *m2;     // chunks x M x F Real
   uint8_t *meta;     // chunks x M x F: (P + 1) << 6 | (i1 + 1)
-  uint8_t *alpha;    // chunks x dc_max x M ([t][p]): bit 2f L(q) < 0, bit 2f+1 sign 0
+  uint8_t *alpha;    // chunks x dc_max x M ([t][p]; 2 frames: nibbles, [t/2][p]): bit 2f L(q) < 0, bit 2f+1 sign 0
   uint8_t *odd;      // chunks x check_waves: frames with an unsatisfied row
   int32_t *capsyn;   // S: syndrome weight of a frame stopping at the cap
   int32_t *it;       // S: iterations the slot's frame has executed

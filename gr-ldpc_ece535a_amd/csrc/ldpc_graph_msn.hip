@@ -97,16 +97,11 @@ __device__ __forceinline__ void stv(Real *p, const Vec<Real> &x) {
 template <typename Real>
 __device__ __forceinline__ Vec<Real> ldv_nt(const Real *p) {
 #if LDPC_MSN_NT
-  typedef Real V2 __attribute__((ext_vector_type(16 / sizeof(Real))));
-  constexpr int n = kF * sizeof(Real) / 16;
+  typedef Real V __attribute__((ext_vector_type(kF)));
+  const V v = __builtin_nontemporal_load((const V *)p);
   Vec<Real> r;
-  static_assert(n >= 1 && sizeof(Vec<Real>) == 16 * n, "");
 #pragma unroll
-  for (int i = 0; i < n; ++i) {
-    const V2 v = __builtin_nontemporal_load((const V2 *)p + i);
-#pragma unroll
-    for (int j = 0; j < (int)(16 / sizeof(Real)); ++j) r.v[i * (16 / sizeof(Real)) + j] = v[j];
-  }
+  for (int j = 0; j < kF; ++j) r.v[j] = v[j];
   return r;
 #else
   return ldv(p);
@@ -115,15 +110,11 @@ __device__ __forceinline__ Vec<Real> ldv_nt(const Real *p) {
 template <typename Real>
 __device__ __forceinline__ void stv_nt(Real *p, const Vec<Real> &x) {
 #if LDPC_MSN_NT
-  typedef Real V2 __attribute__((ext_vector_type(16 / sizeof(Real))));
-  constexpr int n = kF * sizeof(Real) / 16;
+  typedef Real V __attribute__((ext_vector_type(kF)));
+  V v;
 #pragma unroll
-  for (int i = 0; i < n; ++i) {
-    V2 v;
-#pragma unroll
-    for (int j = 0; j < (int)(16 / sizeof(Real)); ++j) v[j] = x.v[i * (16 / sizeof(Real)) + j];
-    __builtin_nontemporal_store(v, (V2 *)p + i);
-  }
+  for (int j = 0; j < kF; ++j) v[j] = x.v[j];
+  __builtin_nontemporal_store(v, (V *)p);
 #else
   stv(p, x);
 #endif
@@ -140,6 +131,12 @@ __device__ __forceinline__ void st_meta(uint8_t *p, MetaWord m) {
 
 // alpha of an edge for frame f from the chunk's byte: bit 2f L(q) < 0, bit
 // 2f+1 sign 0 (:338, sign(0) = sign(NaN) = 0)
+// With 2 frames per chunk an edge's alpha bits take a nibble: slots 2u and
+// 2u + 1 of a row share byte u ([u][p] per chunk), half the bytes.
+constexpr bool kAlphaNibbles = kF == 2;
+__host__ __device__ __forceinline__ int alpha_rows(int dc_max) {
+  return kAlphaNibbles ? (dc_max + 1) / 2 : dc_max;
+}
 __device__ __forceinline__ int alpha_of(uint32_t byte, int f) {
   const uint32_t b = byte >> (2 * f);
   return (b & 2u) ? 0 : ((b & 1u) ? -1 : 1);
@@ -257,7 +254,7 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
   Real *m1 = (Real *)w.m1, *m2 = (Real *)w.m2;
   const Real *LQ = (const Real *)w.LQ;
   const int64_t ro = el(k, g.M, p);
-  uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M + p;  // [t][p]
+  uint8_t *alpha = w.alpha + (int64_t)k * alpha_rows(g.dc_max) * g.M + p;  // [t][p] / [t/2][p]
   Vec<Real> lq[D];
 #pragma unroll
   for (int t = 0; t < D; ++t) lq[t] = ldv(LQ + el(k, g.N, cs[t]));
@@ -303,9 +300,16 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
   stv_nt(m1 + ro, n1);
   stv_nt(m2 + ro, n2);
   st_meta(w.meta + ro, nmt);
+  if constexpr (kAlphaNibbles) {
 #pragma unroll
-  for (int t = 0; t < D; ++t)
-    if (ok[t]) alpha[(int64_t)t * g.M] = (uint8_t)nb[t];
+    for (int u = 0; 2 * u < D; ++u)
+      if (ok[2 * u])
+        alpha[(int64_t)u * g.M] = (uint8_t)(nb[2 * u] | (2 * u + 1 < D ? nb[2 * u + 1] << 4 : 0u));
+  } else {
+#pragma unroll
+    for (int t = 0; t < D; ++t)
+      if (ok[t]) alpha[(int64_t)t * g.M] = (uint8_t)nb[t];
+  }
 }
 
 // One row per lane, the chunk's F frames in the lane.  Frames whose slot is
@@ -316,8 +320,15 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
 // per frame f, "a row of these blocks is unsatisfied" (bits 12(f+1)..), in
 // two levels (8 group words per chunk, then the chunk's word); no fence and
 // no waiting (a chunk that is not live decides in its block 0 alone).
+// occupancy hints (waves per SIMD; A/B knobs)
+#ifndef LDPC_MSN_CHECK_MINB
+#define LDPC_MSN_CHECK_MINB 1
+#endif
+#ifndef LDPC_MSN_VAR_MINB
+#define LDPC_MSN_VAR_MINB 1
+#endif
 template <int PREC, int DC, bool FUSE>
-__global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int mbuf, int max_iters,
+__global__ void __launch_bounds__(256, LDPC_MSN_CHECK_MINB) msn_check(MsnView g, MsnWork w, int mbuf, int max_iters,
                                                  int et_period, int B, int32_t *synd) {
   typedef typename Math<PREC>::Real Real;
   int k, bi;
@@ -336,9 +347,18 @@ __global__ void __launch_bounds__(256) msn_check(MsnView g, MsnWork w, int mbuf,
   const Vec<Real> om1 = ldv_nt((const Real *)w.m1 + ro), om2 = ldv_nt((const Real *)w.m2 + ro);
   const MetaWord omt = ld_meta(w.meta + ro);
   uint32_t ab[DC];
-  const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M + pl;  // [t][p]
+  const uint8_t *alpha = w.alpha + (int64_t)k * alpha_rows(g.dc_max) * g.M + pl;
+  if constexpr (kAlphaNibbles) {
 #pragma unroll
-  for (int t = 0; t < DC; ++t) ab[t] = t < g.dc_max ? alpha[(int64_t)t * g.M] : 0u;
+    for (int u = 0; 2 * u < DC; ++u) {
+      const uint32_t byte = 2 * u < g.dc_max ? alpha[(int64_t)u * g.M] : 0u;
+      ab[2 * u] = byte & 15u;
+      if (2 * u + 1 < DC) ab[2 * u + 1] = byte >> 4;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < DC; ++t) ab[t] = t < g.dc_max ? alpha[(int64_t)t * g.M] : 0u;
+  }
   if (!live) {
     if (FUSE && bi == 0 && threadIdx.x < 64)
       decide_slots(w, k, 0u, mbuf ^ 1, max_iters, et_period, B, synd);
@@ -552,7 +572,7 @@ template <typename Real, int T0, int D, int NW>
 __device__ __forceinline__ void var_edges(const MsnView &g, const MsnWork &w, int k,
                                           const int (&word)[NW], Vec<Real> &s) {
   const Real *m1 = (const Real *)w.m1, *m2 = (const Real *)w.m2;
-  const uint8_t *alpha = w.alpha + (int64_t)k * g.dc_max * g.M;
+  const uint8_t *alpha = w.alpha + (int64_t)k * alpha_rows(g.dc_max) * g.M;
   int v[D];
   edge_values<T0, D>(word, g.cx, v);
   bool ok[D];
@@ -565,7 +585,7 @@ __device__ __forceinline__ void var_edges(const MsnView &g, const MsnWork &w, in
     const int rp = ok[t] ? (v[t] & 0xffffff) : 0;
     place[t] = ok[t] ? (v[t] >> 24) : 0;
     ro[t] = el(k, g.M, rp);
-    ai[t] = (uint32_t)place[t] * (uint32_t)g.M + (uint32_t)rp;
+    ai[t] = (uint32_t)(kAlphaNibbles ? place[t] >> 1 : place[t]) * (uint32_t)g.M + (uint32_t)rp;
   }
   MetaWord mt[D];
   uint32_t ab[D];
@@ -574,6 +594,7 @@ __device__ __forceinline__ void var_edges(const MsnView &g, const MsnWork &w, in
   for (int t = 0; t < D; ++t) {
     mt[t] = ld_meta(w.meta + ro[t]);
     ab[t] = alpha[ai[t]];
+    if constexpr (kAlphaNibbles) ab[t] = (ab[t] >> (4 * (place[t] & 1))) & 15u;
     v1[t] = ldv(m1 + ro[t]);
     v2[t] = ldv(m2 + ro[t]);
   }
@@ -607,7 +628,7 @@ __device__ void var_edges_rt(const MsnView &g, const MsnWork &w, int k, const in
 // bytes (8 lanes' decisions, MSB first, :207-219), iterations, and the
 // optional bits / posteriors -- instead of in msn_post / msn_cols.
 template <typename Real, int DV>
-__global__ void __launch_bounds__(256) msn_var(MsnView g, MsnWork w, DecodeArgs a, int nb) {
+__global__ void __launch_bounds__(256, LDPC_MSN_VAR_MINB) msn_var(MsnView g, MsnWork w, DecodeArgs a, int nb) {
   int k, bi;
   map_block(blockIdx.x, w.chunks, w.nb_var, k, bi);
   const int m = nb * w.chunks + k;  // the decision's mask buffer
@@ -752,7 +773,7 @@ size_t msn_work_bytes(const MsnView &g, int chunks, int prec) {
   const size_t nbc = (size_t)((g.M + kIB - 1) / kIB);
   size_t n = al256(C * g.N * F * 4) + al256(C * g.N * F * real);  // L, LQ
   n += 2 * al256(C * g.M * F * real) + al256(C * g.M * F);        // m1, m2, meta
-  n += al256(C * g.dc_max * g.M);                                 // alpha
+  n += al256(C * alpha_rows(g.dc_max) * g.M);                     // alpha
   n += al256(C * nbc * 4);                                        // odd
   n += 5 * al256(C * F * 4);                                      // capsyn, it, frame, out_frame, used
   n += 4 * al256(2 * C * 4) + al256(C * 9 * 8) + al256(64);      // masks x 2, arrive, ctrl
@@ -780,7 +801,7 @@ void msn_work_carve(MsnWork &w, void *base, const MsnView &g, int chunks, int pr
   w.m1 = take(C * g.M * F * real);
   w.m2 = take(C * g.M * F * real);
   w.meta = (uint8_t *)take(C * g.M * F);
-  w.alpha = (uint8_t *)take(C * g.dc_max * g.M);
+  w.alpha = (uint8_t *)take(C * alpha_rows(g.dc_max) * g.M);
   w.odd = (uint8_t *)take(C * (size_t)w.check_waves);
   w.capsyn = (int32_t *)take(C * F * 4);
   w.it = (int32_t *)take(C * F * 4);
