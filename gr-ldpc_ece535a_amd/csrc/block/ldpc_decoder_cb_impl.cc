@@ -53,6 +53,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cstring>
 #include <iostream>
 #include <cstdio>
@@ -202,7 +203,58 @@ ldpc_decoder_cb_impl::ldpc_decoder_cb_impl(int method, int iterations, ldpc_bloc
   d_backend_user = user;
 }
 
+void ldpc_decoder_cb_impl::stage_async(const float *in, int64_t n_floats, int max_windows) {
+  Stager &sg = d_stager;
+  if (!d_stage_thread) {
+    sg.rc = ldpc_stage_span(d_ctx, in, n_floats, 2, max_windows);
+    return;
+  }
+  if (!sg.th.joinable())
+    sg.th = std::thread([&sg]() {
+      std::unique_lock<std::mutex> lk(sg.mu);
+      for (;;) {
+        sg.cv.wait(lk, [&sg]() { return sg.busy || sg.quit; });
+        if (sg.quit) return;
+        lk.unlock();
+        const int rc = ldpc_stage_span(sg.ctx, sg.in, sg.n, 2, sg.max_windows);
+        lk.lock();
+        sg.rc = rc;
+        sg.busy = false;
+        sg.cv.notify_all();
+      }
+    });
+  std::lock_guard<std::mutex> lk(sg.mu);
+  sg.ctx = d_ctx;
+  sg.in = in;
+  sg.n = n_floats;
+  sg.max_windows = max_windows;
+  sg.busy = true;
+  sg.cv.notify_all();
+}
+
+int ldpc_decoder_cb_impl::stage_wait() {
+  Stager &sg = d_stager;
+  if (!d_stage_thread) return sg.rc;
+  std::unique_lock<std::mutex> lk(sg.mu);
+  sg.cv.wait(lk, [&sg]() { return !sg.busy; });
+  return sg.rc;
+}
+
 ldpc_decoder_cb_impl::~ldpc_decoder_cb_impl() {
+  if (d_stager.th.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(d_stager.mu);
+      d_stager.quit = true;
+      d_stager.cv.notify_all();
+    }
+    d_stager.th.join();
+  }
+  if (d_profile && d_walk_calls)
+    fprintf(stderr,
+            "ldpc_decoder_cb walk profile: %lld calls (%lld fell back to the host planner); host "
+            "%.3f ms, device loop %.3f ms, of it waiting %.3f ms\n",
+            (long long)d_walk_calls, (long long)d_walk_fallbacks, 1e-3 * d_walk_prof[0],
+            1e-3 * d_walk_prof[1], 1e-3 * d_walk_prof[2]);
   if (d_profile)
     fprintf(stderr,
             "ldpc_decoder_cb profile: %lld launches; general_work %.3f ms = exact replay %.3f + "
@@ -450,6 +502,78 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
   return DONE;
 }
 
+// One call's loop on the device (ldpc_walk_span): the same bytes, messages,
+// consumption and state as the replay below, without host round trips.
+// False: the walk did not run (unsupported code, or a wait passed its
+// deadline), and the caller plans the call on the host instead.
+bool ldpc_decoder_cb_impl::walk_call(const float *in, int nin, int noutput_items,
+                                     unsigned char *out, int &produced) {
+  const double t0 = now_s();
+  const int N = (int)d_N;
+  ldpc_walk_io io{};
+  io.state = d_state;
+  io.errors = (int32_t)d_errors;
+  // the last in-sync pass, relative to this span (far below 0: none seen)
+  io.last_pass = d_last_pass >= 0 ? d_last_pass - d_abs : INT64_MIN / 4;
+  io.anchor_pos = d_anchor >= 0 ? ((d_anchor - d_abs) % N + N) % N : -1;
+  const int cap = std::max(64, nin / 4 + 64);  // messages: one sync event per few frames at most
+  if ((int)d_walk_msgs.size() < cap) d_walk_msgs.resize((size_t)cap);
+  const int rc = ldpc_walk_span(d_ctx, d_method, (int)d_iterations, d_precision, in,
+                                2 * (int64_t)nin, 2, 0, noutput_items, &io, out,
+                                d_walk_msgs.data(), cap);
+  if (rc == LDPC_EUNSUPPORTED) {
+    d_walk = false;  // this code stays on the host planner
+    return false;
+  }
+  if (rc == LDPC_ETIMEOUT) {
+    if (d_walk_fallbacks++ == 0)
+      std::cerr << "ldpc_decoder_cb: device walk timed out; planning this call on the host"
+                << std::endl;
+    return false;
+  }
+  if (rc != LDPC_OK)
+    throw std::runtime_error(std::string("ldpc_decoder_cb: walk failed: ") + ldpc_last_error(d_ctx));
+  for (int i = 0; i < io.n_msgs; ++i) {
+    const int m = d_walk_msgs[(size_t)i];
+    if (m == LDPC_WALK_MSG_LOST)
+      std::cout << "MAX ERRORS; OUT OF SYNC" << std::endl;
+    else if (m == LDPC_WALK_MSG_INVERTED)
+      std::cout << "IN SYNC; PHASE INVERTED" << std::endl;
+    else
+      std::cout << "IN SYNC" << std::endl;
+  }
+  d_state = io.state;
+  d_errors = (unsigned)io.errors;
+  if (io.last_pass > INT64_MIN / 8) d_last_pass = d_abs + io.last_pass;
+  if (io.anchor_pos >= 0) d_anchor = (int)((d_abs + io.anchor_pos) % N);
+  d_grid_frames += io.grid_frames;
+  d_grid_fails += io.grid_fails;
+  while (d_grid_frames > 4096) {
+    d_grid_frames *= 0.5;
+    d_grid_fails *= 0.5;
+  }
+  d_abs += io.consumed;
+  d_frames_decoded += io.requests;
+  d_launches += 1;
+  d_walk_calls += 1;
+  consume_each((int)io.consumed);
+  produced = io.produced;
+  if (d_profile) {
+    const double dt = now_s() - t0;
+    d_prof[0] += dt;
+    d_walk_prof[0] += 1e6 * dt;
+    d_walk_prof[1] += io.walk_us;
+    d_walk_prof[2] += io.wait_us;
+    if (getenv("LDPC_BLOCK_PROFILE")[0] == '2')
+      fprintf(stderr,
+              "general_work walk: %.1f us = device loop %.1f (waiting %.1f) + rest; %d windows, "
+              "%d unplanned, %d steps, %d restarts, %lld items\n",
+              1e6 * dt, io.walk_us, io.wait_us, io.requests, io.surprises, io.steps, io.restarts,
+              (long long)io.consumed);
+  }
+  return true;
+}
+
 int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_items,
                                        gr_vector_const_void_star &input_items,
                                        gr_vector_void_star &output_items) {
@@ -458,6 +582,10 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   unsigned char *out = (unsigned char *)output_items[0];
   const int N = (int)d_N;
   const int nin = ninput_items[0];
+  if (d_walk && !d_backend) {
+    int produced = 0;
+    if (walk_call(in, nin, noutput_items, out, produced)) return produced;
+  }
   const size_t npos = (size_t)std::max(nin - N + 1, 0);
   // the memo and the jump table keep their size between calls: only the
   // entries the last call set go back to "not decoded" (a full reset was
@@ -485,12 +613,26 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   Replay r{d_state, d_errors, 0, 0};
   // the span goes to the device while the first dry run plans (every launch
   // of this call then reuses it)
+  // (the worker reads `in`: it is joined on every way out of this call)
+  struct StageJoin {
+    ldpc_decoder_cb_impl *self;
+    bool pending = false;
+    void operator()() {
+      if (pending) {
+        pending = false;
+        if (self->stage_wait() < 0)
+          throw std::runtime_error(std::string("ldpc_decoder_cb: staging failed: ") +
+                                   ldpc_last_error(self->d_ctx));
+      }
+    }
+    ~StageJoin() {
+      if (pending) self->stage_wait();
+    }
+  } join_stage{this};
   bool staged = false;
   if (!d_backend && nin >= N && noutput_items >= d_out_bytes) {
-    if (ldpc_stage_span(d_ctx, in, 2 * (int64_t)nin, 2, max_windows(d_N)) < 0)
-      throw std::runtime_error(std::string("ldpc_decoder_cb: staging failed: ") +
-                               ldpc_last_error(d_ctx));
-    staged = true;
+    stage_async(in, 2 * (int64_t)nin, max_windows(d_N));
+    staged = join_stage.pending = true;
   }
   const int search_first = std::min(std::max(d_search_first, 1), max_windows(d_N));
   int out_budget = search_first;  // out-of-sync positions one launch may guess past
@@ -535,11 +677,23 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       std::cerr << "ldpc_decoder_cb: stall at " << r.consumed << " state " << r.state
                 << " errors " << r.errors << " grid " << d_anchor << ": launch " << d_want.size()
                 << " windows, dry run to " << dry.consumed << " state " << dry.state << std::endl;
+    if (d_debug && getenv("LDPC_BLOCK_DEBUG")[0] == '2') {  // what the launch holds
+      int64_t on_grid[2] = {0, 0}, off_grid[2] = {0, 0}, lo = INT64_MAX, hi = -1;
+      for (int64_t w : d_want) {
+        const int64_t p = w >> 1;
+        ((d_anchor >= 0 && (d_abs + p) % (int64_t)d_N == d_anchor) ? on_grid : off_grid)[w & 1]++;
+        lo = std::min(lo, p);
+        hi = std::max(hi, p);
+      }
+      std::cerr << "  on grid " << on_grid[0] << "+" << on_grid[1] << " off grid " << off_grid[0]
+                << "+" << off_grid[1] << " positions " << lo << ".." << hi << std::endl;
+    }
     if (d_profile) {
       const double t1 = now_s();
       d_prof[2] += t1 - t0;
       t0 = t1;
     }
+    join_stage();  // the span is on its way to the device before the launch
     decode_wanted(in, nin, first && !staged);
     if (d_profile) {
       const double t1 = now_s();
@@ -560,6 +714,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       for (int i = 0; i < 4; ++i) last[i] = d_prof[i];
     }
   }
+  join_stage();  // no launch this call: the staging must still finish
   d_state = r.state;
   d_errors = r.errors;
   d_abs += r.consumed;

@@ -18,7 +18,10 @@
 
 #include <stdlib.h>
 
+#include <condition_variable>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace gr {
@@ -39,6 +42,32 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   void *d_backend_user;
   int64_t d_frames_decoded;
   int64_t d_launches = 0;
+  // A worker thread stages each call's span (ldpc_stage_span: the real parts
+  // copied into pinned memory and sent to the device) while general_work
+  // plans its first launch; joined before that launch.  LDPC_BLOCK_STAGE_THREAD=0:
+  // staged inline.
+  struct Stager {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool busy = false, quit = false;
+    int rc = 0;
+    ldpc_ctx *ctx = nullptr;
+    const float *in = nullptr;
+    int64_t n = 0;
+    int max_windows = 0;
+  } d_stager;
+  bool d_stage_thread = !(getenv("LDPC_BLOCK_STAGE_THREAD") && getenv("LDPC_BLOCK_STAGE_THREAD")[0] == '0');
+  void stage_async(const float *in, int64_t n_floats, int max_windows);
+  int stage_wait();
+  // LDPC_BLOCK_WALK=1: the whole frame loop of a call as one device launch
+  // (ldpc_walk_span); otherwise, with a backend, or for a code the walk does
+  // not take: the host planner below (dry-run replay + window launches)
+  bool d_walk = getenv("LDPC_BLOCK_WALK") && getenv("LDPC_BLOCK_WALK")[0] == '1';
+  std::vector<uint8_t> d_walk_msgs;
+  int64_t d_walk_calls = 0, d_walk_fallbacks = 0;
+  double d_walk_prof[3] = {0, 0, 0};  // host call, device loop, device waits (us)
+  bool walk_call(const float *in, int nin, int noutput_items, unsigned char *out, int &produced);
   bool d_debug = getenv("LDPC_BLOCK_DEBUG") != nullptr;  // one line per launch on stderr
   // LDPC_BLOCK_PROFILE: host time split of general_work, printed when destroyed
   bool d_profile = getenv("LDPC_BLOCK_PROFILE") != nullptr;

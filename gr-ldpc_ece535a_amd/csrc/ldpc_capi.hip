@@ -60,6 +60,15 @@ struct ldpc_ctx {
   int64_t *h_win = nullptr;
   size_t h_win_bytes = 0;
   int64_t span_samples = 0;
+  // ldpc_walk_span (ldpc_walk.hip): [ctl | res | reqd | req] on the device,
+  // zeroed when (re)allocated and when the epoch wraps; summary, messages and
+  // output bytes in mapped pinned memory the walker writes directly
+  void *d_walk = nullptr;
+  size_t walk_bytes = 0;
+  int64_t walk_cap = 0;  // positions per polarity
+  uint32_t walk_epoch = 0;
+  uint8_t *h_walk = nullptr;
+  size_t h_walk_bytes = 0;
   // large-code min-sum: 2 narrow-chunk pipeline (ldpc_graph_msn.hip), 0 the
   // edge-message passes (ldpc_graph.hip)
   int ms_mode = 2;
@@ -920,6 +929,8 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
   if (ctx->d_wstage) (void)hipFree(ctx->d_wstage);
   if (ctx->h_win) (void)hipHostFree(ctx->h_win);
+  if (ctx->d_walk) (void)hipFree(ctx->d_walk);
+  if (ctx->h_walk) (void)hipHostFree(ctx->h_walk);
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
     if (p) (void)hipFree(p);
@@ -1437,9 +1448,179 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   return LDPC_OK;
 }
 
+// The walker's buffers for spans of up to `cap` positions (ldpc_walk_span).
+constexpr int64_t kWalkReqSlack = 16384;  // request slots decoders may claim past the last request
+size_t walk_layout(int64_t cap, size_t off[4]) {
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  off[0] = 0;                                                       // ctl
+  off[1] = al((size_t)ldpc::kWalkCtlWords * 4);                     // res
+  off[2] = off[1] + al((size_t)2 * cap * 8);                        // reqd
+  off[3] = off[2] + al((size_t)2 * cap * 4);                        // req
+  return off[3] + al((size_t)(2 * cap + kWalkReqSlack) * 8);
+}
+
+int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, const float *in,
+                   int64_t n_in_floats, int elem_stride, int reuse_span, int noutput_bytes,
+                   ldpc_walk_io *io, uint8_t *out, uint8_t *msgs, int msgs_cap) {
+  int rc = check_decode_args(ctx, method, max_iters, 1, precision, 1, elem_stride, ctx ? ctx->N : 1);
+  if (rc != LDPC_OK) return rc;
+  const int N = ctx->N, mo = ctx->M / 8;
+  if (ctx->graph || ctx->KB > 4 || mo > 4 || mo < 1 || N > 64)
+    return set_err(ctx, LDPC_EUNSUPPORTED,
+                   "the device walk takes small codes with N <= 64, M/8 <= 4, KB <= 4");
+  if (!in || !io || (noutput_bytes > 0 && !out) || msgs_cap < 0 || (msgs_cap > 0 && !msgs) ||
+      noutput_bytes < 0)
+    return set_err(ctx, LDPC_EINVAL, "bad walk buffers");
+  if (io->state < 0 || io->state > 2 || io->errors < 0 || io->errors > 10)
+    return set_err(ctx, LDPC_EINVAL, "walk state out of range");
+  const int64_t S = (n_in_floats + elem_stride - 1) / elem_stride;
+  const int nout = noutput_bytes / mo;
+  const int64_t anchor_in = io->anchor_pos;
+  io->consumed = 0;
+  io->produced = 0;
+  io->n_msgs = 0;
+  io->anchor_pos = -1;
+  io->grid_frames = io->grid_fails = io->requests = io->surprises = io->steps = io->restarts = 0;
+  io->walk_us = io->wait_us = 0.0;
+  if (S < N || nout == 0 || msgs_cap < 2) return LDPC_OK;  // the loop would not run (:146-147)
+  if (S >= ((int64_t)1 << 30)) return set_err(ctx, LDPC_EINVAL, "span too long for one walk");
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  // the span, as for ldpc_decode_windows
+  rc = ensure_window_stage(ctx, al((size_t)S * 4));
+  if (rc != LDPC_OK) return rc;
+  if (!(reuse_span && ctx->span_samples == S)) {
+    rc = copy_span(ctx, in, S, elem_stride, (float *)ctx->d_wstage);
+    if (rc != LDPC_OK) return rc;
+  }
+  // device buffers
+  size_t off[4];
+  bool zero = false;
+  if (S > ctx->walk_cap) {
+    const int64_t cap = std::max<int64_t>(S + S / 2, 1 << 16);
+    const size_t bytes = walk_layout(cap, off);
+    if (ctx->d_walk) {
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipFree(ctx->d_walk);
+      ctx->d_walk = nullptr;
+      ctx->walk_cap = 0;
+    }
+    if ((e = hipMalloc(&ctx->d_walk, bytes)) != hipSuccess) return hip_err(ctx, e, "hipMalloc(walk)");
+    ctx->walk_bytes = bytes;
+    ctx->walk_cap = cap;
+    zero = true;
+  }
+  walk_layout(ctx->walk_cap, off);
+  if (++ctx->walk_epoch >= (1u << 23)) {  // tags are 23 bits: start over from zeroed buffers
+    ctx->walk_epoch = 1;
+    zero = true;
+  }
+  if (zero && (e = hipMemsetAsync(ctx->d_walk, 0, ctx->walk_bytes, ctx->stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipMemsetAsync(walk)");
+  // the queue heads and the done word, every call
+  if ((e = hipMemsetAsync(ctx->d_walk, 0, (size_t)ldpc::kWalkCtlWords * 4, ctx->stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipMemsetAsync(walk ctl)");
+  // mapped host memory: summary, messages, output bytes
+  const size_t h_need = al(sizeof(ldpc::WalkSummary)) + al((size_t)msgs_cap) + al((size_t)nout * mo);
+  if (h_need > ctx->h_walk_bytes) {
+    if (ctx->h_walk) {
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipHostFree(ctx->h_walk);
+      ctx->h_walk = nullptr;
+      ctx->h_walk_bytes = 0;
+    }
+    const size_t want = std::max(h_need + h_need / 2, (size_t)1 << 16);
+    if ((e = hipHostMalloc((void **)&ctx->h_walk, want, hipHostMallocMapped | hipHostMallocCoherent)) !=
+        hipSuccess)
+      return hip_err(ctx, e, "hipHostMalloc(walk)");
+    ctx->h_walk_bytes = want;
+  }
+  void *dh = nullptr;
+  if ((e = hipHostGetDevicePointer(&dh, ctx->h_walk, 0)) != hipSuccess)
+    return hip_err(ctx, e, "hipHostGetDevicePointer(walk)");
+  char *base = (char *)ctx->d_walk;
+  ldpc::WalkArgs w{};
+  w.ctl = (uint32_t *)(base + off[0]);
+  w.res = (uint64_t *)(base + off[1]);
+  w.reqd = (uint32_t *)(base + off[2]);
+  w.req = (uint64_t *)(base + off[3]);
+  w.sum = (ldpc::WalkSummary *)dh;
+  w.msgs = (uint8_t *)dh + al(sizeof(ldpc::WalkSummary));
+  w.out = w.msgs + al((size_t)msgs_cap);
+  w.cap = ctx->walk_cap;
+  w.req_cap = 2 * ctx->walk_cap + kWalkReqSlack;
+  w.nin = S;
+  w.N = N;
+  w.M = ctx->M;
+  w.KB = ctx->KB;
+  w.mo = mo;
+  w.thr = ctx->M / 8;  // :142
+  w.nout = nout;
+  w.msgs_cap = msgs_cap;
+  w.state = io->state;
+  w.errors = io->errors;
+  w.last_pass = io->last_pass;
+  w.anchor = anchor_in >= 0 ? anchor_in % N : -1;
+  w.epoch = ctx->walk_epoch;
+  const int lead = getenv("LDPC_WALK_LEAD") ? atoi(getenv("LDPC_WALK_LEAD")) : 512;
+  static const double deadline_ms =
+      getenv("LDPC_WALK_DEADLINE_MS") ? atof(getenv("LDPC_WALK_DEADLINE_MS")) : 200.0;
+  w.lead = std::max(lead, 1);
+  w.deadline = (uint64_t)(deadline_ms * 1e5);  // 100 MHz ticks
+  ldpc::DecodeArgs a{};
+  a.in = (const float *)ctx->d_wstage;
+  a.cw_stride = N;
+  a.elem_stride = 1;
+  a.polarity = 1.0f;
+  a.max_iters = max_iters;
+  a.et_period = 1;
+  a.fair_cycles = 0;
+  const int lr = ldpc::launch_walk(code_view(ctx), a, w, method, precision, ctx->slots, ctx->nw, 0,
+                                   ctx->stream);
+  if (lr == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no walk kernel for this code shape");
+  if (lr != 0) return hip_err(ctx, hipGetLastError(), "walk launch");
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipStreamSynchronize(walk)");
+  const ldpc::WalkSummary &sm = *(const ldpc::WalkSummary *)ctx->h_walk;
+  io->walk_us = (double)sm.total_ticks * 1e-2;
+  io->wait_us = (double)sm.wait_ticks * 1e-2;
+  io->requests = sm.requests;
+  io->surprises = sm.surprises;
+  io->steps = sm.steps;
+  io->restarts = sm.restarts;
+  if (getenv("LDPC_WALK_TRACE"))
+    fprintf(stderr,
+            "walk: %.1f us (waiting %.1f), %d steps, %d windows; surprises sync %d search %d retry "
+            "%d; guesses %d (%d wrong); restarts %d (%d behind)\n",
+            io->walk_us, io->wait_us, sm.steps, sm.requests, sm.diag[0], sm.diag[1], sm.diag[2],
+            sm.diag[3], sm.diag[4], sm.restarts, sm.diag[5]);
+  if (sm.status != 0) return set_err(ctx, LDPC_ETIMEOUT, "a wait of the walk passed its deadline");
+  io->state = sm.state;
+  io->errors = sm.errors;
+  io->last_pass = sm.last_pass;
+  io->anchor_pos = sm.anchor_pos;
+  io->consumed = sm.consumed;
+  io->produced = sm.produced * mo;
+  io->n_msgs = sm.n_msgs;
+  io->grid_frames = sm.grid_frames;
+  io->grid_fails = sm.grid_fails;
+  const uint8_t *hm = ctx->h_walk + al(sizeof(ldpc::WalkSummary));
+  if (sm.n_msgs > 0) memcpy(msgs, hm, (size_t)sm.n_msgs);
+  if (sm.produced > 0) memcpy(out, hm + al((size_t)msgs_cap), (size_t)sm.produced * mo);
+  return LDPC_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int ldpc_walk_span(ldpc_ctx *ctx, int method, int max_iters, int precision, const float *in,
+                   int64_t n_in_floats, int elem_stride, int reuse_span, int noutput_bytes,
+                   ldpc_walk_io *io, uint8_t *out, uint8_t *msgs, int msgs_cap) {
+  return walk_span_impl(ctx, method, max_iters, precision, in, n_in_floats, elem_stride,
+                        reuse_span, noutput_bytes, io, out, msgs, msgs_cap);
+}
 
 int ldpc_stage_span(ldpc_ctx *ctx, const float *in, int64_t n_in_floats, int elem_stride,
                     int max_windows) {

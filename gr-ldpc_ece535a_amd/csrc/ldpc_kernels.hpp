@@ -109,6 +109,63 @@ struct DecodeArgs {
   uint32_t fair_cycles;
 };
 
+// ---------------------------------------------------------------------------
+// The block walker (ldpc_walk.hip): one persistent launch runs the
+// reference's frame loop (lib/ldpc_decoder_cb_impl.cc:146-226) over a whole
+// staged span.  Wave 0 of workgroup 0 walks the loop; every other wave decodes
+// the windows it asks for (a window = the N samples at a position, at one
+// polarity), pulled from a request queue.  Hand-offs are 8-byte granules
+// {tag, value} written by one agent-scope (sc1) store and polled with sc1
+// loads (MI355X_MICROARCH.md, inter-workgroup visibility, R2).
+// ---------------------------------------------------------------------------
+constexpr int kWalkDone = 256;  // ctl word set when the walker has finished
+constexpr int kWalkCtlWords = 272;  // zeroed per launch: 8 queue heads (one per 128 B) + done
+enum { kWalkMsgLost = 1, kWalkMsgInverted = 2, kWalkMsgSync = 3 };
+
+struct WalkSummary {
+  int64_t consumed;     // samples the loop consumed
+  int64_t last_pass;    // position of the last window that passed in sync (relative)
+  int64_t anchor_pos;   // a position on the newest grid (two in-sync passes N apart), -1: none
+  int32_t produced;     // frames output
+  int32_t state, errors;
+  int32_t status;       // 0 ok; 1 a wait passed the deadline
+  int32_t n_msgs;
+  int32_t grid_frames, grid_fails;  // in-sync frames seen, and those that failed
+  int32_t requests, surprises, waits;
+  int32_t steps, restarts;  // walker loop turns, speculation restarts
+  int32_t diag[6];          // see Walk (ldpc_walk.hip)
+  int32_t pad;
+  int64_t wait_ticks, total_ticks;  // 100 MHz ticks spent waiting / in the walker
+};
+
+struct WalkArgs {
+  uint64_t *res;        // [2][cap] result granules: hi = (epoch << 9) | syndrome weight, lo = packed bytes
+  uint64_t *req;        // request granules: hi = epoch, lo = (position << 1) | polarity
+  uint32_t *reqd;       // [2][cap] epoch of the call that requested each window
+  uint32_t *ctl;        // kWalkCtlWords, zeroed per launch
+  uint8_t *out;         // output bytes (mo per frame)
+  uint8_t *msgs;        // message codes, in order
+  WalkSummary *sum;
+  int64_t cap;          // positions per polarity in res / reqd
+  int64_t req_cap;      // request slots
+  int64_t nin;          // samples in the span
+  int N, M, KB, mo, thr;
+  int nout;             // frames that fit the output
+  int msgs_cap;
+  int state, errors;
+  int64_t last_pass;
+  int64_t anchor;       // a position on the stream's grid, -1: none known
+  uint32_t epoch;       // 1 .. 2^23 - 1
+  int lead;             // frames the speculation may run ahead of the loop
+  uint64_t deadline;    // ticks one wait may take before the walk gives up
+};
+
+// Launch the walker (host side, ldpc_walk.hip); `blocks` workgroups of
+// kThreads (0: as many as are resident at once).  a.in is the span (elem
+// stride 1); a.max_iters / a.et_period as for launch_decode.
+int launch_walk(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, int method,
+                int prec, int slots, int nw, int blocks, void *stream);
+
 // Launch one decode (host side, implemented in ldpc_kernels.hip).
 // method: 0 min-sum, 1 sum-product, 2 bit-flip, 3 hard; prec 0 f64, 1 f32;
 // slots = ceil(E/64); nw = 1 or 4 (hard-decision words).

@@ -1,0 +1,790 @@
+// ldpc_walk.hip -- the decoder block's frame loop on the device (gfx950).
+//
+// lib/ldpc_decoder_cb_impl.cc:146-226 decodes one window per step -- the N
+// samples at the current position, times +-1 -- and a three-state machine
+// (out of sync / in sync / in sync inverted) picks the next position from the
+// window's syndrome weight.  At the reference's 5 iterations a window is a
+// few microseconds of one wave, so a host that plans launches around the
+// machine (the block's dry-run replay) spends its time in round trips: ~12
+// dependent launches per 4 096-frame call at 4 dB.  Here the machine runs
+// inside one persistent launch:
+//
+//   * wave 0 of workgroup 0 (the walker) steps the machine exactly, 64 frames
+//     or search positions per wave instruction (ballots over the window
+//     results), writes the output bytes and the sync messages;
+//   * ahead of it a speculative cursor in the same wave asks for the windows
+//     the loop will probably need -- the frames on the grid, the -tx retry
+//     where the 11th failure falls and the sample-by-sample search after it,
+//     guessing that the search lands on the same grid -- so results are
+//     usually there when the loop arrives;
+//   * every other wave of the launch decodes requested windows (the same
+//     frame decoder as the batch kernels, ldpc_frame.hpp: results are those of
+//     any other decode of the same samples) and publishes each result as one
+//     8-byte granule {tag = (epoch << 9) | syndrome weight, packed bytes};
+//   * requests are granules too; a decoder claims the next slot of its XCD's
+//     queue shard (one atomic add, eight heads) and polls it.
+// A window the loop needs that nobody asked for (a false sync's grid, a
+// search past the grid position) is requested on the spot and waited for.
+//
+// Visibility: every hand-off word is written by one agent-scope (sc1) store
+// and read by sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility, R2
+// granules); nothing else crosses workgroups.  Every wait is bounded by a
+// deadline on the 100 MHz clock: on expiry the walker reports status 1 and the
+// host redoes the call on its planner path.
+#include "ldpc_frame.hpp"
+
+namespace ldpc {
+namespace {
+
+constexpr int kWalkChunks = 4;  // 64-frame chunks one in-sync step looks at
+enum { kProgress = 0, kWait = 1, kEnd = 2 };
+
+// every access goes through global (address space 1) pointers: the sc1
+// hand-off loads must be global_, never flat_ (the pointers arrive generic)
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint8_t gu8;
+__device__ __forceinline__ uint64_t gload(const uint64_t *p) {
+  return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gstore(uint64_t *p, uint64_t v) {
+  __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t gload32(const uint32_t *p) {
+  return __hip_atomic_load((const gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gstore32(uint32_t *p, uint32_t v) {
+  __hip_atomic_store((gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ticks() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ uint64_t lowmask(int k) { return k >= 64 ? ~0ull : ((1ull << k) - 1); }
+__device__ __forceinline__ int ctz64(uint64_t x) { return x ? __builtin_ctzll(x) : 64; }
+// lane index of the n-th (1-based) set bit of x, which has at least n
+__device__ __forceinline__ int nth_bit(uint64_t x, int n) {
+  for (int i = 1; i < n; ++i) x &= x - 1;
+  return __builtin_ctzll(x);
+}
+
+// One in-sync look at 64 frames (lane k: frame k) with `err` errors so far:
+// R leading frames have results; the loss (the 11th error, :169-176) falls
+// on frame kstar if `loss`, else kstar = R; F / P: failing / passing frames
+// before kstar.
+struct SyncScan {
+  int R, kstar;
+  bool loss;
+  uint64_t F, P;
+};
+
+struct Walk {
+  const WalkArgs &w;
+  const int lane;
+  int64_t tail = 0;  // requests posted
+  // the loop, exactly
+  int64_t pos = 0;
+  int st = 0, err = 0, prod = 0;
+  bool retry = false;  // the -tx retry of a lost frame (:178-198) is pending
+  int rpol = 0;
+  int lst = 1;   // the in-sync state held last
+  int ehst = 1;  // the in-sync state held last on the anchor phase
+  int64_t last_pass = 0, anchor_pos = -1;
+  int nmsg = 0, gframes = 0, gfails = 0, surprises = 0;
+  // the speculative cursor
+  bool pon = false, pretry = false;
+  int64_t pp = 0, pg = 0;
+  int pst = 0, perr = 0, prpol = 0, hst = 1, pgpol = 0, restarts = 0;
+  // guess ring: record i in lane i & 63 (loss frame, guessed landing, state)
+  int64_t gLp = 0, gland = 0;
+  int gst = 0;
+  int gh = 0, gt = 0;  // oldest unverified guess, next free
+  // diagnostics: surprises at a grid frame / in a search / at a retry,
+  // guesses, wrong guesses, restarts because the loop got ahead
+  int d_sync = 0, d_out = 0, d_retry = 0, d_guess = 0, d_wrong = 0, d_behind = 0;
+
+  __device__ Walk(const WalkArgs &a, int l) : w(a), lane(l) {}
+
+  __device__ bool ready(uint64_t g) const { return (uint32_t)(g >> 41) == w.epoch; }
+  __device__ static int synd(uint64_t g) { return (int)((g >> 32) & 511u); }
+  __device__ const uint64_t *res(int pol) const { return w.res + (int64_t)pol * w.cap; }
+  __device__ bool fits(int64_t p) const { return p >= 0 && p + w.N <= w.nin; }
+
+  // ask for window (p, pol) in every lane where `act` (p may differ per
+  // lane); windows asked for before in this call are skipped
+  __device__ void request(int64_t p, int pol, bool act) {
+    act = act && fits(p);
+    gu32 *rd = (gu32 *)(w.reqd + (int64_t)pol * w.cap);
+    const uint32_t e = act ? rd[p] : w.epoch;
+    const bool fresh = act && e != w.epoch;
+    const uint64_t m = __ballot(fresh);
+    if (!m) return;
+    if (fresh) {
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      rd[p] = w.epoch;
+      gstore(w.req + tail + below, ((uint64_t)w.epoch << 32) | (uint32_t)((p << 1) | pol));
+    }
+    tail += __popcll(m);
+  }
+  // the same for windows nobody can have asked for yet (the grid beyond pg):
+  // marked, posted, no look-up (a duplicate would only decode twice)
+  __device__ void request_new(int64_t p, int pol, bool act) {
+    act = act && fits(p);
+    const uint64_t m = __ballot(act);
+    if (!m) return;
+    if (act) {
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      ((gu32 *)(w.reqd + (int64_t)pol * w.cap))[p] = w.epoch;
+      gstore(w.req + tail + below, ((uint64_t)w.epoch << 32) | (uint32_t)((p << 1) | pol));
+    }
+    tail += __popcll(m);
+  }
+  __device__ bool requested(int64_t p, int pol) const {
+    return ((const gu32 *)w.reqd)[(int64_t)pol * w.cap + p] == w.epoch;
+  }
+  // the search positions a + 1 .. z after a lost frame at a, both
+  // polarities (one look-up round for both)
+  __device__ void search(int64_t a, int64_t z) {
+    for (int64_t q0 = a + 1; q0 <= z; q0 += 64) {
+      const int64_t q = q0 + lane;
+      const bool act = q <= z && fits(q);
+      gu32 *rd0 = (gu32 *)w.reqd, *rd1 = (gu32 *)(w.reqd + w.cap);
+      const uint32_t e0 = act ? rd0[q] : w.epoch, e1 = act ? rd1[q] : w.epoch;
+      const bool f0 = act && e0 != w.epoch, f1 = act && e1 != w.epoch;
+      const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
+      const uint32_t b0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+      const uint32_t b1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+      if (f0) {
+        rd0[q] = w.epoch;
+        gstore(w.req + tail + b0, ((uint64_t)w.epoch << 32) | (uint32_t)(q << 1));
+      }
+      if (f1) {
+        rd1[q] = w.epoch;
+        gstore(w.req + tail + __popcll(m0) + b1,
+               ((uint64_t)w.epoch << 32) | (uint32_t)((q << 1) | 1));
+      }
+      tail += __popcll(m0) + __popcll(m1);
+    }
+  }
+  __device__ void request_search(int64_t a) { search(a, a + w.N); }
+  // a position on the stream's grid (this call's newest, else the caller's), -1: none
+  __device__ int64_t anchor() const { return anchor_pos >= 0 ? anchor_pos : w.anchor; }
+
+  __device__ void msg(int code) {
+    if (lane == 0) ((gu8 *)w.msgs)[nmsg] = (uint8_t)code;
+    ++nmsg;
+  }
+  // output frame prod + k (:207-219, bytes built by the decoder)
+  __device__ void put(int k, uint32_t packed, bool act) {
+    if (!act) return;
+    gu8 *o = (gu8 *)w.out + (int64_t)(prod + k) * w.mo;
+    if (w.mo == 4) {
+      *(gu32 *)o = packed;
+    } else {
+      for (int b = 0; b < w.mo; ++b) o[b] = (uint8_t)(packed >> (8 * b));
+    }
+  }
+
+  __device__ SyncScan scan_sync(uint64_t g, bool val, int e) const {
+    const bool rdy = val && ready(g);
+    SyncScan s;
+    s.R = ctz64(~__ballot(rdy));
+    const bool fail = rdy && synd(g) > w.thr;  // checkFrame > M/8 (:166)
+    const uint64_t F = __ballot(fail) & lowmask(s.R);
+    const int need = 11 - e;
+    s.loss = __popcll(F) >= need;
+    s.kstar = s.loss ? nth_bit(F, need) : s.R;
+    s.F = F & lowmask(s.kstar);
+    s.P = __ballot(rdy && !fail) & lowmask(s.kstar);
+    return s;
+  }
+
+  // -- surprises: windows the loop needs and nobody asked for ---------------
+  __device__ void surprise_sync(int pol) {
+    // a grid the speculation did not follow (a false sync): its frames until
+    // 11 of them fail, the retries where the 11th may fall, the search after
+    ++surprises;
+    ++d_sync;
+    const int64_t N = w.N;
+    request(pos + lane * N, pol, lane < 16);
+    const int need = 11 - err;
+    request(pos + (int64_t)(need - 1 + lane) * N, pol ^ 1, lane < 3);
+    request_search(pos + (int64_t)(need - 1) * N);
+  }
+  __device__ void surprise_out() {
+    ++surprises;
+    ++d_out;
+    request(pos + lane, 0, true);
+    request(pos + lane, 1, true);
+  }
+
+  // -- the loop ---------------------------------------------------------------
+  __device__ int e_sync() {
+    const int pol = st == 2;
+    const int64_t N = w.N;
+    {
+      const int64_t A = anchor();
+      if (A < 0 || (pos - A) % N == 0) ehst = st;
+    }
+    uint64_t g[kWalkChunks];
+    bool val[kWalkChunks];
+#pragma unroll
+    for (int c = 0; c < kWalkChunks; ++c) {
+      const int k = 64 * c + lane;
+      const int64_t f = pos + (int64_t)k * N;
+      val[c] = f + N <= w.nin && prod + k < w.nout;  // :146-147
+      g[c] = val[c] ? gload(res(pol) + f) : 0ull;
+    }
+    bool moved = false;
+#pragma unroll
+    for (int c = 0; c < kWalkChunks; ++c) {
+      if (!__ballot(val[c])) return moved ? kProgress : kEnd;
+      const SyncScan s = scan_sync(g[c], val[c], err);
+      if (s.R == 0) {
+        if (!moved && !requested(pos, pol)) surprise_sync(pol);
+        return moved ? kProgress : kWait;
+      }
+      put(lane, (uint32_t)g[c], lane < s.kstar);
+      if (s.P) {  // two passes N apart in sync: their phase is the stream's grid
+        if ((s.P & (s.P << 1)) || ((s.P & 1) && last_pass == pos - N)) anchor_pos = pos;
+        last_pass = pos + (int64_t)(63 - __builtin_clzll(s.P)) * N;
+      }
+      gframes += s.kstar + (s.loss ? 1 : 0);
+      gfails += __popcll(s.F) + (s.loss ? 1 : 0);
+      err += __popcll(s.F);
+      prod += s.kstar;
+      pos += (int64_t)s.kstar * N;
+      moved = true;
+      if (s.loss) {  // :169-176; the -tx retry of this frame follows (e_retry)
+        lst = st;
+        msg(kWalkMsgLost);
+        err = 0;
+        st = 0;
+        retry = true;
+        rpol = pol ^ 1;
+        return kProgress;
+      }
+      if (s.R < 64) return kProgress;
+    }
+    return kProgress;
+  }
+
+  __device__ int e_retry() {  // :178-198 for the frame at pos
+    const uint64_t g = gload(res(rpol) + pos);
+    if (!ready(g)) {
+      if (!requested(pos, rpol)) {
+        ++surprises;
+        ++d_retry;
+        request(pos, rpol, lane == 0);
+      }
+      return kWait;
+    }
+    retry = false;
+    if (synd(g) <= w.thr) {
+      msg(kWalkMsgInverted);
+      st = 2;
+      err = 0;
+      put(0, (uint32_t)g, lane == 0);
+      ++prod;
+      pos += w.N;
+    } else {
+      pos += 1;
+    }
+    return kProgress;
+  }
+
+  __device__ int e_out() {  // out of sync: the search, one sample per step
+    const int64_t q = pos + lane;
+    const bool val = fits(q);
+    const uint64_t vm = __ballot(val);
+    if (!vm) return kEnd;
+    const uint64_t g0 = val ? gload(res(0) + q) : 0ull;
+    const uint64_t g1 = val ? gload(res(1) + q) : 0ull;
+    const bool r0 = ready(g0), r1 = ready(g1);
+    const bool p0 = r0 && synd(g0) <= w.thr, p1 = r1 && synd(g1) <= w.thr;
+    const bool known = val && (p0 || (r0 && r1));
+    const int D = ctz64(~__ballot(known));
+    const uint64_t hit = __ballot(known && (p0 || p1)) & lowmask(D);
+    if (hit) {
+      const int j = ctz64(hit);
+      const bool via0 = (__ballot(p0) >> j) & 1;
+      const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(via0 ? g0 : g1), j);
+      pos += j;
+      msg(via0 ? kWalkMsgSync : kWalkMsgInverted);  // :201-205 / :187-190
+      st = via0 ? 1 : 2;
+      err = 0;
+      put(0, pk, lane == 0);
+      ++prod;
+      pos += w.N;
+      return kProgress;
+    }
+    pos += D;
+    if (D < __popcll(vm)) {
+      if (!requested(pos, 0) || !requested(pos, 1)) surprise_out();
+      return D ? kProgress : kWait;
+    }
+    return kProgress;
+  }
+
+  // -- speculation ------------------------------------------------------------
+  // A second cursor (pp, pst, perr, pretry) runs the same loop ahead of the
+  // exact one and asks for the windows it touches.  Where a result it needs
+  // is not there yet it guesses instead of waiting, logs the guess (one
+  // record per lane of a 64-entry ring) and goes on:
+  //   S (search): the -tx retry of a lost frame fails (if it is pending) and
+  //     the search after it lands on the stream's grid -- the next position
+  //     of the anchor phase, else N samples on -- in the home state (the
+  //     state last held on that grid);
+  //   F (false grid): in sync off the anchor phase (after a false sync, which
+  //     most searches meet: a misaligned window passes ~1 % of the time and a
+  //     search tries ~126), every frame fails until the 11th error.
+  // Each step checks the oldest guesses against the results once they are in;
+  // a wrong one rolls the cursor back to the truth at that point and drops
+  // the later guesses.  So the cursor follows the loop's real path and asks
+  // for a false sync's whole detour (its frames, the retry, the search back)
+  // in one go, and the loop rarely finds a window nobody asked for.
+  // Frames of the home grid are asked for up to `lead` frames ahead (pg: the
+  // next one not asked for).
+  __device__ void p_set(int64_t p, int s_, int e_, bool rt, int rp) {
+    pp = p;
+    pst = s_;
+    perr = e_;
+    pretry = rt;
+    prpol = rp;
+    gt = gh;  // later guesses are void
+  }
+  __device__ void p_restart() {
+    pon = true;
+    ++restarts;
+    gh = gt = 0;
+    p_set(pos, st, err, retry, rpol);
+    hst = ehst;
+  }
+  __device__ void p_log(int64_t a, int64_t b, int bits) {
+    if (lane == (gt & 63)) {
+      gLp = a;
+      gland = b;
+      gst = bits;
+    }
+    ++gt;
+    ++d_guess;
+  }
+  // true: the oldest guess was settled (right, or rolled back)
+  __device__ bool p_verify() {
+    if (gh == gt) return false;
+    const int slot = gh & 63;
+    const int64_t a = ((int64_t)__builtin_amdgcn_readlane((int)(gLp >> 32), slot) << 32) |
+                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gLp, slot);
+    const int64_t z = ((int64_t)__builtin_amdgcn_readlane((int)(gland >> 32), slot) << 32) |
+                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gland, slot);
+    const int gw = __builtin_amdgcn_readlane(gst, slot);
+    const int64_t N = w.N;
+    if (gw & 16) {  // F: frames a, a + N, .. z at polarity, all failing
+      const int pol = (gw >> 3) & 1;
+      const int64_t f = a + (int64_t)lane * N;
+      const bool val = f <= z;
+      const uint64_t g = val ? gload(res(pol) + f) : 0ull;
+      const bool rdy = ready(g);
+      if (__ballot(val && !rdy)) return false;  // not all in yet
+      if (!__ballot(val && synd(g) <= w.thr)) {
+        ++gh;
+        return true;
+      }
+      ++d_wrong;  // one passes: back to the start, where the cursor now reads them
+      p_set(a, pol + 1, (gw >> 8) & 15, false, 0);
+      return true;
+    }
+    // S: retry at a (if pending), then the search a + 1 .. z
+    const int gs = gw & 3;           // guessed state after the landing
+    const bool has_retry = gw & 4;
+    const int rp = (gw >> 3) & 1;    // the retry's polarity
+    const uint64_t gr = has_retry ? gload(res(rp) + a) : 0ull;
+    const int64_t q = a + 1 + lane;
+    const bool val = q <= z;
+    const uint64_t g0 = val ? gload(res(0) + q) : 0ull;
+    const uint64_t g1 = val ? gload(res(1) + q) : 0ull;
+    if (has_retry) {
+      if (!ready(gr)) return false;
+      if (synd(gr) <= w.thr) {  // the retry passes: in sync inverted at a
+        ++d_wrong;
+        p_set(a + N, 2, 0, false, 0);
+        return true;
+      }
+    }
+    const bool r0 = ready(g0), r1 = ready(g1);
+    const bool p0 = r0 && synd(g0) <= w.thr, p1 = r1 && synd(g1) <= w.thr;
+    const bool known = val && (p0 || (r0 && r1));
+    const uint64_t vm = __ballot(val);
+    const int D = ctz64(~__ballot(known));
+    const uint64_t hit = __ballot(known && (p0 || p1)) & lowmask(D);
+    if (hit) {
+      const int j = ctz64(hit);
+      const int s1 = ((__ballot(p0) >> j) & 1) ? 1 : 2;
+      if (a + 1 + j == z && s1 == gs) {
+        ++gh;  // right
+        return true;
+      }
+      ++d_wrong;
+      p_set(a + 1 + j + N, s1, 0, false, 0);  // a false sync, or another state
+      return true;
+    }
+    if (D < __popcll(vm)) return false;  // not all in yet
+    ++d_wrong;
+    p_set(z + 1, 0, 0, false, 0);  // nothing passed up to the guessed landing
+    return true;
+  }
+  // guess S from the loss at Lp (retry pending at polarity rp if has_retry)
+  __device__ void p_guess(int64_t Lp, bool has_retry, int rp) {
+    const int64_t N = w.N, A = anchor();
+    const int64_t land = A >= 0 ? Lp + 1 + (((A - Lp - 1) % N) + N) % N : Lp + N;
+    if (has_retry) request(Lp, rp, lane == 0);
+    search(Lp, land);
+    p_log(Lp, land, hst | (has_retry ? 4 : 0) | (rp << 3));
+    pp = land;  // in sync from the landing frame on (it passes: the scan sees so)
+    pst = hst;
+    perr = 0;
+    pretry = false;
+  }
+  __device__ void p_step() {
+    if (pon && pp < pos) ++d_behind;
+    if (!pon || pp < pos) p_restart();
+    for (int v = 0; v < 4 && p_verify(); ++v) {
+    }
+    if (pp < pos) {
+      ++d_behind;
+      p_restart();
+    }
+    const int64_t N = w.N;
+    const int64_t limit = pos + (int64_t)w.lead * N;
+    // several losses per step: the loop takes about three steps per loss
+    for (int it = 0; it < 8; ++it) {
+      if (pp >= limit || gt - gh >= 62) return;
+      if (pretry) {
+        const uint64_t g = gload(res(prpol) + pp);
+        if (!ready(g)) {
+          p_guess(pp, true, prpol);
+          continue;
+        }
+        pretry = false;
+        if (synd(g) <= w.thr) {
+          pst = 2;
+          perr = 0;
+          pp += N;
+        } else {
+          p_guess(pp, false, 0);
+        }
+        continue;
+      }
+      if (!pst) {
+        // out of sync (a restart in the loop's search, or a wrong landing)
+        if (!fits(pp)) return;
+        p_guess(pp - 1, false, 0);
+        continue;
+      }
+      const int pol = pst == 2;
+      const int64_t A = anchor();
+      const bool home = A < 0 || (pp - A) % N == 0;
+      uint64_t g[kWalkChunks];
+      bool val[kWalkChunks];
+      if (home) {
+        hst = pst;
+        // the grid ahead (pg counts for one phase and polarity)
+        if (pg < pp || (pg - pp) % N != 0 || pgpol != pol) {
+          pg = pp;
+          pgpol = pol;
+        }
+#pragma unroll
+        for (int c = 0; c < kWalkChunks; ++c) {
+          if (pg >= limit) break;
+          const int64_t f = pg + (int64_t)lane * N;
+          request_new(f, pol, f < limit);
+          pg += 64 * N;
+        }
+#pragma unroll
+        for (int c = 0; c < kWalkChunks; ++c) {
+          const int64_t f = pp + (int64_t)(64 * c + lane) * N;
+          val[c] = fits(f);
+          g[c] = val[c] ? gload(res(pol) + f) : 0ull;
+        }
+      } else {
+        // a false grid: its frames up to the 11th error; guess F if they are
+        // not all in, else read them like any other
+        const int need = 11 - perr;
+        const int64_t f = pp + (int64_t)lane * N;
+        const bool in = lane < need && fits(f);
+        request(f, pol, in);
+        const uint64_t gf = in ? gload(res(pol) + f) : 0ull;
+        if (__ballot(in && !ready(gf))) {
+          const int64_t Lf = pp + (int64_t)(need - 1) * N;
+          if (!fits(Lf)) return;
+          p_log(pp, Lf, 16 | (pol << 3) | (perr << 8));
+          pp = Lf;  // the 11th error: the retry next
+          perr = 0;
+          pretry = true;
+          prpol = pol ^ 1;
+          pst = 0;
+          continue;
+        }
+        val[0] = lane < need && fits(f);
+        g[0] = gf;
+#pragma unroll
+        for (int c = 1; c < kWalkChunks; ++c) {
+          val[c] = false;
+          g[c] = 0ull;
+        }
+      }
+      bool lost = false;
+#pragma unroll
+      for (int c = 0; c < kWalkChunks; ++c) {
+        if (!__ballot(val[c])) return;
+        const SyncScan sc = scan_sync(g[c], val[c], perr);
+        perr += __popcll(sc.F);
+        pp += (int64_t)sc.kstar * N;
+        if (sc.loss) {  // the 11th failure: the retry next
+          perr = 0;
+          pretry = true;
+          prpol = pol ^ 1;
+          pst = 0;
+          lost = true;
+          break;
+        }
+        if (sc.R < 64) return;
+      }
+      if (!lost) return;
+    }
+  }
+};
+
+__device__ __forceinline__ void walker_run(const WalkArgs &w) {
+  const int lane = threadIdx.x & 63;
+  Walk k(w, lane);
+  k.st = w.state;
+  k.err = w.errors;
+  k.last_pass = w.last_pass;
+  const uint64_t t0 = ticks();
+  uint64_t t_last = t0, t_moved = t0, wait_ticks = 0;
+  int status = 0, waits = 0, steps = 0;
+  for (;; ++steps) {
+    if (!k.retry && (w.nin - k.pos < w.N || k.prod >= w.nout || k.nmsg + 2 > w.msgs_cap)) break;
+    int r = kProgress;
+    for (int e = 0; e < 4 && r == kProgress; ++e) {
+      if (!k.retry && (w.nin - k.pos < w.N || k.prod >= w.nout || k.nmsg + 2 > w.msgs_cap)) {
+        r = kEnd;
+        break;
+      }
+      r = k.retry ? k.e_retry() : (k.st ? k.e_sync() : k.e_out());
+    }
+    if (r == kEnd && !k.retry) break;
+    k.p_step();
+    const uint64_t t = ticks();
+    if (r == kWait) {
+      ++waits;
+      wait_ticks += t - t_last;
+      if (t - t_moved > w.deadline) {
+        status = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    } else {
+      t_moved = t;
+    }
+    t_last = t;
+  }
+  if (lane == 0) {
+    __attribute__((address_space(1))) WalkSummary *s =
+        (__attribute__((address_space(1))) WalkSummary *)w.sum;
+    s->consumed = k.pos;
+    s->last_pass = k.last_pass;
+    s->anchor_pos = k.anchor_pos;
+    s->produced = k.prod;
+    s->state = k.st;
+    s->errors = k.err;
+    s->status = status;
+    s->n_msgs = k.nmsg;
+    s->grid_frames = k.gframes;
+    s->grid_fails = k.gfails;
+    s->requests = (int32_t)k.tail;
+    s->surprises = k.surprises;
+    s->waits = waits;
+    s->steps = steps;
+    s->restarts = k.restarts;
+    s->diag[0] = k.d_sync;
+    s->diag[1] = k.d_out;
+    s->diag[2] = k.d_retry;
+    s->diag[3] = k.d_guess;
+    s->diag[4] = k.d_wrong;
+    s->diag[5] = k.d_behind;
+    s->wait_ticks = (int64_t)wait_ticks;
+    s->total_ticks = (int64_t)(ticks() - t0);
+    gstore32(w.ctl + kWalkDone, 1u);
+  }
+}
+
+// Workgroup 0: the walker (wave 0; its other waves leave).  Every other wave:
+// a decoder pulling requests until the walker is done.
+template <int PREC, int METHOD, int S, int NW, int DCN, int DVN>
+__global__ void __launch_bounds__(kThreads, 1)
+    walk_small_kernel(CodeView code, DecodeArgs a, WalkArgs w) {
+  typedef typename Math<PREC>::Real Real;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
+  if constexpr (METHOD == 1) stage_tab<PREC>(logtab);
+  if (blockIdx.x == 0) {
+    if (wave == 0) walker_run(w);
+    return;
+  }
+  WaveTables<S, NW> wt;
+  Real *tb, *eb, *rb, *sb;
+  int colq[NW];
+  uint32_t ppos[2];
+  wave_setup<PREC, METHOD, S, NW, DCN, DVN>(code, smem, wave, lane, wt, tb, eb, rb, sb, colq, ppos);
+  // the queue shard of this wave's XCD (speed only: any shard is correct)
+  const uint32_t x = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;
+  uint64_t idle = ticks();
+  for (;;) {
+    uint32_t c = 0;
+    if (lane == 0)
+      c = __hip_atomic_fetch_add((gu32 *)(w.ctl + 32 * x), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+    const int64_t i = (int64_t)c * 8 + x;
+    uint32_t key = 0;
+    for (int spins = 0;; ++spins) {
+      const uint64_t g = i < w.req_cap ? gload(w.req + i) : 0ull;
+      if ((uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) == w.epoch) {
+        key = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+        break;
+      }
+      if ((spins & 7) == 7 && (gload32(w.ctl + kWalkDone) != 0u || ticks() - idle > w.deadline))
+        return;
+      if (spins < 8)
+        __builtin_amdgcn_s_sleep(1);
+      else
+        __builtin_amdgcn_s_sleep(4);
+    }
+    // window key: the N samples from position key >> 1, negated when key & 1
+    const int64_t p = key >> 1;
+    const float sgn = (key & 1) ? -1.0f : 1.0f;
+    const __attribute__((address_space(1))) float *src =
+        (const __attribute__((address_space(1))) float *)a.in + p;
+    float xin[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) xin[q] = colq[q] >= 0 ? src[colq[q]] * sgn : 0.0f;
+    FrameResult r;
+    if constexpr (METHOD == 1) {
+      bool bad = false;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) bad |= !__builtin_isfinite(xin[q]);
+      if (__ballot(bad) == 0)
+        r = decode_frame<PREC, METHOD, S, NW, DCN, DVN, true, Real, false>(
+            code, a, 0, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
+      else
+        r = decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, false>(
+            code, a, 0, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
+    } else {
+      r = decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, false>(
+          code, a, 0, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
+    }
+    uint32_t pk = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      pk |= ((uint32_t)__builtin_amdgcn_readlane((int)r.byte, j) & 255u) << (8 * j);
+    const uint64_t out = ((uint64_t)((w.epoch << 9) | (uint32_t)r.weight) << 32) | pk;
+    if (lane == 0) gstore(w.res + (int64_t)(key & 1) * w.cap + p, out);
+    idle = ticks();
+  }
+}
+
+int cus_now() {
+  static int cus_of[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus_of[dev] &&
+      hipDeviceGetAttribute(&cus_of[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus_of[dev] = 256;
+  return cus_of[dev];
+}
+
+template <int PREC, int METHOD, int S, int NW, int DCN, int DVN>
+int launch_w(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, int blocks,
+             hipStream_t st) {
+  typedef typename Math<PREC>::Real Real;
+  const size_t lds = Layout<Real, METHOD, S, NW, DVN>::total;
+  const void *fn = (const void *)walk_small_kernel<PREC, METHOD, S, NW, DCN, DVN>;
+  static int per_cu = 0;  // resident workgroups per CU (all of them run at once)
+  if (!per_cu) {
+    // one workgroup per CU by default (LDPC_WALK_BLOCKS_PER_CU): ~1 000
+    // decoder waves serve the walk's requests, and the walker's CU is shared
+    // with one other workgroup at most
+    if (lds > 65536 &&
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return -3;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, lds) != hipSuccess || n < 1)
+      n = 1;
+    per_cu = n;
+  }
+  const char *e = getenv("LDPC_WALK_BLOCKS_PER_CU");
+  if (blocks <= 0) blocks = std::min(per_cu, e ? std::max(atoi(e), 1) : 1) * cus_now();
+  hipLaunchKernelGGL((walk_small_kernel<PREC, METHOD, S, NW, DCN, DVN>), dim3((unsigned)blocks),
+                     dim3(kThreads), lds, st, code, a, w);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <int PREC, int METHOD, int NW>
+int walk_slots(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, int slots, int blocks,
+               hipStream_t st) {
+  if constexpr (NW == 1 && METHOD <= 1) {
+    if (code.dc_max <= 6 && code.dv_max <= 3) switch (slots) {
+        case 1: return launch_w<PREC, METHOD, 1, NW, 5, 3>(code, a, w, blocks, st);
+        case 2: return launch_w<PREC, METHOD, 2, NW, 5, 3>(code, a, w, blocks, st);
+        case 3: return launch_w<PREC, METHOD, 3, NW, 5, 3>(code, a, w, blocks, st);
+        case 4: return launch_w<PREC, METHOD, 4, NW, 5, 3>(code, a, w, blocks, st);
+        default: break;
+      }
+  }
+  constexpr int D = kDcMax - 1, V = kDvMax;
+  switch (slots) {
+    case 1: return launch_w<PREC, METHOD, 1, NW, D, V>(code, a, w, blocks, st);
+    case 2: return launch_w<PREC, METHOD, 2, NW, D, V>(code, a, w, blocks, st);
+    case 3: return launch_w<PREC, METHOD, 3, NW, D, V>(code, a, w, blocks, st);
+    case 4: return launch_w<PREC, METHOD, 4, NW, D, V>(code, a, w, blocks, st);
+    case 5: return launch_w<PREC, METHOD, 5, NW, D, V>(code, a, w, blocks, st);
+    case 6: return launch_w<PREC, METHOD, 6, NW, D, V>(code, a, w, blocks, st);
+    case 7: return launch_w<PREC, METHOD, 7, NW, D, V>(code, a, w, blocks, st);
+    case 8: return launch_w<PREC, METHOD, 8, NW, D, V>(code, a, w, blocks, st);
+    default: return -2;
+  }
+}
+
+template <int NW>
+int walk_nw(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, int method, int prec,
+            int slots, int blocks, hipStream_t st) {
+  constexpr int D = kDcMax - 1, V = kDvMax;
+  if (method == 3) return launch_w<1, 3, 1, NW, D, V>(code, a, w, blocks, st);
+  if (method == 2) return launch_w<1, 2, 1, NW, D, V>(code, a, w, blocks, st);
+  if (method == 1) {
+    if (prec == 1) return walk_slots<1, 1, NW>(code, a, w, slots, blocks, st);
+    if (prec == 2) return walk_slots<2, 1, NW>(code, a, w, slots, blocks, st);
+    if (prec == 3) return walk_slots<3, 1, NW>(code, a, w, slots, blocks, st);
+    return walk_slots<0, 1, NW>(code, a, w, slots, blocks, st);
+  }
+  return prec == 1 ? walk_slots<1, 0, NW>(code, a, w, slots, blocks, st)
+                   : walk_slots<0, 0, NW>(code, a, w, slots, blocks, st);
+}
+
+}  // namespace
+
+int launch_walk(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, int method,
+                int prec, int slots, int nw, int blocks, void *stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (w.KB > 4 || w.mo > 4 || w.epoch == 0 || w.epoch >= (1u << 23)) return -2;
+  if (nw == 1) return walk_nw<1>(code, a, w, method, prec, slots, blocks, st);
+  if (nw == 4) return walk_nw<4>(code, a, w, method, prec, slots, blocks, st);
+  return -2;
+}
+
+}  // namespace ldpc
