@@ -60,7 +60,7 @@ struct ldpc_ctx {
   int64_t *h_win = nullptr;
   size_t h_win_bytes = 0;
   int64_t span_samples = 0;
-  // ldpc_walk_span (ldpc_walk.hip): [ctl | res | reqd | req] on the device,
+  // ldpc_walk_span (ldpc_walk.hip): [ctl | res | req] on the device,
   // zeroed when (re)allocated and when the epoch wraps; summary, messages and
   // output bytes in mapped pinned memory the walker writes directly
   void *d_walk = nullptr;
@@ -1449,14 +1449,15 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
 }
 
 // The walker's buffers for spans of up to `cap` positions (ldpc_walk_span).
-constexpr int64_t kWalkReqSlack = 16384;  // request slots decoders may claim past the last request
+// request slots: each window is asked for at most once (2 per position);
+// decoders claim up to kWalkClaimSlack slots past the last request
 size_t walk_layout(int64_t cap, size_t off[4]) {
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   off[0] = 0;                                                       // ctl
   off[1] = al((size_t)ldpc::kWalkCtlWords * 4);                     // res
-  off[2] = off[1] + al((size_t)2 * cap * 8);                        // reqd
-  off[3] = off[2] + al((size_t)2 * cap * 4);                        // req
-  return off[3] + al((size_t)(2 * cap + kWalkReqSlack) * 8);
+  off[2] = off[1] + al((size_t)2 * cap * 8);                        // req
+  off[3] = off[2];
+  return off[2] + al((size_t)(2 * cap + ldpc::kWalkClaimSlack) * 8);
 }
 
 int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, const float *in,
@@ -1473,7 +1474,10 @@ int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, cons
     return set_err(ctx, LDPC_EINVAL, "bad walk buffers");
   if (io->state < 0 || io->state > 2 || io->errors < 0 || io->errors > 10)
     return set_err(ctx, LDPC_EINVAL, "walk state out of range");
-  const int64_t S = (n_in_floats + elem_stride - 1) / elem_stride;
+  // one walk takes at most kWalkMaxSpan samples (the walker's bitmap); the
+  // loop's state carries over to the next call as the reference's does
+  const int64_t S = std::min<int64_t>((n_in_floats + elem_stride - 1) / elem_stride,
+                                      ldpc::kWalkMaxSpan);
   const int nout = noutput_bytes / mo;
   const int64_t anchor_in = io->anchor_pos;
   io->consumed = 0;
@@ -1483,10 +1487,13 @@ int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, cons
   io->grid_frames = io->grid_fails = io->requests = io->surprises = io->steps = io->restarts = 0;
   io->walk_us = io->wait_us = 0.0;
   if (S < N || nout == 0 || msgs_cap < 2) return LDPC_OK;  // the loop would not run (:146-147)
-  if (S >= ((int64_t)1 << 30)) return set_err(ctx, LDPC_EINVAL, "span too long for one walk");
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  const auto tnow = []() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  const double t0 = tnow();
   // the span, as for ldpc_decode_windows
   rc = ensure_window_stage(ctx, al((size_t)S * 4));
   if (rc != LDPC_OK) return rc;
@@ -1543,13 +1550,12 @@ int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, cons
   ldpc::WalkArgs w{};
   w.ctl = (uint32_t *)(base + off[0]);
   w.res = (uint64_t *)(base + off[1]);
-  w.reqd = (uint32_t *)(base + off[2]);
-  w.req = (uint64_t *)(base + off[3]);
+  w.req = (uint64_t *)(base + off[2]);
   w.sum = (ldpc::WalkSummary *)dh;
   w.msgs = (uint8_t *)dh + al(sizeof(ldpc::WalkSummary));
   w.out = w.msgs + al((size_t)msgs_cap);
   w.cap = ctx->walk_cap;
-  w.req_cap = 2 * ctx->walk_cap + kWalkReqSlack;
+  w.req_cap = 2 * ctx->walk_cap + ldpc::kWalkClaimSlack;
   w.nin = S;
   w.N = N;
   w.M = ctx->M;
@@ -1568,6 +1574,13 @@ int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, cons
       getenv("LDPC_WALK_DEADLINE_MS") ? atof(getenv("LDPC_WALK_DEADLINE_MS")) : 200.0;
   w.lead = std::max(lead, 1);
   w.deadline = (uint64_t)(deadline_ms * 1e5);  // 100 MHz ticks
+  // LDPC_WALK_TRACE=2: event records of each walk into LDPC_WALK_TRACE_FILE
+  static uint64_t *d_trace = nullptr;
+  const bool tracing = getenv("LDPC_WALK_TRACE") && getenv("LDPC_WALK_TRACE")[0] == '2';
+  const int trace_cap = 1 << 16;
+  if (tracing && !d_trace && hipMalloc(&d_trace, (size_t)trace_cap * 32) != hipSuccess) d_trace = nullptr;
+  w.trace = tracing ? d_trace : nullptr;
+  w.trace_cap = trace_cap;
   ldpc::DecodeArgs a{};
   a.in = (const float *)ctx->d_wstage;
   a.cw_stride = N;
@@ -1576,12 +1589,15 @@ int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, cons
   a.max_iters = max_iters;
   a.et_period = 1;
   a.fair_cycles = 0;
+  const double t1 = tnow();
   const int lr = ldpc::launch_walk(code_view(ctx), a, w, method, precision, ctx->slots, ctx->nw, 0,
                                    ctx->stream);
+  const double t2 = tnow();
   if (lr == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no walk kernel for this code shape");
   if (lr != 0) return hip_err(ctx, hipGetLastError(), "walk launch");
   if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
     return hip_err(ctx, e, "hipStreamSynchronize(walk)");
+  const double t3 = tnow();
   const ldpc::WalkSummary &sm = *(const ldpc::WalkSummary *)ctx->h_walk;
   io->walk_us = (double)sm.total_ticks * 1e-2;
   io->wait_us = (double)sm.wait_ticks * 1e-2;
@@ -1589,13 +1605,33 @@ int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, cons
   io->surprises = sm.surprises;
   io->steps = sm.steps;
   io->restarts = sm.restarts;
+  if (tracing && d_trace) {
+    std::vector<uint64_t> h((size_t)trace_cap * 4);
+    if (hipMemcpy(h.data(), d_trace, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      const char *fn = getenv("LDPC_WALK_TRACE_FILE") ? getenv("LDPC_WALK_TRACE_FILE") : "walk_trace.bin";
+      if (FILE *f = fopen(fn, "ab")) {
+        const uint64_t hdr[4] = {~0ull, (uint64_t)sm.steps, (uint64_t)sm.total_ticks, 0};
+        fwrite(hdr, 8, 4, f);
+        // records up to the first unwritten one (zero first word)
+        size_t n = 0;
+        while (n < (size_t)trace_cap && h[n * 4] != 0) ++n;
+        fwrite(h.data(), 8, n * 4, f);
+        fclose(f);
+      }
+    }
+    (void)hipMemset(d_trace, 0, (size_t)trace_cap * 32);
+  }
   if (getenv("LDPC_WALK_TRACE"))
     fprintf(stderr,
             "walk: %.1f us (waiting %.1f), %d steps, %d windows; surprises sync %d search %d retry "
-            "%d; guesses %d (%d wrong); restarts %d (%d behind)\n",
+            "%d; guesses %d (%d wrong); restarts %d (%d behind); host: stage %.1f launch %.1f "
+            "wait %.1f us\n",
             io->walk_us, io->wait_us, sm.steps, sm.requests, sm.diag[0], sm.diag[1], sm.diag[2],
-            sm.diag[3], sm.diag[4], sm.restarts, sm.diag[5]);
-  if (sm.status != 0) return set_err(ctx, LDPC_ETIMEOUT, "a wait of the walk passed its deadline");
+            sm.diag[3], sm.diag[4], sm.restarts, sm.diag[5], 1e6 * (t1 - t0), 1e6 * (t2 - t1),
+            1e6 * (t3 - t2));
+  if (sm.status != 0)
+    return set_err(ctx, LDPC_ETIMEOUT, sm.status == 2 ? "the walk's request queue ran out"
+                                                      : "a wait of the walk passed its deadline");
   io->state = sm.state;
   io->errors = sm.errors;
   io->last_pass = sm.last_pass;

@@ -119,7 +119,10 @@ struct DecodeArgs {
 // loads (MI355X_MICROARCH.md, inter-workgroup visibility, R2).
 // ---------------------------------------------------------------------------
 constexpr int kWalkDone = 256;  // ctl word set when the walker has finished
-constexpr int kWalkCtlWords = 272;  // zeroed per launch: 8 queue heads (one per 128 B) + done
+constexpr int kWalkCtlWords = 272;
+constexpr int64_t kWalkClaimSlack = 16384;  // request slots past the walker's last one
+constexpr int kWalkLdsBytes = 96 << 10;     // the walker's bitmap of windows asked for
+constexpr int64_t kWalkMaxSpan = (int64_t)kWalkLdsBytes * 4;  // samples per walk (2 bits each)  // zeroed per launch: 8 queue heads (one per 128 B) + done
 enum { kWalkMsgLost = 1, kWalkMsgInverted = 2, kWalkMsgSync = 3 };
 
 struct WalkSummary {
@@ -138,15 +141,14 @@ struct WalkSummary {
   int64_t wait_ticks, total_ticks;  // 100 MHz ticks spent waiting / in the walker
 };
 
-struct WalkArgs {
+struct alignas(16) WalkArgs {
   uint64_t *res;        // [2][cap] result granules: hi = (epoch << 9) | syndrome weight, lo = packed bytes
   uint64_t *req;        // request granules: hi = epoch, lo = (position << 1) | polarity
-  uint32_t *reqd;       // [2][cap] epoch of the call that requested each window
   uint32_t *ctl;        // kWalkCtlWords, zeroed per launch
   uint8_t *out;         // output bytes (mo per frame)
   uint8_t *msgs;        // message codes, in order
   WalkSummary *sum;
-  int64_t cap;          // positions per polarity in res / reqd
+  int64_t cap;          // positions per polarity in res
   int64_t req_cap;      // request slots
   int64_t nin;          // samples in the span
   int N, M, KB, mo, thr;
@@ -157,6 +159,8 @@ struct WalkArgs {
   int64_t anchor;       // a position on the stream's grid, -1: none known
   uint32_t epoch;       // 1 .. 2^23 - 1
   int lead;             // frames the speculation may run ahead of the loop
+  uint64_t *trace;      // diagnostics (LDPC_WALK_TRACE=2): event records, null = off
+  int trace_cap;        // records (4 words each)
   uint64_t deadline;    // ticks one wait may take before the walk gives up
 };
 

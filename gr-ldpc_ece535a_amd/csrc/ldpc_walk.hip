@@ -36,7 +36,9 @@
 namespace ldpc {
 namespace {
 
-constexpr int kWalkChunks = 4;  // 64-frame chunks one in-sync step looks at
+constexpr int kWalkChunks = 4;   // 64-frame chunks one in-sync step of the loop looks at
+constexpr int kSpecChunks = 8;   // ... and one of the speculation
+constexpr int kVerify = 2;       // guesses settled per speculation step
 enum { kProgress = 0, kWait = 1, kEnd = 2 };
 
 // every access goes through global (address space 1) pointers: the sc1
@@ -44,6 +46,7 @@ enum { kProgress = 0, kWait = 1, kEnd = 2 };
 typedef __attribute__((address_space(1))) uint64_t gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) uint8_t gu8;
+typedef __attribute__((address_space(3))) uint32_t lu32;  // LDS
 __device__ __forceinline__ uint64_t gload(const uint64_t *p) {
   return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -78,7 +81,9 @@ struct SyncScan {
 struct Walk {
   const WalkArgs &w;
   const int lane;
+  uint32_t *bm;  // LDS bitmap of the windows asked for
   int64_t tail = 0;  // requests posted
+  bool full = false;  // the request queue ran out
   // the loop, exactly
   int64_t pos = 0;
   int st = 0, err = 0, prod = 0;
@@ -90,8 +95,9 @@ struct Walk {
   int nmsg = 0, gframes = 0, gfails = 0, surprises = 0;
   // the speculative cursor
   bool pon = false, pretry = false;
-  int64_t pp = 0, pg = 0;
-  int pst = 0, perr = 0, prpol = 0, hst = 1, pgpol = 0, restarts = 0;
+  int64_t pp = 0;
+  int pst = 0, perr = 0, prpol = 0, hst = 1, restarts = 0;
+  int64_t pgph = -1, pgc0 = 0, pgc1 = 0;  // grid prefetch: phase, cursor per polarity
   // guess ring: record i in lane i & 63 (loss frame, guessed landing, state)
   int64_t gLp = 0, gland = 0;
   int gst = 0;
@@ -100,83 +106,86 @@ struct Walk {
   // guesses, wrong guesses, restarts because the loop got ahead
   int d_sync = 0, d_out = 0, d_retry = 0, d_guess = 0, d_wrong = 0, d_behind = 0;
 
-  __device__ Walk(const WalkArgs &a, int l) : w(a), lane(l) {}
+  __device__ __forceinline__ Walk(const WalkArgs &a, int l, uint32_t *b) : w(a), lane(l), bm(b) {}
 
-  __device__ bool ready(uint64_t g) const { return (uint32_t)(g >> 41) == w.epoch; }
-  __device__ static int synd(uint64_t g) { return (int)((g >> 32) & 511u); }
-  __device__ const uint64_t *res(int pol) const { return w.res + (int64_t)pol * w.cap; }
-  __device__ bool fits(int64_t p) const { return p >= 0 && p + w.N <= w.nin; }
+  __device__ __forceinline__ bool ready(uint64_t g) const { return (uint32_t)(g >> 41) == w.epoch; }
+  __device__ __forceinline__ static int synd(uint64_t g) { return (int)((g >> 32) & 511u); }
+  __device__ __forceinline__ const uint64_t *res(int pol) const { return w.res + (int64_t)pol * w.cap; }
+  __device__ __forceinline__ bool fits(int64_t p) const { return p >= 0 && p + w.N <= w.nin; }
 
+  // Which windows were asked for: one bit per (polarity, position) in the
+  // walker's LDS (bits = 2 * nin <= 8 * kWalkLdsBytes; the workgroup's other
+  // waves have left), set with an atomic OR that also tells whether the bit
+  // was already set -- so no window is asked for twice, at LDS latency.
+  __device__ __forceinline__ uint32_t bit_index(int64_t p, int pol) const {
+    return (uint32_t)(pol ? w.nin + p : p);
+  }
+  __device__ __forceinline__ bool claim_bit(int64_t p, int pol) {
+    const uint32_t i = bit_index(p, pol);
+    const uint32_t b = 1u << (i & 31);
+    return (__hip_atomic_fetch_or((lu32 *)bm + (i >> 5), b, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP) & b) == 0;
+  }
   // ask for window (p, pol) in every lane where `act` (p may differ per
-  // lane); windows asked for before in this call are skipped
-  __device__ void request(int64_t p, int pol, bool act) {
+  // lane; no two active lanes name the same window); windows asked for
+  // before in this call are skipped
+  __device__ __forceinline__ void request(int64_t p, int pol, bool act) {
     act = act && fits(p);
-    gu32 *rd = (gu32 *)(w.reqd + (int64_t)pol * w.cap);
-    const uint32_t e = act ? rd[p] : w.epoch;
-    const bool fresh = act && e != w.epoch;
+    const bool fresh = act && claim_bit(p, pol);
     const uint64_t m = __ballot(fresh);
-    if (!m) return;
+    if (!m || !room(__popcll(m))) return;
     if (fresh) {
       const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      rd[p] = w.epoch;
       gstore(w.req + tail + below, ((uint64_t)w.epoch << 32) | (uint32_t)((p << 1) | pol));
     }
     tail += __popcll(m);
   }
-  // the same for windows nobody can have asked for yet (the grid beyond pg):
-  // marked, posted, no look-up (a duplicate would only decode twice)
-  __device__ void request_new(int64_t p, int pol, bool act) {
-    act = act && fits(p);
-    const uint64_t m = __ballot(act);
-    if (!m) return;
-    if (act) {
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      ((gu32 *)(w.reqd + (int64_t)pol * w.cap))[p] = w.epoch;
-      gstore(w.req + tail + below, ((uint64_t)w.epoch << 32) | (uint32_t)((p << 1) | pol));
-    }
-    tail += __popcll(m);
+  __device__ __forceinline__ void request_new(int64_t p, int pol, bool act) { request(p, pol, act); }
+  // request slots left?  (the queue ends kWalkClaimSlack slots before its
+  // end: decoders claim past the last request.)  Full: nothing more is asked
+  // for; a loop that then waits for a window runs into its deadline, and the
+  // host redoes the call.  (With the bitmap a window is asked for once, so
+  // 2 nin slots always suffice.)
+  __device__ __forceinline__ bool room(int n) {
+    if (tail + n <= w.req_cap - kWalkClaimSlack) return true;
+    full = true;
+    return false;
   }
-  __device__ bool requested(int64_t p, int pol) const {
-    return ((const gu32 *)w.reqd)[(int64_t)pol * w.cap + p] == w.epoch;
+  __device__ __forceinline__ bool requested(int64_t p, int pol) const {
+    const uint32_t i = bit_index(p, pol);
+    return (((const lu32 *)bm)[i >> 5] >> (i & 31)) & 1u;
   }
-  // the search positions a + 1 .. z after a lost frame at a, both
-  // polarities (one look-up round for both)
-  __device__ void search(int64_t a, int64_t z) {
+  // the search positions a + 1 .. z after a lost frame at a, both polarities
+  __device__ __forceinline__ void search(int64_t a, int64_t z) {
     for (int64_t q0 = a + 1; q0 <= z; q0 += 64) {
       const int64_t q = q0 + lane;
-      const bool act = q <= z && fits(q);
-      gu32 *rd0 = (gu32 *)w.reqd, *rd1 = (gu32 *)(w.reqd + w.cap);
-      const uint32_t e0 = act ? rd0[q] : w.epoch, e1 = act ? rd1[q] : w.epoch;
-      const bool f0 = act && e0 != w.epoch, f1 = act && e1 != w.epoch;
-      const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
-      const uint32_t b0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
-      const uint32_t b1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-      if (f0) {
-        rd0[q] = w.epoch;
-        gstore(w.req + tail + b0, ((uint64_t)w.epoch << 32) | (uint32_t)(q << 1));
-      }
-      if (f1) {
-        rd1[q] = w.epoch;
-        gstore(w.req + tail + __popcll(m0) + b1,
-               ((uint64_t)w.epoch << 32) | (uint32_t)((q << 1) | 1));
-      }
-      tail += __popcll(m0) + __popcll(m1);
+      request(q, 0, q <= z);
+      request(q, 1, q <= z);
     }
   }
-  __device__ void request_search(int64_t a) { search(a, a + w.N); }
+  __device__ __forceinline__ void request_search(int64_t a) { search(a, a + w.N); }
+  __device__ __forceinline__ void search_new(int64_t a, int64_t z) { search(a, z); }
   // a position on the stream's grid (this call's newest, else the caller's), -1: none
-  __device__ int64_t anchor() const { return anchor_pos >= 0 ? anchor_pos : w.anchor; }
+  __device__ __forceinline__ int64_t anchor() const { return anchor_pos >= 0 ? anchor_pos : w.anchor; }
 
-  __device__ void msg(int code) {
+  // diagnostics: record {ticks | kind << 56, a, b, c}
+  int ntr = 0;
+  __device__ __forceinline__ void tr(int kind, int64_t a, int64_t b, int64_t c) {
+    if (!w.trace || ntr >= w.trace_cap) return;
+    if (lane < 4) {
+      const uint64_t v = lane == 0 ? (ticks() & ((1ull << 56) - 1)) | ((uint64_t)kind << 56)
+                                   : (uint64_t)(lane == 1 ? a : lane == 2 ? b : c);
+      ((gu64 *)w.trace)[(int64_t)ntr * 4 + lane] = v;
+    }
+    ++ntr;
+  }
+  __device__ __forceinline__ void msg(int code) {
     if (lane == 0) ((gu8 *)w.msgs)[nmsg] = (uint8_t)code;
     ++nmsg;
   }
   // output frame prod + k (:207-219, bytes built by the decoder)
-  __device__ void put(int k, uint32_t packed, bool act) {
+  __device__ __forceinline__ void put(int k, uint32_t packed, bool act) {
     if (!act) return;
     gu8 *o = (gu8 *)w.out + (int64_t)(prod + k) * w.mo;
     if (w.mo == 4) {
@@ -186,7 +195,7 @@ struct Walk {
     }
   }
 
-  __device__ SyncScan scan_sync(uint64_t g, bool val, int e) const {
+  __device__ __forceinline__ SyncScan scan_sync(uint64_t g, bool val, int e) const {
     const bool rdy = val && ready(g);
     SyncScan s;
     s.R = ctz64(~__ballot(rdy));
@@ -201,31 +210,84 @@ struct Walk {
   }
 
   // -- surprises: windows the loop needs and nobody asked for ---------------
-  __device__ void surprise_sync(int pol) {
-    // a grid the speculation did not follow (a false sync): its frames until
-    // 11 of them fail, the retries where the 11th may fall, the search after
+  __device__ __forceinline__ void surprise_sync(int pol) {
     ++surprises;
     ++d_sync;
-    const int64_t N = w.N;
-    request(pos + lane * N, pol, lane < 16);
-    const int need = 11 - err;
-    request(pos + (int64_t)(need - 1 + lane) * N, pol ^ 1, lane < 3);
-    request_search(pos + (int64_t)(need - 1) * N);
+    tr(1, pos, st, err);
+    const int64_t A = anchor();
+    if (A < 0 || (pos - A) % w.N == 0) {
+      request(pos + lane * w.N, pol, true);  // the grid: the next 64 frames
+      return;
+    }
+    // a grid the speculation did not follow (a false sync): its frames until
+    // 11 of them fail, the retries where the 11th may fall, the search after
+    detour(pos, pol, err);
   }
-  __device__ void surprise_out() {
+  // the windows a grid off the anchor phase needs from frame p on (errors e
+  // so far) if every frame fails: up to the 11th failure and a few more, the
+  // retries where the 11th may fall, the search from there back to the grid
+  __device__ __forceinline__ void detour(int64_t p, int pol, int e) {
+    const int64_t N = w.N, A = anchor();
+    const int need = 11 - e;
+    request_new(p + lane * N, pol, lane < need + 2);
+    request_new(p + (int64_t)(need - 1 + lane) * N, pol ^ 1, lane < 3);
+    const int64_t L = p + (int64_t)(need - 1) * N;
+    search_new(L, A >= 0 ? L + 1 + (((A - L - 1) % N) + N) % N : L + N);
+  }
+  __device__ __forceinline__ void surprise_out() {
     ++surprises;
     ++d_out;
+    tr(2, pos, st, err);
     request(pos + lane, 0, true);
     request(pos + lane, 1, true);
   }
 
   // -- the loop ---------------------------------------------------------------
-  __device__ int e_sync() {
+  // In sync off the anchor phase (a false sync): the frames up to the 11th
+  // error, that frame's -tx retry and the search after it, loaded in one
+  // round; if every frame fails and the retry fails -- the usual detour --
+  // the loop goes through all of it here.  Anything else: false, and the
+  // ordinary steps take the frames one look at a time.
+  __device__ __forceinline__ bool e_detour() {
+    const int pol = st == 2;
+    const int64_t N = w.N;
+    const int need = 11 - err;
+    const int64_t Lf = pos + (int64_t)(need - 1) * N;
+    if (!fits(Lf) || prod + need > w.nout || nmsg + 3 > w.msgs_cap) return false;
+    const int64_t f = pos + (int64_t)lane * N;
+    const bool in = lane < need;
+    const uint64_t gf = in ? gload(res(pol) + f) : 0ull;
+    const uint64_t gr = gload(res(pol ^ 1) + Lf);
+    const int64_t q = Lf + 1 + lane;
+    const bool val = fits(q);
+    const uint64_t g0 = val ? gload(res(0) + q) : 0ull;
+    const uint64_t g1 = val ? gload(res(1) + q) : 0ull;
+    if (__ballot(in && !(ready(gf) && synd(gf) > w.thr))) return false;
+    if (!ready(gr) || synd(gr) <= w.thr) return false;
+    // frames pos .. Lf - N: in sync, failing, output (:169-176, :207-219)
+    put(lane, (uint32_t)gf, lane < need - 1);
+    gframes += need;
+    gfails += need;
+    prod += need - 1;
+    pos = Lf;
+    msg(kWalkMsgLost);  // the 11th error
+    err = 0;
+    st = 0;
+    lst = pol + 1;
+    pos += 1;  // the retry failed: skip one sample (:193-197)
+    out_scan(g0, g1, val);
+    return true;
+  }
+
+  __device__ __forceinline__ int e_sync() {
     const int pol = st == 2;
     const int64_t N = w.N;
     {
       const int64_t A = anchor();
-      if (A < 0 || (pos - A) % N == 0) ehst = st;
+      if (A < 0 || (pos - A) % N == 0)
+        ehst = st;
+      else if (e_detour())
+        return kProgress;
     }
     uint64_t g[kWalkChunks];
     bool val[kWalkChunks];
@@ -270,12 +332,17 @@ struct Walk {
     return kProgress;
   }
 
-  __device__ int e_retry() {  // :178-198 for the frame at pos
+  __device__ __forceinline__ int e_retry() {  // :178-198 for the frame at pos, then the search
     const uint64_t g = gload(res(rpol) + pos);
+    const int64_t q = pos + 1 + lane;  // the search's first positions, loaded alongside
+    const bool val = fits(q);
+    const uint64_t g0 = val ? gload(res(0) + q) : 0ull;
+    const uint64_t g1 = val ? gload(res(1) + q) : 0ull;
     if (!ready(g)) {
       if (!requested(pos, rpol)) {
         ++surprises;
         ++d_retry;
+        tr(3, pos, rpol, 0);
         request(pos, rpol, lane == 0);
       }
       return kWait;
@@ -290,17 +357,22 @@ struct Walk {
       pos += w.N;
     } else {
       pos += 1;
+      if (prod < w.nout) out_scan(g0, g1, val);
     }
     return kProgress;
   }
 
-  __device__ int e_out() {  // out of sync: the search, one sample per step
+  __device__ __forceinline__ int e_out() {  // out of sync: the search, one sample per step
     const int64_t q = pos + lane;
     const bool val = fits(q);
-    const uint64_t vm = __ballot(val);
-    if (!vm) return kEnd;
     const uint64_t g0 = val ? gload(res(0) + q) : 0ull;
     const uint64_t g1 = val ? gload(res(1) + q) : 0ull;
+    return out_scan(g0, g1, val);
+  }
+  // positions pos + lane (val), results g0 / g1 at the two polarities
+  __device__ __forceinline__ int out_scan(uint64_t g0, uint64_t g1, bool val) {
+    const uint64_t vm = __ballot(val);
+    if (!vm) return kEnd;
     const bool r0 = ready(g0), r1 = ready(g1);
     const bool p0 = r0 && synd(g0) <= w.thr, p1 = r1 && synd(g1) <= w.thr;
     const bool known = val && (p0 || (r0 && r1));
@@ -317,6 +389,10 @@ struct Walk {
       put(0, pk, lane == 0);
       ++prod;
       pos += w.N;
+      // a sync off the anchor phase: its detour, asked for now (the
+      // speculation finds out as late as this)
+      const int64_t A = anchor();
+      if (A >= 0 && (pos - A) % w.N != 0) detour(pos, via0 ? 0 : 1, 0);
       return kProgress;
     }
     pos += D;
@@ -346,7 +422,7 @@ struct Walk {
   // in one go, and the loop rarely finds a window nobody asked for.
   // Frames of the home grid are asked for up to `lead` frames ahead (pg: the
   // next one not asked for).
-  __device__ void p_set(int64_t p, int s_, int e_, bool rt, int rp) {
+  __device__ __forceinline__ void p_set(int64_t p, int s_, int e_, bool rt, int rp) {
     pp = p;
     pst = s_;
     perr = e_;
@@ -354,14 +430,16 @@ struct Walk {
     prpol = rp;
     gt = gh;  // later guesses are void
   }
-  __device__ void p_restart() {
+  __device__ __forceinline__ void p_restart() {
+    tr(4, pos, pp, st);
     pon = true;
     ++restarts;
     gh = gt = 0;
     p_set(pos, st, err, retry, rpol);
     hst = ehst;
   }
-  __device__ void p_log(int64_t a, int64_t b, int bits) {
+  __device__ __forceinline__ void p_log(int64_t a, int64_t b, int bits) {
+    tr(5, a, b, bits);
     if (lane == (gt & 63)) {
       gLp = a;
       gland = b;
@@ -370,87 +448,115 @@ struct Walk {
     ++gt;
     ++d_guess;
   }
-  // true: the oldest guess was settled (right, or rolled back)
-  __device__ bool p_verify() {
-    if (gh == gt) return false;
-    const int slot = gh & 63;
-    const int64_t a = ((int64_t)__builtin_amdgcn_readlane((int)(gLp >> 32), slot) << 32) |
-                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gLp, slot);
-    const int64_t z = ((int64_t)__builtin_amdgcn_readlane((int)(gland >> 32), slot) << 32) |
-                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gland, slot);
-    const int gw = __builtin_amdgcn_readlane(gst, slot);
+  // Settles the oldest guesses whose results are in (up to kVerify, their
+  // results loaded in one round): right ones are dropped, the first wrong one
+  // rolls the cursor back
+  __device__ __forceinline__ void p_verify() {
+    const int n = min(gt - gh, kVerify);
+    if (n <= 0) return;
     const int64_t N = w.N;
-    if (gw & 16) {  // F: frames a, a + N, .. z at polarity, all failing
-      const int pol = (gw >> 3) & 1;
-      const int64_t f = a + (int64_t)lane * N;
-      const bool val = f <= z;
-      const uint64_t g = val ? gload(res(pol) + f) : 0ull;
-      const bool rdy = ready(g);
-      if (__ballot(val && !rdy)) return false;  // not all in yet
-      if (!__ballot(val && synd(g) <= w.thr)) {
-        ++gh;
-        return true;
+    int64_t A_[kVerify], Z_[kVerify];
+    int W_[kVerify];
+    uint64_t ga[kVerify], gb[kVerify], gr[kVerify];
+#pragma unroll
+    for (int i = 0; i < kVerify; ++i) {
+      A_[i] = Z_[i] = 0;
+      W_[i] = 0;
+      ga[i] = gb[i] = gr[i] = 0ull;
+      if (i < n) {
+        const int slot = (gh + i) & 63;
+        A_[i] = ((int64_t)__builtin_amdgcn_readlane((int)(gLp >> 32), slot) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gLp, slot);
+        Z_[i] = ((int64_t)__builtin_amdgcn_readlane((int)(gland >> 32), slot) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gland, slot);
+        W_[i] = __builtin_amdgcn_readlane(gst, slot);
+        const int64_t a = A_[i], z = Z_[i];
+        if (W_[i] & 16) {  // F: frames a, a + N, .. z
+          const int64_t f = a + (int64_t)lane * N;
+          ga[i] = f <= z ? gload(res((W_[i] >> 3) & 1) + f) : 0ull;
+        } else {  // S: the retry at a, the search a + 1 .. z
+          if (W_[i] & 4) gr[i] = gload(res((W_[i] >> 3) & 1) + a);
+          const int64_t q = a + 1 + lane;
+          if (q <= z) {
+            ga[i] = gload(res(0) + q);
+            gb[i] = gload(res(1) + q);
+          }
+        }
       }
-      ++d_wrong;  // one passes: back to the start, where the cursor now reads them
-      p_set(a, pol + 1, (gw >> 8) & 15, false, 0);
-      return true;
     }
-    // S: retry at a (if pending), then the search a + 1 .. z
-    const int gs = gw & 3;           // guessed state after the landing
-    const bool has_retry = gw & 4;
-    const int rp = (gw >> 3) & 1;    // the retry's polarity
-    const uint64_t gr = has_retry ? gload(res(rp) + a) : 0ull;
-    const int64_t q = a + 1 + lane;
-    const bool val = q <= z;
-    const uint64_t g0 = val ? gload(res(0) + q) : 0ull;
-    const uint64_t g1 = val ? gload(res(1) + q) : 0ull;
-    if (has_retry) {
-      if (!ready(gr)) return false;
-      if (synd(gr) <= w.thr) {  // the retry passes: in sync inverted at a
+#pragma unroll
+    for (int i = 0; i < kVerify; ++i) {
+      if (i >= n) return;
+      const int64_t a = A_[i], z = Z_[i];
+      const int gw = W_[i];
+      if (gw & 16) {
+        const int pol = (gw >> 3) & 1;
+        const bool val = a + (int64_t)lane * N <= z;
+        if (__ballot(val && !ready(ga[i]))) return;  // not all in yet
+        if (!__ballot(val && synd(ga[i]) <= w.thr)) {
+          ++gh;
+          tr(6, a, z, gw);
+          continue;
+        }
+        ++d_wrong;  // one passes: back to the start, where the cursor now reads them
+        tr(7, a, z, gw);
+        p_set(a, pol + 1, (gw >> 8) & 15, false, 0);
+        return;
+      }
+      const int gs = gw & 3;  // guessed state after the landing
+      if (gw & 4) {
+        if (!ready(gr[i])) return;
+        if (synd(gr[i]) <= w.thr) {  // the retry passes: in sync inverted at a
+          ++d_wrong;
+          tr(7, a, z, gw);
+          p_set(a + N, 2, 0, false, 0);
+          return;
+        }
+      }
+      const bool val = a + 1 + lane <= z;
+      const bool r0 = ready(ga[i]), r1 = ready(gb[i]);
+      const bool p0 = r0 && synd(ga[i]) <= w.thr, p1 = r1 && synd(gb[i]) <= w.thr;
+      const bool known = val && (p0 || (r0 && r1));
+      const uint64_t vm = __ballot(val);
+      const int D = ctz64(~__ballot(known));
+      const uint64_t hit = __ballot(known && (p0 || p1)) & lowmask(D);
+      if (hit) {
+        const int j = ctz64(hit);
+        const int s1 = ((__ballot(p0) >> j) & 1) ? 1 : 2;
+        if (a + 1 + j == z && s1 == gs) {
+          ++gh;  // right
+          tr(6, a, z, gw);
+          continue;
+        }
         ++d_wrong;
-        p_set(a + N, 2, 0, false, 0);
-        return true;
+        tr(7, a, a + 1 + j, gw | (s1 << 12));
+        p_set(a + 1 + j + N, s1, 0, false, 0);  // a false sync, or another state
+        return;
       }
-    }
-    const bool r0 = ready(g0), r1 = ready(g1);
-    const bool p0 = r0 && synd(g0) <= w.thr, p1 = r1 && synd(g1) <= w.thr;
-    const bool known = val && (p0 || (r0 && r1));
-    const uint64_t vm = __ballot(val);
-    const int D = ctz64(~__ballot(known));
-    const uint64_t hit = __ballot(known && (p0 || p1)) & lowmask(D);
-    if (hit) {
-      const int j = ctz64(hit);
-      const int s1 = ((__ballot(p0) >> j) & 1) ? 1 : 2;
-      if (a + 1 + j == z && s1 == gs) {
-        ++gh;  // right
-        return true;
-      }
+      if (D < __popcll(vm)) return;  // not all in yet
       ++d_wrong;
-      p_set(a + 1 + j + N, s1, 0, false, 0);  // a false sync, or another state
-      return true;
+      tr(7, a, -1, gw);
+      p_set(z + 1, 0, 0, false, 0);  // nothing passed up to the guessed landing
+      return;
     }
-    if (D < __popcll(vm)) return false;  // not all in yet
-    ++d_wrong;
-    p_set(z + 1, 0, 0, false, 0);  // nothing passed up to the guessed landing
-    return true;
   }
   // guess S from the loss at Lp (retry pending at polarity rp if has_retry)
-  __device__ void p_guess(int64_t Lp, bool has_retry, int rp) {
+  __device__ __forceinline__ void p_guess(int64_t Lp, bool has_retry, int rp) {
     const int64_t N = w.N, A = anchor();
     const int64_t land = A >= 0 ? Lp + 1 + (((A - Lp - 1) % N) + N) % N : Lp + N;
-    if (has_retry) request(Lp, rp, lane == 0);
-    search(Lp, land);
+    if (has_retry) request_new(Lp, rp, lane == 0);
+    search_new(Lp, land);
     p_log(Lp, land, hst | (has_retry ? 4 : 0) | (rp << 3));
     pp = land;  // in sync from the landing frame on (it passes: the scan sees so)
     pst = hst;
     perr = 0;
     pretry = false;
   }
-  __device__ void p_step() {
+  // waiting: the loop waits for a result (keep the step short, to look again soon)
+  __device__ __forceinline__ void p_step(bool waiting) {
     if (pon && pp < pos) ++d_behind;
     if (!pon || pp < pos) p_restart();
-    for (int v = 0; v < 4 && p_verify(); ++v) {
-    }
+    p_verify();
     if (pp < pos) {
       ++d_behind;
       p_restart();
@@ -458,8 +564,13 @@ struct Walk {
     const int64_t N = w.N;
     const int64_t limit = pos + (int64_t)w.lead * N;
     // several losses per step: the loop takes about three steps per loss
-    for (int it = 0; it < 8; ++it) {
-      if (pp >= limit || gt - gh >= 62) return;
+    // while the loop waits, one short turn at most (and none when well ahead)
+    if (waiting && gt - gh >= 4) return;
+    for (int it = 0; it < (waiting ? 1 : 8); ++it) {
+      if (pp >= limit || gt - gh >= 62) {
+        tr(11, pp, pst | (pretry << 2), (limit - pos) | ((int64_t)(gt - gh) << 40) | (1ll << 56));
+        return;
+      }
       if (pretry) {
         const uint64_t g = gload(res(prpol) + pp);
         if (!ready(g)) {
@@ -478,7 +589,10 @@ struct Walk {
       }
       if (!pst) {
         // out of sync (a restart in the loop's search, or a wrong landing)
-        if (!fits(pp)) return;
+        if (!fits(pp)) {
+          tr(11, pp, pst, 3ll << 56);
+          return;
+        }
         p_guess(pp - 1, false, 0);
         continue;
       }
@@ -489,35 +603,94 @@ struct Walk {
       bool val[kWalkChunks];
       if (home) {
         hst = pst;
-        // the grid ahead (pg counts for one phase and polarity)
-        if (pg < pp || (pg - pp) % N != 0 || pgpol != pol) {
-          pg = pp;
-          pgpol = pol;
+        // the grid ahead: one cursor per polarity (pgc[pol], the first frame
+        // not asked for), for one phase; only ever moving forward
+        const int64_t ph = ((pp % N) + N) % N;
+        if (ph != pgph) {
+          pgph = ph;
+          pgc0 = pgc1 = pp;
         }
+        int64_t pg = pol ? pgc1 : pgc0;
+        if (pg < pp) pg = pp;
 #pragma unroll
         for (int c = 0; c < kWalkChunks; ++c) {
           if (pg >= limit) break;
           const int64_t f = pg + (int64_t)lane * N;
           request_new(f, pol, f < limit);
-          pg += 64 * N;
+          pg = min(pg + 64 * N, pg + (limit - pg + N - 1) / N * N);
         }
+        if (pol)
+          pgc1 = pg;
+        else
+          pgc0 = pg;
+        // kSpecChunks x 64 frames in one round; every loss among them is
+        // guessed over (S, landing on this grid) without another load
+        uint64_t hg[kSpecChunks];
+        const int64_t base = pp;
 #pragma unroll
-        for (int c = 0; c < kWalkChunks; ++c) {
-          const int64_t f = pp + (int64_t)(64 * c + lane) * N;
-          val[c] = fits(f);
-          g[c] = val[c] ? gload(res(pol) + f) : 0ull;
+        for (int c = 0; c < kSpecChunks; ++c) {
+          const int64_t f = base + (int64_t)(64 * c + lane) * N;
+          hg[c] = fits(f) ? gload(res(pol) + f) : 0ull;
         }
+        int k = 0;  // frames of the window behind the cursor
+        bool stop = false;
+#pragma unroll
+        for (int c = 0; c < kSpecChunks; ++c) {
+          if (!stop && k < 64 * (c + 1)) {
+            const bool val = fits(base + (int64_t)(64 * c + lane) * N);
+            const uint64_t RM = __ballot(val && ready(hg[c]));
+            const uint64_t FM = __ballot(val && ready(hg[c]) && synd(hg[c]) > w.thr) & RM;
+            int b = k - 64 * c;
+            while (b < 64) {
+              const int R = ctz64(~(RM >> b));
+              if (R == 0) {
+                stop = true;
+                break;
+              }
+              const uint64_t F = (FM >> b) & lowmask(R);
+              const int need = 11 - perr;
+              if (__popcll(F) < need) {
+                perr += __popcll(F);
+                b += R;
+                continue;
+              }
+              const int kk = b + nth_bit(F, need);  // the 11th failure
+              const int64_t Lp = base + (int64_t)(64 * c + kk) * N;
+              // the search lands on the first frame after it known to pass
+              // (frames known to fail before it, at most 8, are searched
+              // through), else on the next one
+              const uint64_t after = kk + 1 < 64 ? RM >> (kk + 1) : 0ull;
+              const int run = min(ctz64(~after), 8);
+              const uint64_t passes =
+                  kk + 1 < 64 ? (after & ~(FM >> (kk + 1))) & lowmask(run) : 0ull;
+              const int j = passes ? kk + 1 + ctz64(passes) : kk + 1 + run;
+              const int64_t land = base + (int64_t)(64 * c + j) * N;
+              request_new(Lp, pol ^ 1, lane == 0);
+              search_new(Lp, land);
+              p_log(Lp, land, pst | 4 | ((pol ^ 1) << 3));
+              perr = 0;
+              b = j;
+              if (gt - gh >= 62) {
+                stop = true;
+                break;
+              }
+            }
+            k = 64 * c + b;
+          }
+        }
+        pp = base + (int64_t)k * N;
+        return;
       } else {
         // a false grid: its frames up to the 11th error; guess F if they are
         // not all in, else read them like any other
         const int need = 11 - perr;
         const int64_t f = pp + (int64_t)lane * N;
         const bool in = lane < need && fits(f);
-        request(f, pol, in);
         const uint64_t gf = in ? gload(res(pol) + f) : 0ull;
         if (__ballot(in && !ready(gf))) {
           const int64_t Lf = pp + (int64_t)(need - 1) * N;
           if (!fits(Lf)) return;
+          request_new(f, pol, in && !ready(gf));
           p_log(pp, Lf, 16 | (pol << 3) | (perr << 8));
           pp = Lf;  // the 11th error: the retry next
           perr = 0;
@@ -535,9 +708,13 @@ struct Walk {
         }
       }
       bool lost = false;
+      tr(12, pp, pst | (home << 3), pgc0);
 #pragma unroll
       for (int c = 0; c < kWalkChunks; ++c) {
-        if (!__ballot(val[c])) return;
+        if (!__ballot(val[c])) {
+          tr(11, pp, pst, 4ll << 56);
+          return;
+        }
         const SyncScan sc = scan_sync(g[c], val[c], perr);
         perr += __popcll(sc.F);
         pp += (int64_t)sc.kstar * N;
@@ -549,16 +726,30 @@ struct Walk {
           lost = true;
           break;
         }
-        if (sc.R < 64) return;
+        if (sc.R < 64) {
+          tr(11, pp, pst, (5ll << 56) | sc.R);
+          return;
+        }
       }
-      if (!lost) return;
+      if (!lost) {
+        tr(11, pp, pst, 6ll << 56);
+        return;
+      }
     }
   }
 };
 
-__device__ __forceinline__ void walker_run(const WalkArgs &w) {
+// Compiled once (not per decoder instantiation); its arguments are the
+// kernel's, copied to LDS by the caller, and its state lives in registers.
+__device__ __attribute__((noinline)) void walker_run(const WalkArgs &w, uint32_t *bm) {
   const int lane = threadIdx.x & 63;
-  Walk k(w, lane);
+  // clear the bitmap: 2 nin bits
+  const int words = (int)((2 * w.nin + 31) / 32);
+  for (int i = lane; i < words; i += 64) ((lu32 *)bm)[i] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  Walk k(w, lane, bm);
   k.st = w.state;
   k.err = w.errors;
   k.last_pass = w.last_pass;
@@ -574,15 +765,16 @@ __device__ __forceinline__ void walker_run(const WalkArgs &w) {
         break;
       }
       r = k.retry ? k.e_retry() : (k.st ? k.e_sync() : k.e_out());
+      k.tr(8 + r, k.pos, k.st, k.pp);
     }
     if (r == kEnd && !k.retry) break;
-    k.p_step();
+    k.p_step(r == kWait);
     const uint64_t t = ticks();
     if (r == kWait) {
       ++waits;
       wait_ticks += t - t_last;
-      if (t - t_moved > w.deadline) {
-        status = 1;
+      if (t - t_moved > w.deadline || (k.full && t - t_moved > w.deadline / 16)) {
+        status = k.full ? 2 : 1;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -633,7 +825,14 @@ __global__ void __launch_bounds__(kThreads, 1)
   __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
   if constexpr (METHOD == 1) stage_tab<PREC>(logtab);
   if (blockIdx.x == 0) {
-    if (wave == 0) walker_run(w);
+    if (wave == 0) {
+      __shared__ WalkArgs wl;
+      if (lane == 0) wl = w;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      walker_run(wl, reinterpret_cast<uint32_t *>(smem));
+    }
     return;
   }
   WaveTables<S, NW> wt;
@@ -712,7 +911,8 @@ template <int PREC, int METHOD, int S, int NW, int DCN, int DVN>
 int launch_w(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, int blocks,
              hipStream_t st) {
   typedef typename Math<PREC>::Real Real;
-  const size_t lds = Layout<Real, METHOD, S, NW, DVN>::total;
+  // the decoders' slices, and the walker's bitmap in workgroup 0
+  const size_t lds = std::max(Layout<Real, METHOD, S, NW, DVN>::total, (size_t)kWalkLdsBytes);
   const void *fn = (const void *)walk_small_kernel<PREC, METHOD, S, NW, DCN, DVN>;
   static int per_cu = 0;  // resident workgroups per CU (all of them run at once)
   if (!per_cu) {
