@@ -1299,14 +1299,20 @@ int copy_span(ldpc_ctx *ctx, const float *in, int64_t S, int elem_stride, float 
   int rc = ensure_host_stage(ctx, (size_t)S * 4);
   if (rc != LDPC_OK) return rc;
   float *h = ctx->h_stage;
-  if (elem_stride == 1)
-    memcpy(h, in, (size_t)S * 4);
-  else if (elem_stride == 2)  // gr_complex real parts (the block): a constant stride vectorises
-    for (int64_t i = 0; i < S; ++i) h[i] = in[2 * i];
-  else
-    for (int64_t i = 0; i < S; ++i) h[i] = in[i * elem_stride];
-  hipError_t e = hipMemcpyAsync(d_span, h, (size_t)S * 4, hipMemcpyHostToDevice, ctx->stream);
-  if (e != hipSuccess) return hip_err(ctx, e, "hipMemcpyAsync(span)");
+  // in pieces: each piece's copy to the device runs while the next is gathered
+  const int64_t piece = S >= ((int64_t)1 << 17) ? ((int64_t)1 << 15) : S;
+  for (int64_t i0 = 0; i0 < S; i0 += piece) {
+    const int64_t i1 = std::min(S, i0 + piece);
+    if (elem_stride == 1)
+      memcpy(h + i0, in + i0, (size_t)(i1 - i0) * 4);
+    else if (elem_stride == 2)  // gr_complex real parts (the block): a constant stride vectorises
+      for (int64_t i = i0; i < i1; ++i) h[i] = in[2 * i];
+    else
+      for (int64_t i = i0; i < i1; ++i) h[i] = in[i * elem_stride];
+    hipError_t e = hipMemcpyAsync(d_span + i0, h + i0, (size_t)(i1 - i0) * 4,
+                                  hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) return hip_err(ctx, e, "hipMemcpyAsync(span)");
+  }
   ctx->h_stage_busy = true;
   ctx->span_samples = S;
   return LDPC_OK;
@@ -1605,6 +1611,11 @@ int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, cons
   io->surprises = sm.surprises;
   io->steps = sm.steps;
   io->restarts = sm.restarts;
+  if (tracing) {
+    uint32_t dc[2] = {0, 0};
+    if (hipMemcpy(dc, (char *)ctx->d_walk + 264 * 4, 8, hipMemcpyDeviceToHost) == hipSuccess && dc[1])
+      fprintf(stderr, "walk decoders: %u windows, %.2f us each\n", dc[1], 1e-2 * dc[0] / dc[1]);
+  }
   if (tracing && d_trace) {
     std::vector<uint64_t> h((size_t)trace_cap * 4);
     if (hipMemcpy(h.data(), d_trace, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {

@@ -564,9 +564,12 @@ struct Walk {
     const int64_t N = w.N;
     const int64_t limit = pos + (int64_t)w.lead * N;
     // several losses per step: the loop takes about three steps per loss
-    // while the loop waits, one short turn at most (and none when well ahead)
-    if (waiting && gt - gh >= 4) return;
-    for (int it = 0; it < (waiting ? 1 : 8); ++it) {
+    // while the loop waits and the cursor is ahead (unsettled guesses), the
+    // loop is not kept from looking again; behind (after a rollback), the
+    // cursor takes a full turn: the windows after the landing it now knows
+    // are what the loop will wait for next
+    if (waiting && gt - gh >= 2) return;
+    for (int it = 0; it < 8; ++it) {
       if (pp >= limit || gt - gh >= 62) {
         tr(11, pp, pst | (pretry << 2), (limit - pos) | ((int64_t)(gt - gh) << 40) | (1ll << 56));
         return;
@@ -864,6 +867,7 @@ __global__ void __launch_bounds__(kThreads, 1)
       else
         __builtin_amdgcn_s_sleep(4);
     }
+    const uint64_t t_got = ticks();
     // window key: the N samples from position key >> 1, negated when key & 1
     const int64_t p = key >> 1;
     const float sgn = (key & 1) ? -1.0f : 1.0f;
@@ -894,6 +898,11 @@ __global__ void __launch_bounds__(kThreads, 1)
     const uint64_t out = ((uint64_t)((w.epoch << 9) | (uint32_t)r.weight) << 32) | pk;
     if (lane == 0) gstore(w.res + (int64_t)(key & 1) * w.cap + p, out);
     idle = ticks();
+    if (w.trace && lane == 0) {  // diagnostics: decode time and count
+      __hip_atomic_fetch_add((gu32 *)(w.ctl + 264), (uint32_t)(idle - t_got), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add((gu32 *)(w.ctl + 265), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
