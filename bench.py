@@ -454,11 +454,14 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
         sys.path.insert(0, REPO)
         from oracle import oracle as orc
     # (name, Eb/N0, iterations, CPU sample in frames: ~3-15 s of one core each)
-    runs = (("in-sync stream (4 dB)", 4.0, args.iters, cpu_frames),
-            ("2 dB stream (sync losses)", 2.0, args.iters, cpu_frames // 2),
+    runs = (("in-sync stream (4 dB)", 4.0, args.iters, cpu_frames, False),
+            ("2 dB stream (sync losses)", 2.0, args.iters, cpu_frames // 2, False),
             # make(method) as the reference builds it: 5 iterations (:40)
-            ("make(1) defaults, 5 iterations, 4 dB", 4.0, 5, cpu_frames))
-    for name, ebn0, iters, n_cpu in runs:
+            ("make(1) defaults, 5 iterations, 4 dB", 4.0, 5, cpu_frames, False),
+            # the same stream through the device-side frame loop (LDPC_BLOCK_WALK=1)
+            ("make(1) defaults, 5 iterations, 4 dB, device walk", 4.0, 5, cpu_frames, True))
+    last_ref = None
+    for name, ebn0, iters, n_cpu, walk in runs:
         dec = L.Decoder(device=dev.index or 0)
         y, _ = synth_device(L, torch, dec, (reps + 1) * B, ebn0, args.seed + 77, dev,
                             check_frames=0)
@@ -467,13 +470,23 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
         stream = np.zeros(2 * y.numel(), np.float32)
         stream[0::2] = y.cpu().numpy().ravel()
         cx = stream.view(np.complex64)
-        blk = blocks.ldpc_decoder_cb(1, iterations=iters, precision=0, device=dev.index or 0)
+        if walk:
+            os.environ["LDPC_BLOCK_WALK"] = "1"
+        try:
+            blk = blocks.ldpc_decoder_cb(1, iterations=iters, precision=0, device=dev.index or 0)
+        finally:
+            os.environ.pop("LDPC_BLOCK_WALK", None)
         dt, made, calls, launches, windows = drive_stream(blk, cx, B)
         out[name] = {"Mbit/s": round(made * 8 / dt / 1e6, 2), "calls": calls,
                      "ms_per_call": round(dt / max(1, calls) * 1e3, 4),
                      "launches_per_call": round(launches / max(1, calls), 2),
                      "windows_per_output_frame": round(windows / max(1, made // 4), 2),
                      "bytes_out": int(made)}
+        if walk and last_ref is not None:  # the previous run's CPU restatement, same stream
+            gpu_bytes = drive_stream.last_out
+            out[name]["bytes_equal_cpu_prefix"] = bool(
+                gpu_bytes.size >= last_ref.size and (gpu_bytes[:last_ref.size] == last_ref).all())
+            continue
         if orc is not None:
             gpu_bytes = drive_stream.last_out
             sample = cx[:n_cpu * 64]
@@ -481,6 +494,7 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
             stats = {}
             ref = orc.run_stream(1, Hr, sample, iterations=iters, stats=stats)
             cpu_s = time.perf_counter() - t0
+            last_ref = ref
             out[name]["cpu_baseline"] = {
                 "Mbit/s": round(ref.size * 8 / cpu_s / 1e6, 5), "cores": 1, "kind": "port",
                 "sample": "the stream's first %d frames of samples through the restated "

@@ -12,12 +12,19 @@ from ldpc_ece535a import flowgraph as fg
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("walk", ["0", "1"])
 @pytest.mark.parametrize("name", ["aligned", "offset", "inverted", "burst", "noisy"])
 @pytest.mark.parametrize("method", [0, 1, 2, 3])
-def test_gpu_block_streams(golden, name, method):
+def test_gpu_block_streams(golden, name, method, walk):
+    """walk "1": the block's calls run the frame loop on the device (ldpc_walk_span)."""
+    import os
     st = golden("streams.npz")
     s = st[name + "_in"]
-    blk = L.ldpc_decoder_cb(method)
+    os.environ["LDPC_BLOCK_WALK"] = walk
+    try:
+        blk = L.ldpc_decoder_cb(method)
+    finally:
+        os.environ.pop("LDPC_BLOCK_WALK", None)
     tb = fg.top_block(chunk=[97, 13, 640, 5, 2000] * 4)
     src, dst = fg.vector_source_c(s), fg.vector_sink_b()
     tb.connect((src, 0), (blk, 0))
