@@ -829,4 +829,18 @@ __device__ __forceinline__ void wave_setup(const CodeView &code, unsigned char *
   }
 }
 
+// LDS of the workgroup-per-frame kernels (decode_mw_kernel, walk_mw_kernel):
+// tb / eb per edge cell, per-wave rb / sb, the frame slot
+template <typename Real, int S, int NW>
+struct MwLayout {
+  size_t eb, waves, per_wave, fslot, total;
+  __host__ __device__ MwLayout() {
+    eb = align16((64 * S + 2) * sizeof(Real));           // tb at 0
+    waves = eb + align16((64 * S + 2) * sizeof(Real));   // per-wave rb, sb
+    per_wave = align16(2 * 64 * NW * sizeof(Real));
+    fslot = waves + (size_t)S * per_wave;
+    total = fslot + 16;
+  }
+};
+
 }  // namespace ldpc

@@ -211,17 +211,6 @@ __global__ void __launch_bounds__(kThreads, MINB)
 // every wave redundantly from the shared check messages, so every wave
 // reaches the same early-exit decision without a third barrier.
 // ---------------------------------------------------------------------------
-template <typename Real, int S, int NW>
-struct MwLayout {
-  size_t eb, waves, per_wave, fslot, total;
-  __host__ __device__ MwLayout() {
-    eb = align16((64 * S + 2) * sizeof(Real));           // tb at 0
-    waves = eb + align16((64 * S + 2) * sizeof(Real));   // per-wave rb, sb
-    per_wave = align16(2 * 64 * NW * sizeof(Real));
-    fslot = waves + (size_t)S * per_wave;
-    total = fslot + 16;
-  }
-};
 
 template <int PREC, int METHOD, int S, int NW>
 __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, DecodeArgs a) {

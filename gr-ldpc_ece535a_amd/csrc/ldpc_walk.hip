@@ -916,6 +916,269 @@ int cus_now() {
   return cus_of[dev];
 }
 
+// The decoders in workgroup form (LDPC_WALK_MW, sum-product and min-sum):
+// each workgroup of S waves decodes one window at a time, one edge per lane
+// -- the decode_mw_kernel arithmetic (ldpc_kernels.hip), whose iteration is
+// ~1.1 us against ~2 us for one wave -- so a round of the loop's chain (a
+// false sync's detour) waits less.  Workgroup 0 is the walker, as above.
+template <int PREC, int METHOD, int S, int NW>
+__global__ void __launch_bounds__(64 * S)
+    walk_mw_kernel(CodeView code, DecodeArgs a, WalkArgs w) {
+  typedef typename Math<PREC>::Real Real;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const MwLayout<Real, S, NW> L;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = code.M, N = code.N;
+  constexpr int kDummy = 64 * S;
+  __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
+  if constexpr (METHOD == 1) stage_tab<PREC>(logtab);
+  if (blockIdx.x == 0) {
+    if (wave == 0) {
+      __shared__ WalkArgs wl;
+      if (lane == 0) wl = w;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      walker_run(wl, reinterpret_cast<uint32_t *>(smem));
+    }
+    return;
+  }
+  Real *tb = reinterpret_cast<Real *>(smem);
+  Real *eb = reinterpret_cast<Real *>(smem + L.eb);
+  Real *rb = reinterpret_cast<Real *>(smem + L.waves + (size_t)wave * L.per_wave);
+  Real *sb = rb + 64 * NW;
+  int *fslot = reinterpret_cast<int *>(smem + L.fslot);
+  if (tid == 0) tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
+  uint32_t rn[4], cn[2], ce[NW][2];
+  {
+    const uint4 r = reinterpret_cast<const uint4 *>(code.erow)[tid];
+    rn[0] = r.x;
+    rn[1] = r.y;
+    rn[2] = r.z;
+    rn[3] = r.w;
+    const uint2 c = reinterpret_cast<const uint2 *>(code.ecol)[tid];
+    cn[0] = c.x;
+    cn[1] = c.y;
+  }
+  uint64_t rowmask[NW][NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const uint4 c = reinterpret_cast<const uint4 *>(code.cols)[lane + 64 * q];
+    ce[q][0] = c.x;
+    ce[q][1] = c.y;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int j = lane + 64 * q;
+      rowmask[q][k] = j < M ? code.rowmask[j * NW + k] : 0ull;
+    }
+  }
+  int col = field(rn, 7);
+  col = col != kNone ? col : 0;
+  int colq[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const uint32_t c = code.lane_col[lane + 64 * q];
+    colq[q] = c == kNone ? -1 : (int)c;
+  }
+  const uint32_t x = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;
+  uint64_t idle = ticks();
+  for (;;) {
+    if (tid == 0) {  // claim a slot of this XCD's shard, wait for its request
+      const uint32_t c = __hip_atomic_fetch_add((gu32 *)(w.ctl + 32 * x), 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t i = (int64_t)c * 8 + x;
+      int key = -1;
+      for (int spins = 0;; ++spins) {
+        const uint64_t g = i < w.req_cap ? gload(w.req + i) : 0ull;
+        if ((uint32_t)(g >> 32) == w.epoch) {
+          key = (int)(uint32_t)g;
+          break;
+        }
+        if ((spins & 7) == 7 &&
+            (gload32(w.ctl + kWalkDone) != 0u || ticks() - idle > w.deadline))
+          break;
+        if (spins < 8)
+          __builtin_amdgcn_s_sleep(1);
+        else
+          __builtin_amdgcn_s_sleep(4);
+      }
+      *fslot = key;
+    }
+    __syncthreads();
+    const int key = *fslot;
+    if (key < 0) return;  // the walk is over (every thread of the workgroup)
+    const int64_t p = key >> 1;
+    const float polv = (key & 1) ? -1.0f : 1.0f;
+    const __attribute__((address_space(1))) float *src =
+        (const __attribute__((address_space(1))) float *)a.in + p;
+    Real post[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int c = lane + 64 * q;
+      float xv = 0.0f;
+      if (colq[q] >= 0) xv = src[colq[q]] * polv;
+      rb[c] = -(Real)xv;
+      post[q] = (Real)xv;
+    }
+    __syncthreads();
+    uint64_t hard[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) hard[q] = 0;
+    int weight = 0;
+    Real msg = rb[col], lr = Real(0);
+    for (int h = 0; h < a.max_iters; ++h) {
+      opaque(rn);
+      opaque(cn);
+      if constexpr (METHOD == 1)
+        tb[tid] = Math<PREC>::tanh_half(msg, logtab);  // :509
+      else
+        tb[tid] = msg;
+      __syncthreads();
+      Real nb[kDcMax - 1];
+#pragma unroll
+      for (int k = 0; k < kDcMax - 1; ++k) {
+        const int n = field(rn, k);
+        nb[k] = tb[n == kNone ? kDummy : n];
+      }
+      if constexpr (METHOD == 1) {
+        Real T = Real(1);  // ascending column; dummies are exact 1.0 (:506-511)
+#pragma unroll
+        for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[k];
+        eb[tid] = Math<PREC>::check_msg(T, logtab);  // :513
+      } else {
+        const int self = sgn(msg);  // :350-376
+        int prod = self;
+        Real lo = Math<PREC>::max_();
+#pragma unroll
+        for (int k = 0; k < kDcMax - 1; ++k) {
+          prod *= sgn(nb[k]);
+          const Real beta = Math<PREC>::abs_(nb[k]);
+          lo = beta < lo ? beta : lo;
+        }
+        lr = (Real)(prod * self) * lo;
+        eb[tid] = lr;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        opaque(ce[q]);
+        const int c = lane + 64 * q;
+        Real ev[kDvMax];
+#pragma unroll
+        for (int k = 0; k < kDvMax; ++k) {
+          const int n = field(ce[q], k);
+          ev[k] = eb[n == kNone ? kDummy : n];
+        }
+        const Real rc = rb[c];
+        Real acc = Real(0);
+        bool bit;
+        if constexpr (METHOD == 1) {  // :519-532
+#pragma unroll
+          for (int k = 0; k < kDvMax; ++k)
+            acc = field(ce[q], k) != kNone ? acc + (ev[k] + rc) : acc;
+          bit = acc <= Real(0);
+          post[q] = acc;
+        } else {  // :379-403
+#pragma unroll
+          for (int k = 0; k < kDvMax; ++k)
+            acc = field(ce[q], k) != kNone ? acc + ev[k] : acc;
+          const Real LQ = rc + acc;
+          sb[c] = LQ;
+          bit = LQ < Real(0);
+          post[q] = LQ;
+        }
+        hard[q] = __ballot(bit && c < N);
+      }
+      weight = 0;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        int odd = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) odd ^= __popcll(rowmask[q][k] & hard[k]);
+        weight += __popcll(__ballot((odd & 1) != 0 && lane + 64 * q < M));
+      }
+      if (h + 1 == a.max_iters) break;
+      if ((h + 1) % a.et_period == 0 && weight == 0) break;
+      if constexpr (METHOD == 1) {  // :540-553
+        const Real rc = rb[col];
+        Real cv[kDvMax - 1];
+#pragma unroll
+        for (int k = 0; k < kDvMax - 1; ++k) {
+          const int n = field(cn, k);
+          cv[k] = eb[n == kNone ? kDummy : n];
+        }
+        Real acc = Real(0);
+#pragma unroll
+        for (int k = 0; k < kDvMax - 1; ++k)
+          acc = field(cn, k) != kNone ? acc + (cv[k] + rc) : acc;
+        msg = acc;
+      } else {
+        wave_lds_sync();  // this wave's sb
+        msg = sb[col] - lr;  // :387-392
+      }
+    }
+    (void)post;
+    if (wave == 0) {  // packed bytes M.. (:207-219), then the granule
+      uint32_t o = 0;
+      if (lane < code.KB) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = M + 8 * lane + j;
+          if (c < N) {
+            const int xp = code.col_lane[c];  // position of column c
+            o |= (uint32_t)((word_at<NW>(hard, xp >> 6) >> (xp & 63)) & 1) << (7 - j);
+          }
+        }
+      }
+      uint32_t pk = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        pk |= ((uint32_t)__builtin_amdgcn_readlane((int)o, j) & 255u) << (8 * j);
+      const uint64_t out = ((uint64_t)((w.epoch << 9) | (uint32_t)weight) << 32) | pk;
+      if (lane == 0) gstore(w.res + (int64_t)(key & 1) * w.cap + p, out);
+    }
+    wave_lds_sync();
+    __syncthreads();  // the window's LDS reads done before the next window's writes
+    idle = ticks();
+  }
+}
+
+template <int PREC, int METHOD, int S, int NW>
+int launch_wmw(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, hipStream_t st) {
+  typedef typename Math<PREC>::Real Real;
+  const size_t bm = (size_t)((2 * w.nin + 127) / 128) * 16;  // the walker's bitmap
+  const size_t lds = std::max(MwLayout<Real, S, NW>().total, bm);
+  const void *fn = (const void *)walk_mw_kernel<PREC, METHOD, S, NW>;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kWalkLdsBytes) !=
+        hipSuccess)
+      return -3;
+    attr = true;
+  }
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * S, lds) != hipSuccess || n < 1)
+    n = 1;
+  const char *e = getenv("LDPC_WALK_BLOCKS_PER_CU");
+  const int blocks = std::min(n, e ? std::max(atoi(e), 1) : 4) * cus_now();
+  hipLaunchKernelGGL((walk_mw_kernel<PREC, METHOD, S, NW>), dim3((unsigned)blocks),
+                     dim3(64 * S), lds, st, code, a, w);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <int PREC, int METHOD, int NW>
+int walk_mw_slots(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, int slots,
+                  hipStream_t st) {
+  switch (slots) {
+    case 1: return launch_wmw<PREC, METHOD, 1, NW>(code, a, w, st);
+    case 2: return launch_wmw<PREC, METHOD, 2, NW>(code, a, w, st);
+    case 3: return launch_wmw<PREC, METHOD, 3, NW>(code, a, w, st);
+    case 4: return launch_wmw<PREC, METHOD, 4, NW>(code, a, w, st);
+    default: return -2;
+  }
+}
+
+
 template <int PREC, int METHOD, int S, int NW, int DCN, int DVN>
 int launch_w(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, int blocks,
              hipStream_t st) {
@@ -991,6 +1254,20 @@ int launch_walk(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, in
                 int prec, int slots, int nw, int blocks, void *stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (w.KB > 4 || w.mo > 4 || w.epoch == 0 || w.epoch >= (1u << 23)) return -2;
+  // LDPC_WALK_MW=1: workgroup decoders for sum-product / min-sum (codes with
+  // <= 4 edge slots)
+  const bool mw = getenv("LDPC_WALK_MW") && getenv("LDPC_WALK_MW")[0] == '1';
+  if (mw && method <= 1 && slots <= 4) {
+    if (nw == 1) {
+      if (method == 1)
+        return prec == 1 ? walk_mw_slots<1, 1, 1>(code, a, w, slots, st)
+             : prec == 2 ? walk_mw_slots<2, 1, 1>(code, a, w, slots, st)
+             : prec == 3 ? walk_mw_slots<3, 1, 1>(code, a, w, slots, st)
+                         : walk_mw_slots<0, 1, 1>(code, a, w, slots, st);
+      return prec == 1 ? walk_mw_slots<1, 0, 1>(code, a, w, slots, st)
+                       : walk_mw_slots<0, 0, 1>(code, a, w, slots, st);
+    }
+  }
   if (nw == 1) return walk_nw<1>(code, a, w, method, prec, slots, blocks, st);
   if (nw == 4) return walk_nw<4>(code, a, w, method, prec, slots, blocks, st);
   return -2;
