@@ -454,12 +454,13 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
         sys.path.insert(0, REPO)
         from oracle import oracle as orc
     # (name, Eb/N0, iterations, CPU sample in frames: ~3-15 s of one core each)
-    runs = (("in-sync stream (4 dB)", 4.0, args.iters, cpu_frames, False),
-            ("2 dB stream (sync losses)", 2.0, args.iters, cpu_frames // 2, False),
+    runs = (("in-sync stream (4 dB)", 4.0, args.iters, cpu_frames, None),
+            ("2 dB stream (sync losses)", 2.0, args.iters, cpu_frames // 2, None),
             # make(method) as the reference builds it: 5 iterations (:40)
-            ("make(1) defaults, 5 iterations, 4 dB", 4.0, 5, cpu_frames, False),
-            # the same stream through the device-side frame loop (LDPC_BLOCK_WALK=1)
-            ("make(1) defaults, 5 iterations, 4 dB, device walk", 4.0, 5, cpu_frames, True))
+            ("make(1) defaults, 5 iterations, 4 dB", 4.0, 5, cpu_frames, None),
+            # the same stream through the block's other path, the device-side
+            # frame loop (LDPC_BLOCK_WALK=1; the default is the host planner)
+            ("make(1) defaults, 5 iterations, 4 dB, device walk", 4.0, 5, cpu_frames, "1"))
     last_ref = None
     for name, ebn0, iters, n_cpu, walk in runs:
         dec = L.Decoder(device=dev.index or 0)
@@ -470,8 +471,8 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
         stream = np.zeros(2 * y.numel(), np.float32)
         stream[0::2] = y.cpu().numpy().ravel()
         cx = stream.view(np.complex64)
-        if walk:
-            os.environ["LDPC_BLOCK_WALK"] = "1"
+        if walk is not None:
+            os.environ["LDPC_BLOCK_WALK"] = walk
         try:
             blk = blocks.ldpc_decoder_cb(1, iterations=iters, precision=0, device=dev.index or 0)
         finally:
@@ -482,7 +483,7 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
                      "launches_per_call": round(launches / max(1, calls), 2),
                      "windows_per_output_frame": round(windows / max(1, made // 4), 2),
                      "bytes_out": int(made)}
-        if walk and last_ref is not None:  # the previous run's CPU restatement, same stream
+        if walk is not None and last_ref is not None:  # the earlier run's CPU restatement, same stream
             gpu_bytes = drive_stream.last_out
             out[name]["bytes_equal_cpu_prefix"] = bool(
                 gpu_bytes.size >= last_ref.size and (gpu_bytes[:last_ref.size] == last_ref).all())

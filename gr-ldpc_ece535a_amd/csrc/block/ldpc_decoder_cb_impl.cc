@@ -193,6 +193,18 @@ void ldpc_decoder_cb_impl::adopt(ldpc_ctx *ctx) {
   d_M = (unsigned)M;
   d_N = (unsigned)N;
   d_out_bytes = M / 8;
+  // a walk that may run: load its kernel now, with one window of zeros (its
+  // first launch costs milliseconds; a call's timing should not)
+  if (d_walk_mode == 1 || (d_walk_mode < 0 && d_iterations <= 10)) {
+    std::vector<float> z((size_t)2 * N, 0.0f);
+    std::vector<uint8_t> o((size_t)std::max(d_out_bytes, 1)), m(64);
+    ldpc_walk_io io{};
+    io.last_pass = INT64_MIN / 4;
+    io.anchor_pos = -1;
+    const int rc = ldpc_walk_span(ctx, d_method, (int)d_iterations, d_precision, z.data(),
+                                  2 * (int64_t)N, 2, 0, d_out_bytes, &io, o.data(), m.data(), 64);
+    if (rc == LDPC_EUNSUPPORTED) d_walk = false;
+  }
 }
 
 ldpc_decoder_cb_impl::ldpc_decoder_cb_impl(int method, int iterations, ldpc_block_backend_fn fn,
@@ -582,9 +594,14 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   unsigned char *out = (unsigned char *)output_items[0];
   const int N = (int)d_N;
   const int nin = ninput_items[0];
-  if (d_walk && !d_backend) {
+  const bool walk = pick_walk();
+  const double t_pick = d_walk_mode < 0 ? now_s() : 0.0;
+  if (walk) {
     int produced = 0;
-    if (walk_call(in, nin, noutput_items, out, produced)) return produced;
+    if (walk_call(in, nin, noutput_items, out, produced)) {
+      if (d_walk_mode < 0) note_cost(true, 1e6 * (now_s() - t_pick), produced);
+      return produced;
+    }
   }
   const size_t npos = (size_t)std::max(nin - N + 1, 0);
   // the memo and the jump table keep their size between calls: only the
@@ -719,7 +736,26 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   d_errors = r.errors;
   d_abs += r.consumed;
   consume_each(r.consumed);
+  if (d_walk_mode < 0 && !walk) note_cost(false, 1e6 * (now_s() - t_pick), r.produced);
   return r.produced;
+}
+
+bool ldpc_decoder_cb_impl::pick_walk() {
+  if (d_backend || !d_walk || d_walk_mode == 0) return false;
+  if (d_walk_mode == 1) return true;
+  if (d_iterations > 10) return false;
+  ++d_auto_calls;
+  if (d_cost[0] == 0.0) return false;  // the planner first (the first call also acquires)
+  if (d_cost[1] == 0.0) return true;
+  const bool better = d_cost[1] < d_cost[0];
+  return d_auto_calls % 32 == 0 ? !better : better;
+}
+
+void ldpc_decoder_cb_impl::note_cost(bool walk, double us, int produced) {
+  if (produced < 256) return;  // a short call says little
+  const double c = us / produced;
+  double &e = d_cost[walk ? 1 : 0];
+  e = e == 0.0 ? c : 0.75 * e + 0.25 * c;
 }
 
 }  // namespace ldpc_ece535a

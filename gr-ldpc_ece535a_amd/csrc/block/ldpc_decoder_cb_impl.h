@@ -60,10 +60,23 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   bool d_stage_thread = !(getenv("LDPC_BLOCK_STAGE_THREAD") && getenv("LDPC_BLOCK_STAGE_THREAD")[0] == '0');
   void stage_async(const float *in, int64_t n_floats, int max_windows);
   int stage_wait();
-  // LDPC_BLOCK_WALK=1: the whole frame loop of a call as one device launch
-  // (ldpc_walk_span); otherwise, with a backend, or for a code the walk does
-  // not take: the host planner below (dry-run replay + window launches)
-  bool d_walk = getenv("LDPC_BLOCK_WALK") && getenv("LDPC_BLOCK_WALK")[0] == '1';
+  // Two ways to run a call, same outputs: the host planner below (dry-run
+  // replay + window launches; the default) or the whole frame loop as one
+  // device launch (ldpc_walk_span; LDPC_BLOCK_WALK=1).  LDPC_BLOCK_WALK=auto:
+  // at iteration caps <= 10 the block times both on its own stream and keeps
+  // the faster, trying the other again every 32 calls (measured: the two tie
+  // at 4 dB, the planner is 3x faster at 2 dB, and the probes cost more than
+  // they gain over a short stream -- profiles/round4/block/walk/).  A backend,
+  // or a code the walk does not take: the planner.
+  int d_walk_mode = !getenv("LDPC_BLOCK_WALK")              ? 0
+                    : getenv("LDPC_BLOCK_WALK")[0] == '1'   ? 1
+                    : getenv("LDPC_BLOCK_WALK")[0] == 'a'   ? -1
+                                                            : 0;
+  bool d_walk = true;              // the walk takes this code (until it says otherwise)
+  double d_cost[2] = {0.0, 0.0};   // auto: us per output byte, planner / walk (decayed)
+  int64_t d_auto_calls = 0;
+  bool pick_walk();
+  void note_cost(bool walk, double us, int produced);
   std::vector<uint8_t> d_walk_msgs;
   int64_t d_walk_calls = 0, d_walk_fallbacks = 0;
   double d_walk_prof[3] = {0, 0, 0};  // host call, device loop, device waits (us)
