@@ -1,17 +1,18 @@
 // ldpc_graph_msn.hip -- large-code min-sum with the
 // gathered state kept in one XCD's L2.
 //
-// Same arithmetic as ldpc_graph_ms.hip (the reference's horizontal and
-// vertical steps, lib/ldpc_decoder_cb_impl.cc:340-403, with a row's L(r)
-// recovered exactly from {m1, m2, i1, P} and a 2-bit alpha per edge), laid
-// out for the cache hierarchy instead of for one wave per 64 frames:
+// The reference's horizontal and vertical steps (lib/ldpc_decoder_cb_impl.cc:
+// 340-403) with a row's L(r) recovered exactly from {m1, m2, i1, P} and a
+// 2-bit alpha per edge (the compressed messages of the round-2 64-frame
+// pipeline, retired in round 4), laid out for the cache hierarchy:
 //
-// * Narrow chunks.  A chunk holds F = 4 frames (element x of frame f at
-//   (k * n + x) * F + f), so the tables a pass gathers from -- LQ in the check
-//   pass (8 N F bytes = 2.1 MB for N = 64800), the row state {m1, m2, meta}
-//   in the variable pass (17 M F = 2.2 MB) -- fit one XCD's 4 MiB L2.  With
-//   64-frame chunks they were 33-35 MB, every gather went to the Infinity
-//   Cache (~8 TB/s) and the passes moved 8.4 MB per frame-iteration.
+// * Narrow chunks.  A chunk holds F = kF frames (2 since round 4; element x
+//   of frame f at (k * n + x) * F + f), so the tables a pass gathers from --
+//   LQ in the check pass (8 N F bytes = 1.05 MB for N = 64800 at F = 2), the
+//   row state {m1, m2, meta} in the variable pass (17 M F = 1.1 MB) -- fit
+//   one XCD's 4 MiB L2.  With 64-frame chunks they were 33-35 MB, every
+//   gather went to the Infinity Cache (~8 TB/s) and the passes moved 8.4 MB
+//   per frame-iteration.
 // * XCD-aware placement.  Workgroup b runs on XCD b mod 8; chunk k's blocks
 //   are the ones with b mod 8 == k mod 8, in chunk order, so each XCD works
 //   through its chunks one after another and a chunk's table is gathered
@@ -762,9 +763,10 @@ void msn_pass(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int par, 
 int msn_default_chunks() {
   const char *e = getenv("LDPC_MSN_CHUNKS");  // A/B knob
   const int v = e ? atoi(e) : 0;
-  // 40 chunks = 160 frames in flight, 5 per XCD, 222 MB of chunk state (the
-  // 256 MB Infinity Cache holds it): 2 283-2 291 Mbit/s against 2 223-2 235
-  // for 32 and 2 189-2 201 for 48 (profiles/round3/msn/chunks_fused.txt)
+  // 80 chunks of 2 frames = 160 frames in flight, 10 chunks per XCD:
+  // 2 518-2 522 Mbit/s against 2 486 for 64, 2 469 for 96 and 2 104 for 112
+  // (profiles/round4/msn_chunks/; round 3 at 4 frames per chunk: 40 chunks,
+  // profiles/round3/msn/chunks_fused.txt)
   return v >= 1 ? v : 80;
 }
 
