@@ -440,7 +440,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       guessed_out = !pass;
       // a frame in sync is also wanted at the other polarity when its result
       // decides a sync loss's "-tx" retry (:178-187)
-      if (pass && (d_spec_both == 1 || (d_spec_both > 1 && 8 * d_grid_fails > d_grid_frames)))
+      if (pass && (d_spec_both == 1 || (d_spec_both > 1 && grid_fails_often())))
         want(pos, pol ^ 1, nin);
       if (!pass && r.state == STATE_OUT_OF_SYNC) d_forks.push_back(pos);
     }
@@ -502,8 +502,8 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       if (inverted) std::cout << "IN SYNC; PHASE INVERTED" << std::endl;
       if (synced) std::cout << "IN SYNC" << std::endl;
     }
-    if (!exact && d_searches > 0 && guessed_out && n.state == STATE_OUT_OF_SYNC &&
-        out_run == 0 && searches++ >= d_searches)
+    if (!exact && d_searches_now > 0 && guessed_out && n.state == STATE_OUT_OF_SYNC &&
+        out_run == 0 && searches++ >= d_searches_now)
       return STALLED;  // a later search: the first one likely syncs off the grid first
     r = n;
     if (!exact) {
@@ -681,6 +681,8 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       cap = std::min(d_max_want, cap);
     else if (d_max_want == 0 && d_iterations >= 20 && 8 * d_grid_fails <= d_grid_frames)
       cap = std::min(1024, cap);
+    d_searches_now = d_searches >= 0 ? d_searches
+                                     : (d_iterations <= 10 && !grid_fails_often() ? 4 : 0);
     replay(dry, false, nin, noutput_items, nullptr, out_budget, (size_t)cap);
     // then the branches where a search position passes, nearest first, while
     // the launch has room: windows up to about one per wave slot of the GPU

@@ -88,9 +88,14 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   static double now_s();
   // In-sync frames guessed to pass are also wanted at the other polarity
   // (LDPC_BLOCK_SPEC_BOTH):
-  // 0: never, 1: always, otherwise (default) when more than 1 in 8 frames on
-  // the grid fail (then sync losses, and their retries, are frequent)
+  // 0: never, 1: always, otherwise (default) when more than 1 in d frames on
+  // the grid fail (then sync losses, and their retries, are frequent; the
+  // reference's 4 dB stream fails 1 in 4..8, 2 dB more than 1 in 2).
+  // d = LDPC_BLOCK_SPEC_DIV, default 4 (was 8: at 4 dB / 5 iterations it
+  // requested every grid frame twice, 9.1 windows per output frame)
   int d_spec_both = getenv("LDPC_BLOCK_SPEC_BOTH") ? atoi(getenv("LDPC_BLOCK_SPEC_BOTH")) : 2;
+  int d_spec_div = getenv("LDPC_BLOCK_SPEC_DIV") ? std::max(1, atoi(getenv("LDPC_BLOCK_SPEC_DIV"))) : 4;
+  bool grid_fails_often() const { return d_spec_div * d_grid_fails > d_grid_frames; }
   double d_grid_frames = 0, d_grid_fails = 0;  // decayed counts of in-sync frames
   // A/B knob: LDPC_BLOCK_FORK=1 also decodes the branches where a search position syncs
   bool d_fork = getenv("LDPC_BLOCK_FORK") && getenv("LDPC_BLOCK_FORK")[0] == '1';
@@ -101,7 +106,14 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   // with high probability (~1 % per window, ~126 windows) and the searches
   // after such a false sync move, yet a limit of 1 or 2 costs more launches
   // than the windows it saves (tools/block_policy_sim.py)
-  int d_searches = getenv("LDPC_BLOCK_SEARCHES") ? atoi(getenv("LDPC_BLOCK_SEARCHES")) : 0;
+  // Default (unset): 4 for short windows (iterations <= 10) while the grid
+  // rarely fails, no limit otherwise: at 4 dB / 5 iterations 26 launches of
+  // 3.7 windows per output frame beat 14 of 9.1 (128 vs 119 and
+  // 123 vs 117.5 Mbit/s on two boxes, profiles/round4/block/ab_spec_searches.txt); where a launch costs a
+  // 50-iteration window's latency, or searches are frequent, the extra
+  // launches cost more than the windows they save
+  int d_searches = getenv("LDPC_BLOCK_SEARCHES") ? atoi(getenv("LDPC_BLOCK_SEARCHES")) : -1;
+  int d_searches_now = 0;  // this dry run's limit
   // out-of-sync positions a dry run may guess past in a row before the launch
   // (LDPC_BLOCK_SEARCH_FIRST, default 128; x4 per launch while the search goes on)
   int d_search_first = getenv("LDPC_BLOCK_SEARCH_FIRST") ? atoi(getenv("LDPC_BLOCK_SEARCH_FIRST"))

@@ -9,7 +9,7 @@
 //   g++ -O2 -std=c++17 -Igr-ldpc_ece535a_amd/csrc/block -Igr-ldpc_ece535a_amd/include \
 //       -Iinclude tools/native/block_plan_cost.cc gr-ldpc_ece535a_amd/csrc/block/*.cc \
 //       -Lgr-ldpc_ece535a_amd/lib -lldpc_hip -Wl,-rpath,$PWD/gr-ldpc_ece535a_amd/lib -o /tmp/bpc
-//   /tmp/bpc x.bin synd.bin packed.bin <chunk frames> <reps>
+//   /tmp/bpc x.bin synd.bin packed.bin <chunk frames> <reps> [iterations, default 50]
 // one block, a long periodic stream (the table's stream repeated): steady-state planning cost
 #include <ldpc_block.h>
 #include <chrono>
@@ -35,7 +35,8 @@ int main(int argc, char **argv) {
   for (int r = 0; r < reps; ++r) memcpy(big.data() + (size_t)r * S * 2, x.data(), x.size());
   T t{big.data(), (const int32_t *)s.data(), (const uint8_t *)k.data(), (int64_t)(s.size() / 8), S};
   int dn = open("/dev/null", O_WRONLY); dup2(dn, 1);
-  ldpc_block *b = ldpc_decoder_cb_make_with_backend(1, 50, fn, &t);
+  const int iters = argc > 6 ? atoi(argv[6]) : 50;  // the planner's launch cap depends on it
+  ldpc_block *b = ldpc_decoder_cb_make_with_backend(1, iters, fn, &t);
   int64_t nS = S * reps, pos = 0; std::vector<uint8_t> out(chunk / 16 + 16); int calls = 0; long long l0 = 0;
   auto t0 = std::chrono::steady_clock::now();
   while (pos + 64 <= nS) { int used = 0; int n = (int)std::min<int64_t>(chunk, nS - pos);
