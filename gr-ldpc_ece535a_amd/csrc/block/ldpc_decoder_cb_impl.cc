@@ -189,6 +189,8 @@ void ldpc_decoder_cb_impl::adopt(ldpc_ctx *ctx) {
   if (getenv("LDPC_BLOCK_TP") && getenv("LDPC_BLOCK_TP")[0] == '1')
     (void)ldpc_set_launch_mode(ctx, LDPC_MODE_THROUGHPUT);
   if (getenv("LDPC_BLOCK_WPC")) (void)ldpc_set_waves_per_cu(ctx, atoi(getenv("LDPC_BLOCK_WPC")));
+  // A/B knob: LDPC_BLOCK_SCHEDULE=1|2 forces the one-wave / workgroup form for every launch
+  if (getenv("LDPC_BLOCK_SCHEDULE")) (void)ldpc_set_schedule(ctx, atoi(getenv("LDPC_BLOCK_SCHEDULE")));
   d_ctx = ctx;
   d_M = (unsigned)M;
   d_N = (unsigned)N;
