@@ -126,20 +126,21 @@ def sigma_of(ebn0):
 _STREAMS = {}
 
 
-def bench_streams(torch, dev, n):
-    """n streams for one measurement: fresh ones (default, as every round so
-    far), or with LDPC_BENCH_STREAMS=shared one set created at startup and
-    reused.  Which hardware queues (GPU_MAX_HW_QUEUES = 4) the in-flight
-    batches' streams share depends on the streams the process made before
-    them: measured four batches in flight at 800 instead of 1 120 Mbit/s after
-    ten extra streams, and with the shared set (profiles/round4/headline/)."""
-    if os.environ.get("LDPC_BENCH_STREAMS", "fresh") == "fresh":
-        return [torch.cuda.Stream(dev) for _ in range(n)]
-    key = (str(dev),)
-    have = _STREAMS.setdefault(key, [])
-    while len(have) < n:
-        have.append(torch.cuda.Stream(dev))
-    return have[:n]
+def side_stream(torch, dev):
+    """The one torch stream the bench makes its data on (every synth_device
+    call): the decode launches themselves run on the decoder context's own
+    in-flight streams (ldpc_ctx_streams, each on its own hardware queue), so
+    what the process made before does not decide which of them overlap."""
+    key = str(dev)
+    if key not in _STREAMS:
+        _STREAMS[key] = torch.cuda.Stream(dev)
+    return _STREAMS[key]
+
+
+def ctx_streams(torch, dec, dev, n):
+    """The decoder context's n in-flight streams as torch streams (for the
+    HIP events that time them)."""
+    return [torch.cuda.ExternalStream(h, device=dev) for h in dec.streams(n)]
 
 
 def synth_device(L, torch, dec, B, ebn0, seed, dev, check_frames=64):
@@ -150,7 +151,7 @@ def synth_device(L, torch, dec, B, ebn0, seed, dev, check_frames=64):
     K, N = dec.K, dec.N
     # one explicit (non-null) stream for every step: a NULL stream argument
     # would mean the context's own stream for ldpc_encode_device
-    st = bench_streams(torch, dev, 1)[0]
+    st = side_stream(torch, dev)
     sp = ctypes.c_void_p(st.cuda_stream)
     with torch.cuda.stream(st):
         d_bits = torch.empty((B, K), dtype=torch.uint8, device=dev)
@@ -287,7 +288,7 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
     D = max(1, inflight)
     dev = inputs[0].device
     if streams is None:
-        streams = bench_streams(torch, dev, D)
+        streams = ctx_streams(torch, dec, dev, D)
     sps = [ctypes.c_void_p(s.cuda_stream) for s in streams]
     outs = [(torch.empty((B, dec.KB), dtype=torch.uint8, device=dev),
              torch.empty(B, dtype=torch.int32, device=dev),
@@ -594,9 +595,8 @@ def config5_variant(L, torch, args, dev, sizes=(1, 16, 256, 4096, 65536), check_
                     "cap, one launch at a time (latency mode); latency = HIP-event span per "
                     "launch"}
     kept = {}
-    # one stream for all of it: every stream a process creates shifts which
-    # hardware queues the headline's streams get (profiles/round4/headline/)
-    c5_stream = [torch.cuda.Stream(dev)]
+    # one launch at a time: the context's first in-flight stream
+    c5_stream = ctx_streams(torch, dec, dev, 1)
     for name, m in (("sum-product f64 (exact)", 1), ("min-sum f64", 0)):
         rows = {}
         for Bs in sizes:
@@ -787,8 +787,6 @@ def main():
     if args.batch is None:
         args.batch = 1024 if dvb else 4096
     D = max(1, args.inflight)
-    if os.environ.get("LDPC_BENCH_STREAMS", "fresh") != "fresh":
-        bench_streams(torch, dev, max(4, D))
 
     csr = None
     if dvb:

@@ -195,6 +195,30 @@ void ldpc_decoder_cb_impl::adopt(ldpc_ctx *ctx) {
   d_M = (unsigned)M;
   d_N = (unsigned)N;
   d_out_bytes = M / 8;
+  // the window server: load its kernel now with one round of one window of
+  // zeros (a kernel's first launch costs milliseconds); codes or methods it
+  // does not take keep a launch per round
+  if (d_serve && (d_method == 0 || d_method == 1)) {
+    std::vector<float> z((size_t)2 * N, 0.0f);
+    int rc = ldpc_stage_span(ctx, z.data(), 2 * (int64_t)N, 2, 1);
+    if (rc == LDPC_OK) rc = ldpc_serve_begin(ctx, d_method, (int)d_iterations, d_precision, 1);
+    if (rc == LDPC_OK) {
+      const int64_t key = 0;
+      std::vector<uint8_t> pk((size_t)std::max(1, (N - M + 7) / 8));
+      int32_t sy = 0;
+      rc = ldpc_serve_windows(ctx, &key, 1, pk.data(), &sy);
+      (void)ldpc_serve_end(ctx);
+    }
+    if (rc == LDPC_EUNSUPPORTED) d_serve = false;
+    else if (rc < 0) {
+      const std::string why = ldpc_last_error(ctx);
+      ldpc_destroy(ctx);
+      d_ctx = nullptr;
+      throw std::runtime_error("ldpc_decoder_cb: window server: " + why);
+    }
+  } else {
+    d_serve = false;
+  }
   // a walk that may run: load its kernel now, with one window of zeros (its
   // first launch costs milliseconds; a call's timing should not)
   if (d_walk_mode == 1 || (d_walk_mode < 0 && d_iterations <= 10)) {
@@ -217,10 +241,26 @@ ldpc_decoder_cb_impl::ldpc_decoder_cb_impl(int method, int iterations, ldpc_bloc
   d_backend_user = user;
 }
 
+int ldpc_decoder_cb_impl::Stager::run() {
+  const int r = ldpc_stage_span(ctx, in, n, 2, max_windows);
+  serve_rc = LDPC_EUNSUPPORTED;
+  if (r == LDPC_OK && serve) serve_rc = ldpc_serve_begin(ctx, method, iterations, precision, max_windows);
+  return r;
+}
+
 void ldpc_decoder_cb_impl::stage_async(const float *in, int64_t n_floats, int max_windows) {
   Stager &sg = d_stager;
+  const bool serve = d_serve && (d_method == 0 || d_method == 1);
   if (!d_stage_thread) {
-    sg.rc = ldpc_stage_span(d_ctx, in, n_floats, 2, max_windows);
+    sg.ctx = d_ctx;
+    sg.in = in;
+    sg.n = n_floats;
+    sg.max_windows = max_windows;
+    sg.serve = serve;
+    sg.method = d_method;
+    sg.iterations = (int)d_iterations;
+    sg.precision = d_precision;
+    sg.rc = sg.run();
     return;
   }
   if (!sg.th.joinable())
@@ -230,7 +270,7 @@ void ldpc_decoder_cb_impl::stage_async(const float *in, int64_t n_floats, int ma
         sg.cv.wait(lk, [&sg]() { return sg.busy || sg.quit; });
         if (sg.quit) return;
         lk.unlock();
-        const int rc = ldpc_stage_span(sg.ctx, sg.in, sg.n, 2, sg.max_windows);
+        const int rc = sg.run();
         lk.lock();
         sg.rc = rc;
         sg.busy = false;
@@ -242,15 +282,25 @@ void ldpc_decoder_cb_impl::stage_async(const float *in, int64_t n_floats, int ma
   sg.in = in;
   sg.n = n_floats;
   sg.max_windows = max_windows;
+  sg.serve = serve;
+  sg.method = d_method;
+  sg.iterations = (int)d_iterations;
+  sg.precision = d_precision;
   sg.busy = true;
   sg.cv.notify_all();
 }
 
 int ldpc_decoder_cb_impl::stage_wait() {
   Stager &sg = d_stager;
-  if (!d_stage_thread) return sg.rc;
-  std::unique_lock<std::mutex> lk(sg.mu);
-  sg.cv.wait(lk, [&sg]() { return !sg.busy; });
+  if (d_stage_thread) {
+    std::unique_lock<std::mutex> lk(sg.mu);
+    sg.cv.wait(lk, [&sg]() { return !sg.busy; });
+  }
+  if (sg.rc == LDPC_OK && sg.serve) {
+    d_serving = sg.serve_rc == LDPC_OK;
+    if (sg.serve_rc == LDPC_EUNSUPPORTED) d_serve = false;  // this code / method: launches
+    else if (sg.serve_rc < 0) return sg.serve_rc;
+  }
   return sg.rc;
 }
 
@@ -314,6 +364,11 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
       if (rc < 0) throw std::runtime_error("ldpc_decoder_cb: decode failed: backend error");
       i = j;
     }
+  } else if (d_serving) {
+    const int rc = ldpc_serve_windows(d_ctx, d_want.data(), B, packed, synd);
+    if (rc < 0)
+      throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
+                               ldpc_last_error(d_ctx));
   } else {
     const int rc = ldpc_decode_windows(d_ctx, d_method, (int)d_iterations, 1, d_precision, in,
                                        2 * (int64_t)nin, 2, first ? 0 : 1, d_want.data(), B,
@@ -736,6 +791,10 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
     }
   }
   join_stage();  // no launch this call: the staging must still finish
+  if (d_serving) {  // the call's window server may finish (no wait)
+    d_serving = false;
+    (void)ldpc_serve_end(d_ctx);
+  }
   d_state = r.state;
   d_errors = r.errors;
   d_abs += r.consumed;

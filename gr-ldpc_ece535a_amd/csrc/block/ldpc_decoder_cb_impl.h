@@ -46,6 +46,9 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   // copied into pinned memory and sent to the device) while general_work
   // plans its first launch; joined before that launch.  LDPC_BLOCK_STAGE_THREAD=0:
   // staged inline.
+  // With the window server (ldpc_serve_begin: one persistent launch serves
+  // every round of the call) the worker also starts the launch, right behind
+  // the span's copy in the context's stream.
   struct Stager {
     std::thread th;
     std::mutex mu;
@@ -56,8 +59,17 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
     const float *in = nullptr;
     int64_t n = 0;
     int max_windows = 0;
+    bool serve = false;          // start the window server after staging
+    int method = 0, iterations = 0, precision = 0;
+    int serve_rc = 0;            // ldpc_serve_begin's result
+    int run();                   // stage (+ serve); returns the staging result
   } d_stager;
   bool d_stage_thread = !(getenv("LDPC_BLOCK_STAGE_THREAD") && getenv("LDPC_BLOCK_STAGE_THREAD")[0] == '0');
+  // Rounds of windows through the window server (ldpc_serve_*), one launch
+  // per call; false: a launch per round (ldpc_decode_windows), and for codes
+  // or methods the server does not take (LDPC_BLOCK_SERVE=0 forces it, A/B).
+  bool d_serve = !(getenv("LDPC_BLOCK_SERVE") && getenv("LDPC_BLOCK_SERVE")[0] == '0');
+  bool d_serving = false;  // this call's server is running
   void stage_async(const float *in, int64_t n_floats, int max_windows);
   int stage_wait();
   // Two ways to run a call, same outputs: the host planner below (dry-run

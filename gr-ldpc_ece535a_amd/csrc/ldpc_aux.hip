@@ -216,4 +216,33 @@ int launch_gather_windows(const float *span, const int64_t *win, int B, int N, f
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// Stream concurrency probe (ldpc_ctx_streams): k_probe_wait spins on a flag
+// for at most `deadline` ticks of the 100 MHz clock and records what it saw;
+// k_probe_set raises the flag.  Enqueued on two streams, the wait sees the
+// flag only if the two run at the same time -- on one hardware queue the set
+// runs after the wait has given up.
+namespace {
+__global__ void __launch_bounds__(64) k_probe_wait(uint32_t *flag, uint64_t deadline) {
+  if (threadIdx.x != 0) return;
+  typedef __attribute__((address_space(1))) uint32_t gu32;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t v = 0;
+  while ((v = __hip_atomic_load((gu32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u &&
+         __builtin_amdgcn_s_memrealtime() - t0 < deadline)
+    __builtin_amdgcn_s_sleep(2);
+  __hip_atomic_store((gu32 *)(flag + 1), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void __launch_bounds__(64) k_probe_set(uint32_t *flag) {
+  typedef __attribute__((address_space(1))) uint32_t gu32;
+  if (threadIdx.x == 0) __hip_atomic_store((gu32 *)flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace
+
+int launch_probe_pair(uint32_t *flag, uint64_t deadline, void *wait_stream, void *set_stream) {
+  hipLaunchKernelGGL(k_probe_wait, dim3(1), dim3(64), 0, (hipStream_t)wait_stream, flag, deadline);
+  if (hipGetLastError() != hipSuccess) return -3;
+  hipLaunchKernelGGL(k_probe_set, dim3(1), dim3(64), 0, (hipStream_t)set_stream, flag);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 }  // namespace ldpc

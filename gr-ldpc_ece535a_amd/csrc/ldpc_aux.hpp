@@ -22,4 +22,8 @@ int launch_encode_ira(const int32_t *rp, const int32_t *ci, int M, int K, const 
 int launch_gather_windows(const float *span, const int64_t *win, int B, int N, float *out,
                           void *stream);
 
+// flag[0] = 0 and flag[1] = 0 beforehand; afterwards flag[1] == 1 iff the two
+// streams ran the pair concurrently (ldpc_aux.hip)
+int launch_probe_pair(uint32_t *flag, uint64_t deadline, void *wait_stream, void *set_stream);
+
 }  // namespace ldpc

@@ -69,6 +69,21 @@ struct ldpc_ctx {
   uint32_t walk_epoch = 0;
   uint8_t *h_walk = nullptr;
   size_t h_walk_bytes = 0;
+  // the window server (ldpc_serve.hip, ldpc_serve_*): mapped pinned memory
+  // [round word | keys | result granules] for srv_cap windows, the device
+  // copy of the round word, and the running launch's parameters
+  bool serving = false;
+  uint8_t *h_srv = nullptr;
+  int64_t srv_cap = 0;
+  uint64_t *d_srv_ctl = nullptr;
+  uint32_t srv_epoch = 0;  // the last round posted (grows across launches)
+  int srv_method = 0, srv_iters = 0, srv_prec = 0;
+  int srv_launches = 0, srv_rounds = 0;
+  int srv_workgroups = 0;  // decoder workgroups of the running launch
+  // in-flight stream set for throughput callers (ldpc_ctx_streams): streams
+  // verified to run concurrently, i.e. on distinct hardware queues
+  std::vector<hipStream_t> tp_streams;
+  uint32_t *d_probe = nullptr;
   // large-code min-sum: 2 narrow-chunk pipeline (ldpc_graph_msn.hip), 0 the
   // edge-message passes (ldpc_graph.hip)
   int ms_mode = 2;
@@ -303,6 +318,31 @@ int build_tables(ldpc_ctx *ctx, std::vector<EdgeRowRec> &erecs, std::vector<Edge
   return LDPC_OK;
 }
 
+
+// ---- the window server (ldpc_serve_*) --------------------------------------
+// Mapped pinned memory: the round word (its own 256 bytes), the keys, the
+// result granules.
+size_t srv_keys_off() { return 256; }
+size_t srv_res_off(int64_t cap) { return 256 + (((size_t)cap * 8 + 255) & ~(size_t)255); }
+size_t srv_bytes(int64_t cap) { return srv_res_off(cap) + (size_t)cap * 8; }
+
+// Posts round word (epoch << 32) | B after the keys (x86 stores are ordered;
+// the device reads the keys only after it has seen the round word).
+void serve_post(ldpc_ctx *ctx, uint32_t B) {
+  ++ctx->srv_epoch;  // < 2^23: ldpc_serve_begin restarts the epochs well before
+  __atomic_store_n(reinterpret_cast<uint64_t *>(ctx->h_srv),
+                   ((uint64_t)ctx->srv_epoch << 32) | B, __ATOMIC_RELEASE);
+}
+
+// Ends a running window server: posts its quit round and waits for the
+// launch to finish, so whatever the caller enqueues next does not queue
+// behind a launch that polls for rounds.
+void serve_stop(ldpc_ctx *ctx) {
+  if (!ctx || !ctx->serving) return;
+  serve_post(ctx, ldpc::kServeQuit);
+  ctx->serving = false;
+  (void)hipStreamSynchronize(ctx->stream);
+}
 
 int ensure_stage(ldpc_ctx *ctx, size_t bytes) {
   if (bytes <= ctx->stage_bytes) return LDPC_OK;
@@ -911,6 +951,7 @@ ldpc_ctx *ldpc_create_csr(int M, int N, const int32_t *row_ptr, const int32_t *c
 
 void ldpc_destroy(ldpc_ctx *ctx) {
   if (!ctx) return;
+  serve_stop(ctx);
   if (ctx->win_profile && ctx->win_calls)
     fprintf(stderr,
             "ldpc_decode_windows profile: %lld calls, %lld windows; staging %.3f ms, window list + "
@@ -931,6 +972,13 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->h_win) (void)hipHostFree(ctx->h_win);
   if (ctx->d_walk) (void)hipFree(ctx->d_walk);
   if (ctx->h_walk) (void)hipHostFree(ctx->h_walk);
+  if (ctx->h_srv) (void)hipHostFree(ctx->h_srv);
+  for (hipStream_t t : ctx->tp_streams) {
+    (void)hipStreamSynchronize(t);
+    (void)hipStreamDestroy(t);
+  }
+  if (ctx->d_probe) (void)hipFree(ctx->d_probe);
+  if (ctx->d_srv_ctl) (void)hipFree(ctx->d_srv_ctl);
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
     if (p) (void)hipFree(p);
@@ -1049,6 +1097,7 @@ int ldpc_plan_layout(const uint8_t *H, int M, int N, int flags, int32_t *cell_ou
 
 int ldpc_encode_device(ldpc_ctx *ctx, const uint8_t *d_data_bits, int B, uint8_t *d_codewords,
                        void *hip_stream) {
+  serve_stop(ctx);
   if (!ctx) return LDPC_EINVAL;
   if (B < 0 || (B > 0 && (!d_data_bits || !d_codewords)))
     return set_err(ctx, LDPC_EINVAL, "bad encoder arguments");
@@ -1111,6 +1160,7 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
                        int32_t *d_iters_used_opt, int32_t *d_syn_weight_opt,
                        float *d_llr_out_opt, void *hip_stream,
                        const int64_t *d_win = nullptr) {
+  serve_stop(ctx);
   int rc = check_decode_args(ctx, method, max_iters, et_period, precision, B, elem_stride,
                              cw_stride);
   if (rc != LDPC_OK) return rc;
@@ -1210,6 +1260,7 @@ int decode_host_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, in
                      const float *in, int64_t n_in_floats, int64_t cw_stride, int elem_stride,
                      float polarity, int B, bool both, uint8_t *out_packed, uint8_t *out_bits_opt,
                      int32_t *iters_used_opt, int32_t *syn_weight_opt, float *llr_out_opt) {
+  serve_stop(ctx);
   int rc = check_decode_args(ctx, method, max_iters, et_period, precision, B, elem_stride,
                              cw_stride);
   if (rc != LDPC_OK) return rc;
@@ -1321,6 +1372,7 @@ int copy_span(ldpc_ctx *ctx, const float *in, int64_t S, int elem_stride, float 
 int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
                         const float *in, int64_t n_in_floats, int elem_stride, int reuse_span,
                         const int64_t *win, int B, uint8_t *out_packed, int32_t *syn_weight_opt) {
+  serve_stop(ctx);
   int rc = check_decode_args(ctx, method, max_iters, et_period, precision, B, elem_stride,
                              ctx ? ctx->N : 1);
   if (rc != LDPC_OK) return rc;
@@ -1469,6 +1521,7 @@ size_t walk_layout(int64_t cap, size_t off[4]) {
 int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, const float *in,
                    int64_t n_in_floats, int elem_stride, int reuse_span, int noutput_bytes,
                    ldpc_walk_io *io, uint8_t *out, uint8_t *msgs, int msgs_cap) {
+  serve_stop(ctx);
   int rc = check_decode_args(ctx, method, max_iters, 1, precision, 1, elem_stride, ctx ? ctx->N : 1);
   if (rc != LDPC_OK) return rc;
   const int N = ctx->N, mo = ctx->M / 8;
@@ -1658,6 +1711,153 @@ int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, cons
   return LDPC_OK;
 }
 
+
+// Launches the window server for the context's parameters on its stream
+// (ctl zeroed first: it must read below every epoch the launch serves).
+int serve_launch(ldpc_ctx *ctx) {
+  hipError_t e;
+  if ((e = hipMemsetAsync(ctx->d_srv_ctl, 0, 256, ctx->stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipMemsetAsync(server ctl)");
+  void *dh = nullptr;
+  if ((e = hipHostGetDevicePointer(&dh, ctx->h_srv, 0)) != hipSuccess)
+    return hip_err(ctx, e, "hipHostGetDevicePointer(server)");
+  ldpc::ServeArgs sa{};
+  sa.round = (const uint64_t *)dh;
+  sa.keys = (const int64_t *)((uint8_t *)dh + srv_keys_off());
+  sa.res = (uint64_t *)((uint8_t *)dh + srv_res_off(ctx->srv_cap));
+  sa.ctl = ctx->d_srv_ctl;
+  const char *dl = getenv("LDPC_SERVE_DEADLINE_MS");
+  sa.deadline = (uint64_t)((dl ? atof(dl) : 200.0) * 1e5);  // 100 MHz ticks
+  sa.start_epoch = ctx->srv_epoch;
+  // decoder workgroups per CU (capped by occupancy); 0 = as many as fit
+  static const int per_cu = getenv("LDPC_SERVE_BLOCKS_PER_CU") ? atoi(getenv("LDPC_SERVE_BLOCKS_PER_CU")) : 0;
+  sa.blocks_per_cu = per_cu;
+  int wg = 0;
+  ldpc::DecodeArgs a{};
+  a.in = (const float *)ctx->d_wstage;
+  a.cw_stride = ctx->N;
+  a.elem_stride = 1;
+  a.polarity = 1.0f;
+  a.max_iters = ctx->srv_iters;
+  a.et_period = 1;
+  const int rc = ldpc::launch_serve(code_view(ctx), a, sa, ctx->srv_method, ctx->srv_prec,
+                                    ctx->slots, ctx->nw, ctx->stream, &wg);
+  ctx->srv_workgroups = wg;
+  if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no window server for this code shape");
+  if (rc != 0) return hip_err(ctx, hipGetLastError(), "window server launch");
+  ctx->srv_launches += 1;
+  return LDPC_OK;
+}
+
+int serve_begin_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, int max_windows) {
+  int rc = check_decode_args(ctx, method, max_iters, 1, precision, 1, 1, ctx ? ctx->N : 1);
+  if (rc != LDPC_OK) return rc;
+  if (ctx->graph || ctx->KB > 4 || (method != 0 && method != 1))
+    return set_err(ctx, LDPC_EUNSUPPORTED,
+                   "the window server takes min-sum / sum-product on small codes with KB <= 4");
+  if (ctx->span_samples <= 0) return set_err(ctx, LDPC_EINVAL, "no staged span (ldpc_stage_span)");
+  if (max_windows < 1 || max_windows > (1 << 19))
+    return set_err(ctx, LDPC_EINVAL, "max_windows must be in [1, 2^19]");
+  if (ctx->serving) {
+    if (ctx->srv_method == method && ctx->srv_iters == max_iters && ctx->srv_prec == precision &&
+        ctx->srv_cap >= max_windows)
+      return LDPC_OK;
+    serve_stop(ctx);
+  }
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  if (!ctx->d_srv_ctl && (e = hipMalloc((void **)&ctx->d_srv_ctl, 256)) != hipSuccess)
+    return hip_err(ctx, e, "hipMalloc(server ctl)");
+  // a new buffer (or epochs near the end of their range) starts the epochs over:
+  // the previous launch has finished first
+  if (ctx->srv_cap < max_windows || ctx->srv_epoch >= (1u << 23) - (1u << 16)) {
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->srv_cap < max_windows) {
+      if (ctx->h_srv) (void)hipHostFree(ctx->h_srv);
+  for (hipStream_t t : ctx->tp_streams) {
+    (void)hipStreamSynchronize(t);
+    (void)hipStreamDestroy(t);
+  }
+  if (ctx->d_probe) (void)hipFree(ctx->d_probe);
+      ctx->h_srv = nullptr;
+      ctx->srv_cap = 0;
+      const int64_t cap = std::max<int64_t>(max_windows, 4096);
+      if ((e = hipHostMalloc((void **)&ctx->h_srv, srv_bytes(cap),
+                             hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+        return hip_err(ctx, e, "hipHostMalloc(server)");
+      ctx->srv_cap = cap;
+    }
+    memset(ctx->h_srv, 0, srv_bytes(ctx->srv_cap));
+    ctx->srv_epoch = 0;
+  }
+  ctx->srv_method = method;
+  ctx->srv_iters = max_iters;
+  ctx->srv_prec = precision;
+  rc = serve_launch(ctx);
+  if (rc != LDPC_OK) return rc;
+  ctx->serving = true;
+  return LDPC_OK;
+}
+
+int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_packed,
+                       int32_t *syn_weight_opt) {
+  if (!ctx) return LDPC_EINVAL;
+  if (!ctx->serving) return set_err(ctx, LDPC_EINVAL, "no window server running (ldpc_serve_begin)");
+  if (B < 0) return set_err(ctx, LDPC_EINVAL, "B < 0");
+  if (B == 0) return LDPC_OK;
+  if (!win || !out_packed) return set_err(ctx, LDPC_EINVAL, "null buffer");
+  const int N = ctx->N, KB = ctx->KB;
+  for (int b = 0; b < B; ++b)
+    if (win[b] < 0 || (win[b] >> 1) + N > ctx->span_samples)
+      return set_err(ctx, LDPC_EINVAL, "window outside the staged span");
+  int64_t *keys = (int64_t *)(ctx->h_srv + srv_keys_off());
+  const uint64_t *res = (const uint64_t *)(ctx->h_srv + srv_res_off(ctx->srv_cap));
+  const double timeout_s = 10.0;
+  for (int b0 = 0; b0 < B; b0 += (int)ctx->srv_cap) {
+    const int n = (int)std::min<int64_t>(ctx->srv_cap, B - b0);
+    memcpy(keys, win + b0, (size_t)n * 8);
+    serve_post(ctx, (uint32_t)n);
+    ctx->srv_rounds += 1;
+    const uint32_t tag = ctx->srv_epoch & 0x7FFFFFu;
+    const auto t0 = std::chrono::steady_clock::now();
+    int relaunches = 0;
+    for (int b = 0; b < n; ++b) {
+      uint64_t g;
+      for (uint32_t spins = 1;; ++spins) {
+        g = __atomic_load_n(res + b, __ATOMIC_ACQUIRE);
+        if ((uint32_t)(g >> 41) == tag) break;
+        if ((spins & 0xFFFu) == 0) {
+          // the launch ended (its deadline passed between rounds): start another
+          const hipError_t q = hipStreamQuery(ctx->stream);
+          if (q == hipSuccess) {
+            if (++relaunches > 4) {
+              ctx->serving = false;
+              return set_err(ctx, LDPC_ETIMEOUT, "the window server keeps ending before its round");
+            }
+            ctx->srv_epoch -= 1;  // the launch serves epochs above start_epoch
+            const int rc = serve_launch(ctx);
+            ctx->srv_epoch += 1;
+            if (rc != LDPC_OK) {
+              ctx->serving = false;
+              return rc;
+            }
+          } else if (q != hipErrorNotReady) {
+            ctx->serving = false;
+            return hip_err(ctx, q, "window server");
+          }
+          if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+            serve_stop(ctx);
+            return set_err(ctx, LDPC_ETIMEOUT, "a window server round passed its timeout");
+          }
+        }
+      }
+      const uint32_t pk = (uint32_t)g;
+      for (int j = 0; j < KB; ++j) out_packed[(size_t)(b0 + b) * KB + j] = (uint8_t)(pk >> (8 * j));
+      if (syn_weight_opt) syn_weight_opt[b0 + b] = (int32_t)((g >> 32) & 511u);
+    }
+  }
+  return LDPC_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -1671,6 +1871,7 @@ int ldpc_walk_span(ldpc_ctx *ctx, int method, int max_iters, int precision, cons
 
 int ldpc_stage_span(ldpc_ctx *ctx, const float *in, int64_t n_in_floats, int elem_stride,
                     int max_windows) {
+  serve_stop(ctx);
   if (!ctx) return LDPC_EINVAL;
   if (!in || elem_stride < 1 || n_in_floats < 0 || max_windows < 0)
     return set_err(ctx, LDPC_EINVAL, "bad span");
@@ -1685,6 +1886,24 @@ int ldpc_stage_span(ldpc_ctx *ctx, const float *in, int64_t n_in_floats, int ele
   int rc = ensure_window_stage(ctx, al((size_t)S * 4) + extra);
   if (rc != LDPC_OK) return rc;
   return copy_span(ctx, in, S, elem_stride, (float *)ctx->d_wstage);
+}
+
+int ldpc_serve_begin(ldpc_ctx *ctx, int method, int max_iters, int precision, int max_windows) {
+  return serve_begin_impl(ctx, method, max_iters, precision, max_windows);
+}
+
+int ldpc_serve_windows(ldpc_ctx *ctx, const int64_t *windows, int B, uint8_t *out_packed,
+                       int32_t *syn_weight_opt) {
+  return serve_windows_impl(ctx, windows, B, out_packed, syn_weight_opt);
+}
+
+int ldpc_serve_end(ldpc_ctx *ctx) {
+  if (!ctx) return LDPC_EINVAL;
+  if (ctx->serving) {  // the launch finishes on its own; the stream orders what follows
+    serve_post(ctx, ldpc::kServeQuit);
+    ctx->serving = false;
+  }
+  return LDPC_OK;
 }
 
 int ldpc_decode_windows(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
@@ -1732,6 +1951,58 @@ int ldpc_decode(ldpc_ctx *ctx, int method, int max_iters, int et_period, int pre
                              iters_used_opt, syn_weight_opt, nullptr);
 }
 
+int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
+  if (!ctx || n < 1 || n > 16 || !streams_out)
+    return set_err(ctx, LDPC_EINVAL, "n must be in [1, 16] with an output array");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  if (!ctx->d_probe && (e = hipMalloc((void **)&ctx->d_probe, 256)) != hipSuccess)
+    return hip_err(ctx, e, "hipMalloc(probe)");
+  // Which hardware queue a stream lands on (GPU_MAX_HW_QUEUES of them) depends
+  // on every stream the process made before it; two streams on one queue run
+  // their launches one after the other.  A candidate joins the set only if a
+  // probe pair runs concurrently with every member; the others are kept until
+  // the set is complete (so the next candidate lands elsewhere), then freed.
+  std::vector<hipStream_t> spare;
+  int rc = LDPC_OK;
+  for (int tries = 0; (int)ctx->tp_streams.size() < n; ++tries) {
+    if (tries >= 8 * n) {
+      rc = set_err(ctx, LDPC_EDEVICE, "no set of concurrent streams of that size");
+      break;
+    }
+    hipStream_t c = nullptr;
+    if ((e = hipStreamCreateWithFlags(&c, hipStreamNonBlocking)) != hipSuccess) {
+      rc = hip_err(ctx, e, "hipStreamCreate");
+      break;
+    }
+    bool ok = true;
+    for (hipStream_t a : ctx->tp_streams) {
+      uint32_t seen = 0;
+      if ((e = hipMemset(ctx->d_probe, 0, 8)) != hipSuccess ||
+          ldpc::launch_probe_pair(ctx->d_probe, 200000 /* 2 ms */, a, c) != 0 ||
+          (e = hipStreamSynchronize(a)) != hipSuccess || (e = hipStreamSynchronize(c)) != hipSuccess ||
+          (e = hipMemcpy(&seen, ctx->d_probe + 1, 4, hipMemcpyDeviceToHost)) != hipSuccess) {
+        rc = hip_err(ctx, e, "stream probe");
+        ok = false;
+        break;
+      }
+      if (seen != 1u) {
+        ok = false;
+        break;
+      }
+    }
+    if (rc != LDPC_OK) {
+      (void)hipStreamDestroy(c);
+      break;
+    }
+    (ok ? ctx->tp_streams : spare).push_back(c);
+  }
+  for (hipStream_t t : spare) (void)hipStreamDestroy(t);
+  if (rc != LDPC_OK) return rc;
+  for (int i = 0; i < n; ++i) streams_out[i] = (void *)ctx->tp_streams[(size_t)i];
+  return LDPC_OK;
+}
+
 int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu) {
   if (!ctx || waves_per_cu < 0 || waves_per_cu > 32)
     return set_err(ctx, LDPC_EINVAL, "waves_per_cu must be in [0, 32]");
@@ -1760,6 +2031,7 @@ int ldpc_set_schedule(ldpc_ctx *ctx, int schedule) {
 }
 
 int ldpc_synchronize(ldpc_ctx *ctx) {
+  serve_stop(ctx);
   if (!ctx) return LDPC_EINVAL;
   hipError_t e = hipStreamSynchronize(ctx->stream);
   return e == hipSuccess ? LDPC_OK : hip_err(ctx, e, "hipStreamSynchronize");

@@ -829,7 +829,7 @@ __device__ __forceinline__ void wave_setup(const CodeView &code, unsigned char *
   }
 }
 
-// LDS of the workgroup-per-frame kernels (decode_mw_kernel, walk_mw_kernel):
+// LDS of the workgroup-per-frame kernels (decode_mw_kernel, serve_mw_kernel):
 // tb / eb per edge cell, per-wave rb / sb, the frame slot
 template <typename Real, int S, int NW>
 struct MwLayout {
@@ -842,5 +842,195 @@ struct MwLayout {
     total = fslot + 16;
   }
 };
+
+// ---------------------------------------------------------------------------
+// Workgroup-per-frame form: one frame on S waves, one edge per lane (thread
+// tid owns edge cell tid), two workgroup barriers per iteration.  The cheap
+// column phase (posterior, hard decision, syndrome) is computed by every wave
+// redundantly from the shared check messages, so every wave reaches the same
+// early-exit decision without a third barrier.  Used by the batch kernel
+// (decode_mw_kernel) and the block's window server (ldpc_serve.hip).
+// ---------------------------------------------------------------------------
+template <int NW>
+struct MwTables {
+  uint32_t rn[4], cn[2], ce[NW][2];  // EdgeRowRec / EdgeColRec of edge tid, ColRec.e per position
+  uint64_t rowmask[NW][NW];
+  int col;                           // the edge's column position (0 for padding)
+  int colq[NW];                      // column at each of the lane's positions (-1: none)
+};
+
+template <int NW>
+__device__ __forceinline__ void mw_setup(const CodeView &code, int tid, MwTables<NW> &t) {
+  const int lane = tid & 63, M = code.M;
+  const uint4 r = reinterpret_cast<const uint4 *>(code.erow)[tid];
+  t.rn[0] = r.x;
+  t.rn[1] = r.y;
+  t.rn[2] = r.z;
+  t.rn[3] = r.w;
+  const uint2 c = reinterpret_cast<const uint2 *>(code.ecol)[tid];
+  t.cn[0] = c.x;
+  t.cn[1] = c.y;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const uint4 cc = reinterpret_cast<const uint4 *>(code.cols)[lane + 64 * q];
+    t.ce[q][0] = cc.x;
+    t.ce[q][1] = cc.y;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int j = lane + 64 * q;
+      t.rowmask[q][k] = j < M ? code.rowmask[j * NW + k] : 0ull;
+    }
+  }
+  const int cl = field(t.rn, 7);
+  t.col = cl != kNone ? cl : 0;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const uint32_t cq = code.lane_col[lane + 64 * q];
+    t.colq[q] = cq == kNone ? -1 : (int)cq;
+  }
+}
+
+// One frame: samples src[colq] * pol.  Leaves the hard decisions (by lane
+// position) and posteriors in every wave; returns the syndrome weight and
+// the iterations used.  Starts with a workgroup barrier (the caller's LDS
+// reads of the previous frame must be done when it is entered: every caller
+// ends a frame with __syncthreads).  tb[64 S] must hold the identity.
+template <int PREC, int METHOD, int S, int NW, typename Real = typename Math<PREC>::Real>
+__device__ __forceinline__ int mw_frame(const CodeView &code, int max_iters, int et_period,
+                                        MwTables<NW> &t, Real *tb, Real *eb, Real *rb, Real *sb,
+                                        const typename Math<PREC>::Tab *logtab, const float *src,
+                                        float pol, int elem_stride, uint64_t (&hard)[NW],
+                                        Real (&post)[NW], int &used) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int M = code.M, N = code.N;
+  constexpr int kDummy = 64 * S;
+  // channel samples, one private copy per wave (:149-153, :486)
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const int c = lane + 64 * q;
+    float x = 0.0f;
+    if (t.colq[q] >= 0) x = src[(int64_t)t.colq[q] * elem_stride] * pol;
+    rb[c] = -(Real)x;
+    post[q] = (Real)x;
+  }
+  __syncthreads();  // dummy written; previous frame's tb/eb readers done
+#pragma unroll
+  for (int q = 0; q < NW; ++q) hard[q] = 0;
+  int weight = 0;
+  used = 0;
+  Real msg = rb[t.col], lr = Real(0);
+  for (int h = 0; h < max_iters; ++h) {
+    opaque(t.rn);
+    opaque(t.cn);
+    if constexpr (METHOD == 1)
+      tb[tid] = Math<PREC>::tanh_half(msg, logtab);  // :509
+    else
+      tb[tid] = msg;
+    __syncthreads();
+    Real nb[kDcMax - 1];
+#pragma unroll
+    for (int k = 0; k < kDcMax - 1; ++k) {
+      const int n = field(t.rn, k);
+      nb[k] = tb[n == kNone ? kDummy : n];
+    }
+    if constexpr (METHOD == 1) {
+      Real T = Real(1);  // ascending column; dummies are exact 1.0 (:506-511)
+#pragma unroll
+      for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[k];
+      eb[tid] = Math<PREC>::check_msg(T, logtab);  // :513
+    } else {
+      const int self = sgn(msg);  // :350-376
+      int prod = self;
+      Real lo = Math<PREC>::max_();
+#pragma unroll
+      for (int k = 0; k < kDcMax - 1; ++k) {
+        prod *= sgn(nb[k]);
+        const Real beta = Math<PREC>::abs_(nb[k]);
+        lo = beta < lo ? beta : lo;
+      }
+      lr = (Real)(prod * self) * lo;
+      eb[tid] = lr;
+    }
+    __syncthreads();
+    // column phase, identical in every wave
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      opaque(t.ce[q]);
+      const int c = lane + 64 * q;
+      Real ev[kDvMax];
+#pragma unroll
+      for (int k = 0; k < kDvMax; ++k) {
+        const int n = field(t.ce[q], k);
+        ev[k] = eb[n == kNone ? kDummy : n];
+      }
+      const Real rc = rb[c];
+      Real acc = Real(0);
+      bool bit;
+      if constexpr (METHOD == 1) {  // :519-532
+#pragma unroll
+        for (int k = 0; k < kDvMax; ++k)
+          acc = field(t.ce[q], k) != kNone ? acc + (ev[k] + rc) : acc;
+        bit = acc <= Real(0);
+        post[q] = acc;
+      } else {  // :379-403
+#pragma unroll
+        for (int k = 0; k < kDvMax; ++k)
+          acc = field(t.ce[q], k) != kNone ? acc + ev[k] : acc;
+        const Real LQ = rc + acc;
+        sb[c] = LQ;
+        bit = LQ < Real(0);
+        post[q] = LQ;
+      }
+      hard[q] = __ballot(bit && c < N);
+    }
+    weight = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      int odd = 0;
+#pragma unroll
+      for (int k = 0; k < NW; ++k) odd ^= __popcll(t.rowmask[q][k] & hard[k]);
+      weight += __popcll(__ballot((odd & 1) != 0 && lane + 64 * q < M));
+    }
+    used = h + 1;
+    if (h + 1 == max_iters) break;
+    if ((h + 1) % et_period == 0 && weight == 0) break;
+    if constexpr (METHOD == 1) {  // :540-553
+      const Real rc = rb[t.col];
+      Real cv[kDvMax - 1];
+#pragma unroll
+      for (int k = 0; k < kDvMax - 1; ++k) {
+        const int n = field(t.cn, k);
+        cv[k] = eb[n == kNone ? kDummy : n];
+      }
+      Real acc = Real(0);
+#pragma unroll
+      for (int k = 0; k < kDvMax - 1; ++k)
+        acc = field(t.cn, k) != kNone ? acc + (cv[k] + rc) : acc;
+      msg = acc;
+    } else {
+      wave_lds_sync();  // this wave's sb
+      msg = sb[t.col] - lr;  // :387-392
+    }
+  }
+  return weight;
+}
+
+// packed info byte `lane` (lanes < KB) of a frame's hard decisions (:207-219)
+template <int NW>
+__device__ __forceinline__ uint32_t mw_packed_byte(const CodeView &code, const uint64_t (&hard)[NW],
+                                                   int lane) {
+  uint32_t o = 0;
+  if (lane < code.KB) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = code.M + 8 * lane + j;
+      if (c < code.N) {
+        const int x = code.col_lane[c];  // position of column c
+        o |= (uint32_t)((word_at<NW>(hard, x >> 6) >> (x & 63)) & 1) << (7 - j);
+      }
+    }
+  }
+  return o;
+}
 
 }  // namespace ldpc

@@ -201,15 +201,13 @@ __global__ void __launch_bounds__(kThreads, MINB)
 }
 
 // ---------------------------------------------------------------------------
-// Multi-wave kernel: one frame per S-wave workgroup, one edge per lane.
+// Multi-wave kernel: one frame per S-wave workgroup, one edge per lane
+// (mw_frame, ldpc_frame.hpp).
 //
 // At small batches the decode time is set by the frames that run to the
 // iteration cap, i.e. by one frame's per-iteration latency.  Spreading a
 // frame over S waves (on different SIMDs of the CU) divides the edge work of
-// an iteration by S; the price is two workgroup barriers per iteration.  The
-// cheap column phase (posterior, hard decision, syndrome) is computed by
-// every wave redundantly from the shared check messages, so every wave
-// reaches the same early-exit decision without a third barrier.
+// an iteration by S; the price is two workgroup barriers per iteration.
 // ---------------------------------------------------------------------------
 
 template <int PREC, int METHOD, int S, int NW>
@@ -218,7 +216,7 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
   extern __shared__ __align__(16) unsigned char smem[];
   const MwLayout<Real, S, NW> L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int M = code.M, N = code.N;
+  const int N = code.N;
   constexpr int kDummy = 64 * S;
   Real *tb = reinterpret_cast<Real *>(smem);
   Real *eb = reinterpret_cast<Real *>(smem + L.eb);
@@ -228,148 +226,19 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
   __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
   if constexpr (METHOD == 1) stage_tab<PREC>(logtab);
   if (tid == 0) tb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();
-
-  // this lane's edge, and (every wave) the columns lane + 64 q
-  uint32_t rn[4], cn[2], ce[NW][2];
-  {
-    const uint4 r = reinterpret_cast<const uint4 *>(code.erow)[tid];
-    rn[0] = r.x; rn[1] = r.y; rn[2] = r.z; rn[3] = r.w;
-    const uint2 c = reinterpret_cast<const uint2 *>(code.ecol)[tid];
-    cn[0] = c.x; cn[1] = c.y;
-  }
-  uint64_t rowmask[NW][NW];
-#pragma unroll
-  for (int q = 0; q < NW; ++q) {
-    const uint4 c = reinterpret_cast<const uint4 *>(code.cols)[lane + 64 * q];
-    ce[q][0] = c.x; ce[q][1] = c.y;
-#pragma unroll
-    for (int k = 0; k < NW; ++k) {
-      const int j = lane + 64 * q;
-      rowmask[q][k] = j < M ? code.rowmask[j * NW + k] : 0ull;
-    }
-  }
-  int col = field(rn, 7);
-  col = col != kNone ? col : 0;
-  int colq[NW];  // column at each of the lane's positions (-1: none)
-#pragma unroll
-  for (int q = 0; q < NW; ++q) {
-    const uint32_t c = code.lane_col[lane + 64 * q];
-    colq[q] = c == kNone ? -1 : (int)c;
-  }
+  MwTables<NW> t;
+  mw_setup<NW>(code, tid, t);
 
   int64_t b = blockIdx.x;
   while (b < a.B) {
-    // channel samples, one private copy per wave (:149-153, :486)
     float pol;
     const float *src = frame_src(a, b, pol);
-    Real post[NW];
-#pragma unroll
-    for (int q = 0; q < NW; ++q) {
-      const int c = lane + 64 * q;
-      float x = 0.0f;
-      if (colq[q] >= 0) x = src[(int64_t)colq[q] * a.elem_stride] * pol;
-      rb[c] = -(Real)x;
-      post[q] = (Real)x;
-    }
-    __syncthreads();  // dummy written; previous frame's tb/eb readers done
     uint64_t hard[NW];
-#pragma unroll
-    for (int q = 0; q < NW; ++q) hard[q] = 0;
-    int weight = 0, used = 0;
-    Real msg = rb[col], lr = Real(0);
-    for (int h = 0; h < a.max_iters; ++h) {
-      opaque(rn);
-      opaque(cn);
-      if constexpr (METHOD == 1)
-        tb[tid] = Math<PREC>::tanh_half(msg, logtab);  // :509
-      else
-        tb[tid] = msg;
-      __syncthreads();
-      Real nb[kDcMax - 1];
-#pragma unroll
-      for (int k = 0; k < kDcMax - 1; ++k) {
-        const int n = field(rn, k);
-        nb[k] = tb[n == kNone ? kDummy : n];
-      }
-      if constexpr (METHOD == 1) {
-        Real T = Real(1);  // ascending column; dummies are exact 1.0 (:506-511)
-#pragma unroll
-        for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[k];
-        eb[tid] = Math<PREC>::check_msg(T, logtab);  // :513
-      } else {
-        const int self = sgn(msg);  // :350-376
-        int prod = self;
-        Real lo = Math<PREC>::max_();
-#pragma unroll
-        for (int k = 0; k < kDcMax - 1; ++k) {
-          prod *= sgn(nb[k]);
-          const Real beta = Math<PREC>::abs_(nb[k]);
-          lo = beta < lo ? beta : lo;
-        }
-        lr = (Real)(prod * self) * lo;
-        eb[tid] = lr;
-      }
-      __syncthreads();
-      // column phase, identical in every wave
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        opaque(ce[q]);
-        const int c = lane + 64 * q;
-        Real ev[kDvMax];
-#pragma unroll
-        for (int k = 0; k < kDvMax; ++k) {
-          const int n = field(ce[q], k);
-          ev[k] = eb[n == kNone ? kDummy : n];
-        }
-        const Real rc = rb[c];
-        Real acc = Real(0);
-        bool bit;
-        if constexpr (METHOD == 1) {  // :519-532
-#pragma unroll
-          for (int k = 0; k < kDvMax; ++k)
-            acc = field(ce[q], k) != kNone ? acc + (ev[k] + rc) : acc;
-          bit = acc <= Real(0);
-          post[q] = acc;
-        } else {  // :379-403
-#pragma unroll
-          for (int k = 0; k < kDvMax; ++k)
-            acc = field(ce[q], k) != kNone ? acc + ev[k] : acc;
-          const Real LQ = rc + acc;
-          sb[c] = LQ;
-          bit = LQ < Real(0);
-          post[q] = LQ;
-        }
-        hard[q] = __ballot(bit && c < N);
-      }
-      weight = 0;
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        int odd = 0;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) odd ^= __popcll(rowmask[q][k] & hard[k]);
-        weight += __popcll(__ballot((odd & 1) != 0 && lane + 64 * q < M));
-      }
-      used = h + 1;
-      if (h + 1 == a.max_iters) break;
-      if ((h + 1) % a.et_period == 0 && weight == 0) break;
-      if constexpr (METHOD == 1) {  // :540-553
-        const Real rc = rb[col];
-        Real cv[kDvMax - 1];
-#pragma unroll
-        for (int k = 0; k < kDvMax - 1; ++k) {
-          const int n = field(cn, k);
-          cv[k] = eb[n == kNone ? kDummy : n];
-        }
-        Real acc = Real(0);
-#pragma unroll
-        for (int k = 0; k < kDvMax - 1; ++k)
-          acc = field(cn, k) != kNone ? acc + (cv[k] + rc) : acc;
-        msg = acc;
-      } else {
-        wave_lds_sync();  // this wave's sb
-        msg = sb[col] - lr;  // :387-392
-      }
-    }
+    Real post[NW];
+    int used = 0;
+    const int weight = mw_frame<PREC, METHOD, S, NW>(code, a.max_iters, a.et_period, t, tb, eb,
+                                                     rb, sb, logtab, src, pol, a.elem_stride,
+                                                     hard, post, used);
     // outputs (wave 0)
     if (wave == 0) {
       if (lane == 0) {
@@ -378,7 +247,7 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
       }
 #pragma unroll
       for (int q = 0; q < NW; ++q) {
-        const int c = colq[q];
+        const int c = t.colq[q];
         if (c >= 0) {
           if (a.bits) a.bits[b * N + c] = (uint8_t)((hard[q] >> lane) & 1);
           if (a.llr) a.llr[b * N + c] = (float)post[q];
@@ -388,7 +257,7 @@ __global__ void __launch_bounds__(64 * S) decode_mw_kernel(CodeView code, Decode
         uint32_t o = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int c = M + 8 * p + j;
+          const int c = code.M + 8 * p + j;
           if (c < N) {
             const int x = code.col_lane[c];  // position of column c
             o |= (uint32_t)((word_at<NW>(hard, x >> 6) >> (x & 63)) & 1) << (7 - j);

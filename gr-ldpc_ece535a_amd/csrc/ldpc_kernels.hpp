@@ -170,6 +170,27 @@ struct alignas(16) WalkArgs {
 int launch_walk(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, int method,
                 int prec, int slots, int nw, int blocks, void *stream);
 
+// ---------------------------------------------------------------------------
+// The block's window server (ldpc_serve.hip): one persistent launch per
+// general_work call serves rounds of windows of the staged span.  The host
+// writes a round's keys, then the round word (epoch << 32) | B; results come
+// back as 8-byte granules {(epoch mod 2^23) << 9 | syndrome weight, packed
+// bytes}.  Epochs only grow; a launch serves epochs above start_epoch.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kServeQuit = 0xFFFFFFFFu;  // B of the round that ends the launch
+struct alignas(16) ServeArgs {
+  const uint64_t *round;  // host-mapped round word
+  const int64_t *keys;    // host-mapped window keys, (position << 1) | polarity
+  uint64_t *res;          // host-mapped result granules
+  uint64_t *ctl;          // device: the round as the poller published it (zeroed per launch)
+  uint64_t deadline;      // 100 MHz ticks without a new round before the launch ends
+  uint32_t start_epoch;   // the last epoch posted before this launch
+  int blocks_per_cu;      // decoder workgroups per CU (capped by occupancy; 0: occupancy)
+};
+// *workgroups_out: the launch's decoder workgroups
+int launch_serve(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, int method,
+                 int prec, int slots, int nw, void *stream, int *workgroups_out);
+
 // Launch one decode (host side, implemented in ldpc_kernels.hip).
 // method: 0 min-sum, 1 sum-product, 2 bit-flip, 3 hard; prec 0 f64, 1 f32;
 // slots = ceil(E/64); nw = 1 or 4 (hard-decision words).

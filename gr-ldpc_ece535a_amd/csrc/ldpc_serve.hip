@@ -1,0 +1,308 @@
+// ldpc_serve.hip -- the decoder block's window server (gfx950).
+//
+// lib/ldpc_decoder_cb_impl.cc:146-226 decodes one window per step (the N
+// samples at the current position, times +-1) and its state machine picks the
+// next position from the result.  The block replays that loop on the host over
+// decoded windows and asks for the windows a dry run says it will need
+// (csrc/block/ldpc_decoder_cb_impl.cc); at the reference's 5 iterations most
+// of a call is a chain of such dependent rounds of a few hundred windows, and
+// a kernel launch per round costs ~21 us whatever its size: dispatch, the
+// kernel's prologue (code tables, the log table into LDS, the window list
+// over the bus), completion and the host's wake-up -- against ~6 us for the
+// windows' 5 iterations.
+//
+// Here ONE launch serves every round of a general_work call:
+//   * workgroup 0 (one lane) is the poller: it watches the round word in
+//     host-mapped memory, {epoch, B}, and republishes it in device memory;
+//   * every other workgroup is a decoder: tables and the log table are loaded
+//     into LDS once, then it waits for a new epoch, decodes windows g, g + G,
+//     ... of the round's list (the batch kernels' workgroup-per-frame
+//     arithmetic, mw_frame in ldpc_frame.hpp: results equal every other
+//     decode of the same samples) and publishes each result as one 8-byte
+//     granule {(epoch << 9) | syndrome weight, packed bytes} in host-mapped
+//     memory, which the host polls;
+//   * B = kServeQuit ends the launch; so does a deadline (no round for
+//     `deadline` ticks of the 100 MHz clock), after which the host relaunches
+//     the server if it still wants a round.
+// Visibility: the device reads host memory with system-scope loads (the
+// round word, then the keys, which the host wrote before it), writes results
+// with one system-scope 8-byte store per window, and hands the round word to
+// the decoders as one agent-scope (sc1) granule polled with sc1 loads
+// (MI355X_MICROARCH.md, inter-workgroup visibility, R2).
+#include "ldpc_frame.hpp"
+
+namespace ldpc {
+namespace {
+
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) int64_t gi64;
+
+__device__ __forceinline__ uint64_t ticks() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ uint64_t agent_load(const uint64_t *p) {
+  return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void agent_store(uint64_t *p, uint64_t v) {
+  __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t sys_load(const uint64_t *p) {
+  return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ int64_t sys_load_i64(const int64_t *p) {
+  return __hip_atomic_load((const gi64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(uint64_t *p, uint64_t v) {
+  __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The round as the poller publishes it, one 8-byte granule: epoch (bits
+// 40..63), the decoders sharing it (20..39), B (0..19).  A decoder takes the
+// census (one atomic add, once per launch) when it starts; the windows of a
+// round go to the decoders counted when the round was published -- running,
+// so no window waits on a workgroup that is not resident.  Host epochs stay
+// below 2^23 (ldpc_serve_begin restarts them).
+constexpr uint64_t kQuitRound = ~0ull;  // epoch all ones: every decoder leaves
+__device__ __forceinline__ uint64_t ctl_word(uint32_t ep, uint32_t live, uint32_t B) {
+  return ((uint64_t)ep << 40) | ((uint64_t)(live & 0xFFFFFu) << 20) | (B & 0xFFFFFu);
+}
+__device__ __forceinline__ uint32_t census_load(uint64_t *ctl) {
+  return __hip_atomic_load((const __attribute__((address_space(1))) uint32_t *)(ctl + 16),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t census_take(uint64_t *ctl) {
+  return __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t *)(ctl + 16), 1u,
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Workgroup 0: the poller (one lane).  Others: decoders.  A round of at most
+// as many windows as there are decoder workgroups is decoded one window per
+// workgroup (mw_frame: S waves, one edge per lane, the lowest latency); a
+// bigger round one window per wave (decode_frame, the batch kernels' one-wave
+// form: fewer issue slots per window), windows w, w + W, ... for wave w of W.
+// The two forms share the workgroup's LDS (never at the same time).
+template <int PREC, int METHOD, int S, int NW, int DCN, int DVN>
+__global__ void __launch_bounds__(64 * S, 3) serve_kernel(CodeView code, DecodeArgs a, ServeArgs s) {
+  typedef typename Math<PREC>::Real Real;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ int64_t sslot[2];  // the round, the window key (mw form)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (blockIdx.x == 0) {
+    if (tid != 0) return;
+    uint32_t last = s.start_epoch;
+    uint64_t t_last = ticks();
+    for (;;) {
+      const uint64_t r = sys_load(s.round);
+      const uint32_t ep = (uint32_t)(r >> 32);
+      if (ep != last) {
+        // the decoders that have started by now share the round
+        const uint32_t live = census_load(s.ctl);
+        agent_store(s.ctl, (uint32_t)r == kServeQuit ? kQuitRound : ctl_word(ep, live, (uint32_t)r));
+        last = ep;
+        t_last = ticks();
+        if ((uint32_t)r == kServeQuit) return;
+      } else if (ticks() - t_last > s.deadline) {
+        agent_store(s.ctl, kQuitRound);
+        return;
+      }
+    }
+  }
+  __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
+  if constexpr (METHOD == 1) stage_tab<PREC>(logtab);
+  // workgroup-per-window form: tables per edge, LDS per MwLayout
+  const MwLayout<Real, S, NW> L;
+  constexpr int kDummy = 64 * S;
+  Real *mtb = reinterpret_cast<Real *>(smem);
+  Real *meb = reinterpret_cast<Real *>(smem + L.eb);
+  Real *mrb = reinterpret_cast<Real *>(smem + L.waves + (size_t)wave * L.per_wave);
+  Real *msb = mrb + 64 * NW;
+  MwTables<NW> mt;
+  mw_setup<NW>(code, tid, mt);
+  // wave-per-window form: the wave's tables in registers, its own LDS slice
+  WaveTables<S, NW> wt;
+  Real *tb, *eb, *rb, *sb;
+  int colq[NW];
+  uint32_t ppos[2];
+  wave_setup<PREC, METHOD, S, NW, DCN, DVN>(code, smem, wave, lane, wt, tb, eb, rb, sb, colq, ppos);
+  if (tid == 0) sslot[1] = (int64_t)census_take(s.ctl);
+  __syncthreads();
+  const int64_t g = sslot[1];  // this decoder's place among those that started
+  // epochs only grow (ctl is zeroed before the launch, below start_epoch)
+  uint32_t last = s.start_epoch;
+  uint64_t idle = ticks();
+  for (;;) {
+    if (tid == 0) {  // the next round
+      uint64_t r;
+      for (int spins = 0;; ++spins) {
+        r = agent_load(s.ctl);
+        if ((uint32_t)(r >> 40) > last) break;
+        if ((spins & 15) == 15 && ticks() - idle > s.deadline) {
+          r = kQuitRound;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      sslot[0] = (int64_t)r;
+    }
+    __syncthreads();
+    const uint64_t r = (uint64_t)sslot[0];
+    if (r == kQuitRound) return;  // every thread of the workgroup
+    const uint32_t ep = (uint32_t)(r >> 40), B = (uint32_t)r & 0xFFFFFu;
+    const int64_t G = (int64_t)((r >> 20) & 0xFFFFFu);
+    const uint64_t tag = (uint64_t)((ep & 0x7FFFFFu) << 9) << 32;
+    if ((int64_t)B <= G) {
+      // one window per workgroup
+      if (g < (int64_t)B) {
+        if (tid == 0) {
+          sslot[1] = sys_load_i64(s.keys + g);
+          mtb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();  // (the LDS is shared)
+        }
+        __syncthreads();  // (mw_frame's first barrier orders the key's readers)
+        const int64_t key = sslot[1];
+        uint64_t hard[NW];
+        Real post[NW];
+        int used = 0;
+        const int weight = mw_frame<PREC, METHOD, S, NW>(code, a.max_iters, 1, mt, mtb, meb, mrb,
+                                                         msb, logtab, a.in + (key >> 1),
+                                                         (key & 1) ? -1.0f : 1.0f, 1, hard, post,
+                                                         used);
+        (void)post;
+        if (wave == 0) {  // packed bytes M.. (:207-219), then the granule
+          const uint32_t o = mw_packed_byte<NW>(code, hard, lane);
+          uint32_t pk = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            pk |= ((uint32_t)__builtin_amdgcn_readlane((int)o, j) & 255u) << (8 * j);
+          if (lane == 0) sys_store(s.res + g, tag | ((uint64_t)(uint32_t)weight << 32) | pk);
+        }
+        wave_lds_sync();
+      }
+    } else {
+      // one window per wave
+      const int64_t W = G * S;
+      for (int64_t b = g * S + wave; b < (int64_t)B && g < G; b += W) {
+        const uint64_t kv = (uint64_t)sys_load_i64(s.keys + b);  // (one request for the wave)
+        const int64_t key = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(kv >> 32)) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)kv));
+        const float *src = a.in + (key >> 1);
+        const float sgn = (key & 1) ? -1.0f : 1.0f;
+        float xin[NW];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) xin[q] = colq[q] >= 0 ? src[colq[q]] * sgn : 0.0f;
+        FrameResult fr;
+        if constexpr (METHOD == 1) {
+          bool bad = false;
+#pragma unroll
+          for (int q = 0; q < NW; ++q) bad |= !__builtin_isfinite(xin[q]);
+          if (__ballot(bad) == 0)
+            fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, true, Real, false>(
+                code, a, 0, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
+          else
+            fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, false>(
+                code, a, 0, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
+        } else {
+          fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, false>(
+              code, a, 0, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
+        }
+        uint32_t pk = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          pk |= ((uint32_t)__builtin_amdgcn_readlane((int)fr.byte, j) & 255u) << (8 * j);
+        if (lane == 0) sys_store(s.res + b, tag | ((uint64_t)(uint32_t)fr.weight << 32) | pk);
+      }
+    }
+    __syncthreads();  // the round's LDS reads done, and every thread has read the round
+    last = ep;
+    idle = ticks();
+  }
+}
+
+int cus_of_device() {
+  static int cus_of[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus_of[dev] &&
+      hipDeviceGetAttribute(&cus_of[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus_of[dev] = 256;
+  return cus_of[dev];
+}
+
+template <int PREC, int METHOD, int S, int NW, int DCN, int DVN>
+int launch_s(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, hipStream_t st,
+             int *wg) {
+  typedef typename Math<PREC>::Real Real;
+  // the two forms' LDS, overlaid
+  const size_t lds = std::max(MwLayout<Real, S, NW>().total,
+                              (size_t)S * Layout<Real, METHOD, S, NW, DVN>::per_wave);
+  const void *fn = (const void *)serve_kernel<PREC, METHOD, S, NW, DCN, DVN>;
+  static int per_cu = 0;  // resident decoder workgroups per CU
+  if (!per_cu) {
+    if (lds > 65536 &&
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return -3;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * S, lds) != hipSuccess || n < 1)
+      n = 1;
+    // the API can count more than the hardware admits (SGPR-limited waves,
+    // MI355X_MICROARCH.md "Residency"): workgroups past the resident ones
+    // only start once the launch ends, and rounds go to the decoders that
+    // started (the census), so this is a speed matter only
+    per_cu = std::min(n, 8);
+  }
+  const int blocks = (s.blocks_per_cu > 0 ? std::min(per_cu, s.blocks_per_cu) : per_cu) *
+                     cus_of_device();
+  *wg = blocks - 1;
+  hipLaunchKernelGGL((serve_kernel<PREC, METHOD, S, NW, DCN, DVN>), dim3((unsigned)blocks),
+                     dim3(64 * S), lds, st, code, a, s);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <int PREC, int METHOD, int NW>
+int serve_slots(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, int slots,
+                hipStream_t st, int *wg) {
+  // low-degree codes (the reference's H) get loops sized to their degrees, as
+  // the batch kernels (ldpc_kernels.hip launch_slots)
+  if constexpr (NW == 1) {
+    if (code.dc_max <= 6 && code.dv_max <= 3) switch (slots) {
+        case 1: return launch_s<PREC, METHOD, 1, NW, 5, 3>(code, a, s, st, wg);
+        case 2: return launch_s<PREC, METHOD, 2, NW, 5, 3>(code, a, s, st, wg);
+        case 3: return launch_s<PREC, METHOD, 3, NW, 5, 3>(code, a, s, st, wg);
+        case 4: return launch_s<PREC, METHOD, 4, NW, 5, 3>(code, a, s, st, wg);
+        default: break;
+      }
+  }
+  constexpr int D = kDcMax - 1, V = kDvMax;
+  switch (slots) {
+    case 1: return launch_s<PREC, METHOD, 1, NW, D, V>(code, a, s, st, wg);
+    case 2: return launch_s<PREC, METHOD, 2, NW, D, V>(code, a, s, st, wg);
+    case 3: return launch_s<PREC, METHOD, 3, NW, D, V>(code, a, s, st, wg);
+    case 4: return launch_s<PREC, METHOD, 4, NW, D, V>(code, a, s, st, wg);
+    default: return -2;  // workgroups of more than 4 waves: launches
+  }
+}
+
+template <int NW>
+int serve_nw(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, int method, int prec,
+             int slots, hipStream_t st, int *wg) {
+  if (method == 1) {
+    if (prec == 1) return serve_slots<1, 1, NW>(code, a, s, slots, st, wg);
+    if (prec == 2) return serve_slots<2, 1, NW>(code, a, s, slots, st, wg);
+    if (prec == 3) return serve_slots<3, 1, NW>(code, a, s, slots, st, wg);
+    return serve_slots<0, 1, NW>(code, a, s, slots, st, wg);
+  }
+  if (method == 0)  // min-sum: both f64 modes are the same arithmetic
+    return prec == 1 ? serve_slots<1, 0, NW>(code, a, s, slots, st, wg)
+                     : serve_slots<0, 0, NW>(code, a, s, slots, st, wg);
+  return -2;
+}
+
+}  // namespace
+
+int launch_serve(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, int method,
+                 int prec, int slots, int nw, void *stream, int *workgroups_out) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (code.KB > 4 || s.start_epoch >= (1u << 23) - (1u << 16)) return -2;
+  if (nw == 1) return serve_nw<1>(code, a, s, method, prec, slots, st, workgroups_out);
+  if (nw == 4) return serve_nw<4>(code, a, s, method, prec, slots, st, workgroups_out);
+  return -2;
+}
+
+}  // namespace ldpc

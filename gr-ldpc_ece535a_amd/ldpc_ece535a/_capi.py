@@ -78,6 +78,10 @@ SIGNATURES = {
     "ldpc_decode_windows": (_i, [_vp, _i, _i, _i, _i, _f32p, _i64, _i, _i,
                                  ctypes.POINTER(ctypes.c_int64), _i, _u8p, _i32p]),
     "ldpc_stage_span": (_i, [_vp, _f32p, _i64, _i, _i]),
+    "ldpc_serve_begin": (_i, [_vp, _i, _i, _i, _i]),
+    "ldpc_serve_windows": (_i, [_vp, ctypes.POINTER(ctypes.c_int64), _i, _u8p, _i32p]),
+    "ldpc_serve_end": (_i, [_vp]),
+    "ldpc_ctx_streams": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_void_p)]),
     "ldpc_walk_span": (_i, [_vp, _i, _i, _i, _f32p, _i64, _i, _i, _i, ctypes.c_void_p, _u8p,
                             _u8p, _i]),
     "ldpc_alist_read": (_i, [ctypes.c_char_p, _i32p, _i32p, _i32p, _i32p, _i64]),
@@ -339,6 +343,34 @@ class Decoder:
                                          w.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), B,
                                          _p(packed, _u8p), _p(synd, _i32p)), self._ctx)
         return dict(packed=packed, synd=synd)
+
+    def serve_begin(self, method=METHOD_SUMPRODUCT, max_iters=5, precision=PREC_F64,
+                    max_windows=4096):
+        """ldpc_serve_begin: start the window server over the span staged last
+        (stage_span); rounds then go through serve_windows."""
+        _check(lib().ldpc_serve_begin(self._ctx, int(method), int(max_iters), int(precision),
+                                      int(max_windows)), self._ctx)
+
+    def serve_windows(self, windows):
+        """ldpc_serve_windows: one round of windows (int64 (start << 1) | negate)
+        of the staged span.  Returns dict(packed (B,KB), synd (B,))."""
+        w = np.ascontiguousarray(windows, np.int64)
+        B = w.size
+        packed = np.zeros((B, self.KB), np.uint8)
+        synd = np.zeros(B, np.int32)
+        _check(lib().ldpc_serve_windows(self._ctx, w.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                        B, _p(packed, _u8p), _p(synd, _i32p)), self._ctx)
+        return dict(packed=packed, synd=synd)
+
+    def streams(self, n):
+        """ldpc_ctx_streams: n hipStream_t handles (ints) of the context's
+        in-flight set, each on its own hardware queue."""
+        arr = (ctypes.c_void_p * int(n))()
+        _check(lib().ldpc_ctx_streams(self._ctx, int(n), arr), self._ctx)
+        return [int(x) for x in arr]
+
+    def serve_end(self):
+        _check(lib().ldpc_serve_end(self._ctx), self._ctx)
 
     def walk_span(self, samples, noutput_bytes, method=METHOD_SUMPRODUCT, max_iters=5,
                   precision=PREC_F64, elem_stride=1, state=0, errors=0, last_pass=-(1 << 60),

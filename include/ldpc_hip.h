@@ -13,7 +13,7 @@
  *       ldpc_create_csr takes H as a sparse row list, for codes whose dense
  *       M x N matrix the reference could not hold
  *   ldpc_decode, ldpc_decode_strided, ldpc_decode_strided_both, ldpc_decode_windows,
- *   ldpc_decode_device
+ *   ldpc_serve_begin / ldpc_serve_windows / ldpc_serve_end, ldpc_decode_device
  *       decodeLogDomainSimple :309-412, decodeSumProductSoft :478-557,
  *       decodeBitFlipping :414-476, decodeHard :559-572 and the early-exit
  *       checkFrame(vhat, 0) they call, dispatched as general_work :155-164;
@@ -87,7 +87,7 @@ extern "C" {
 #define LDPC_EDEVICE -3     /* HIP runtime error (no GPU, launch failure...) */
 #define LDPC_ESINGULAR -4   /* encoder: singular triangular factor */
 #define LDPC_ENOMEM -5
-#define LDPC_ETIMEOUT -6    /* ldpc_walk_span: a wait in the launch passed its deadline */
+#define LDPC_ETIMEOUT -6    /* a wait on a persistent launch passed its deadline */
 
 typedef struct ldpc_ctx ldpc_ctx;
 
@@ -256,6 +256,26 @@ int ldpc_decode_windows(ldpc_ctx *ctx, int method, int max_iters, int et_period,
 int ldpc_stage_span(ldpc_ctx *ctx, const float *in, int64_t n_in_floats, int elem_stride,
                     int max_windows);
 
+/* The window server: the rounds of ldpc_decode_windows calls over the span
+ * staged last (ldpc_stage_span) served by ONE persistent launch instead of a
+ * launch per round (reference general_work lib/ldpc_decoder_cb_impl.cc:
+ * 133-234 decodes one window per step; the block asks for each step's windows
+ * in dependent rounds).  ldpc_serve_begin starts the launch for (method,
+ * max_iters, precision) with room for max_windows windows per round: min-sum
+ * and sum-product on small codes with KB <= 4 (the reference's codes); other
+ * codes and methods return LDPC_EUNSUPPORTED and the caller keeps
+ * ldpc_decode_windows.  ldpc_serve_windows decodes one round: windows and
+ * outputs as for ldpc_decode_windows (et_period 1), synchronous -- it returns
+ * when every result is in (LDPC_ETIMEOUT after 10 s).  ldpc_serve_end lets
+ * the launch finish without waiting for it.  Any other call on the context
+ * that uses its stream ends a running server first.
+ * The launch ends on its own after LDPC_SERVE_DEADLINE_MS (default 200) without
+ * a round; a later round then starts another. */
+int ldpc_serve_begin(ldpc_ctx *ctx, int method, int max_iters, int precision, int max_windows);
+int ldpc_serve_windows(ldpc_ctx *ctx, const int64_t *windows, int B, uint8_t *out_packed,
+                       int32_t *syn_weight_opt);
+int ldpc_serve_end(ldpc_ctx *ctx);
+
 /* The decoder block's whole frame loop over one host span, on the device
  * (reference general_work lib/ldpc_decoder_cb_impl.cc:146-226: every decode,
  * the sync state machine, the output bytes and the sync messages).  One
@@ -316,6 +336,16 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
                        int B, uint8_t *d_out_packed, uint8_t *d_out_bits_opt,
                        int32_t *d_iters_used_opt, int32_t *d_syn_weight_opt,
                        float *d_llr_out_opt, void *hip_stream);
+
+/* The context's in-flight streams (hipStream_t) for callers that keep
+ * several ldpc_decode_device calls in flight (LDPC_MODE_THROUGHPUT): n
+ * (1..16) streams that run concurrently -- each on its own hardware queue,
+ * checked by a probe launch pair when the set is first made -- owned by the
+ * context (destroyed by ldpc_destroy).  A caller's own streams may share a
+ * hardware queue, depending on the streams the process made before them, and
+ * then serialise their launches.  (Replaces nothing in the reference: its
+ * decode runs on the calling thread, lib/ldpc_decoder_cb_impl.cc:155-164.) */
+int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out);
 
 /* Tuning: persistent waves per CU for the decode kernel (0 = default).
  * Frames are pulled from a per-launch queue by that many resident waves. */

@@ -12,19 +12,30 @@ from ldpc_ece535a import flowgraph as fg
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("walk", ["0", "1"])
+PATHS = {"serve": {}, "launch": {"LDPC_BLOCK_SERVE": "0"}, "walk": {"LDPC_BLOCK_WALK": "1"}}
+
+
+def _block(method, path, **kw):
+    """The block with its rounds through the window server (default), a
+    launch per round (LDPC_BLOCK_SERVE=0), or the frame loop on the device
+    (LDPC_BLOCK_WALK=1)."""
+    import os
+    env = PATHS[path]
+    os.environ.update(env)
+    try:
+        return L.ldpc_decoder_cb(method, **kw)
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+
+
+@pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("name", ["aligned", "offset", "inverted", "burst", "noisy"])
 @pytest.mark.parametrize("method", [0, 1, 2, 3])
-def test_gpu_block_streams(golden, name, method, walk):
-    """walk "1": the block's calls run the frame loop on the device (ldpc_walk_span)."""
-    import os
+def test_gpu_block_streams(golden, name, method, path):
     st = golden("streams.npz")
     s = st[name + "_in"]
-    os.environ["LDPC_BLOCK_WALK"] = walk
-    try:
-        blk = L.ldpc_decoder_cb(method)
-    finally:
-        os.environ.pop("LDPC_BLOCK_WALK", None)
+    blk = _block(method, path)
     tb = fg.top_block(chunk=[97, 13, 640, 5, 2000] * 4)
     src, dst = fg.vector_source_c(s), fg.vector_sink_b()
     tb.connect((src, 0), (blk, 0))
@@ -50,7 +61,8 @@ def test_qa_loopback_default_h(method):
     assert dec.state == L.STATE_IN_SYNC
 
 
-def test_gpu_block_long_random_stream(golden):
+@pytest.mark.parametrize("path", sorted(PATHS))
+def test_gpu_block_long_random_stream(golden, path):
     """A longer mixed stream: results equal the restated general_work."""
     import sys
     from oracle import oracle as orc
@@ -63,7 +75,7 @@ def test_gpu_block_long_random_stream(golden):
                         rng.standard_normal(64 * 13).astype(np.float32), -x[150:].ravel()])
     s = s.astype(np.complex64)
     exp = orc.run_stream(1, Hr, s, iterations=5)
-    blk = L.ldpc_decoder_cb(1)
+    blk = _block(1, path)
     tb = fg.top_block(chunk=1000, out_space=64)
     src, dst = fg.vector_source_c(s), fg.vector_sink_b()
     tb.connect(src, blk, dst)
@@ -108,15 +120,16 @@ def _zero_region_stream(Hr, seed):
     return s.astype(np.complex64)
 
 
+@pytest.mark.parametrize("path", ["serve", "launch"])
 @pytest.mark.parametrize("method,iters", [(0, 5), (1, 5), (1, 50), (2, 5), (3, 5)])
-def test_gpu_block_zero_filled_region(golden, method, iters):
+def test_gpu_block_zero_filled_region(golden, method, iters, path):
     from oracle import oracle as orc
     Hr = golden("frames_default.npz")["H_reordered"]
     s = _zero_region_stream(Hr, 31 + method)
     exp = orc.run_stream(method, Hr, s, iterations=iters)
     assert len(exp) > 0
     for chunk in ([97, 13, 640, 5, 2000] * 8, 100000):
-        blk = L.ldpc_decoder_cb(method, iterations=iters)
+        blk = _block(method, path, iterations=iters)
         tb = fg.top_block(chunk=chunk, out_space=61)
         src, dst = fg.vector_source_c(s), fg.vector_sink_b()
         tb.connect(src, blk, dst)

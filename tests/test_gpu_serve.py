@@ -1,0 +1,98 @@
+"""The window server (ldpc_serve_*, csrc/ldpc_serve.hip): rounds of windows
+of one staged span, served by one persistent launch, equal the same windows
+through ldpc_decode_windows (a launch per round) and the oracle's decodes of
+the same samples -- every polarity, round sizes from 1 to past the host
+buffer, both methods the server takes -- and the launch survives its own
+deadline between rounds (the next round starts another)."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import ldpc_ece535a as L
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _span(Hr, frames, seed, ebn0=2.0):
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 2, size=(frames, Hr.shape[1] - Hr.shape[0]), dtype=np.uint8)
+    x = 2.0 * L.encode(Hr, data) - 1.0
+    y = x + np.sqrt(10 ** (-ebn0 / 10)) * rng.standard_normal(x.shape)
+    s = np.concatenate([rng.standard_normal(37), y.ravel()]).astype(np.float32)
+    return s
+
+
+def _windows(rng, n, span_len, N):
+    p = rng.integers(0, span_len - N + 1, size=n).astype(np.int64)
+    return (p << 1) | rng.integers(0, 2, size=n).astype(np.int64)
+
+
+def _oracle(method, Hr, s, win, iters):
+    N = Hr.shape[1]
+    p, neg = win >> 1, (win & 1).astype(bool)
+    frames = np.stack([s[q:q + N] for q in p]).astype(np.float32)
+    frames[neg] = -frames[neg]
+    return orc.decode_batch(method, Hr, frames, iters)
+
+
+@pytest.mark.parametrize("method,iters", [(1, 5), (1, 50), (0, 5), (0, 50)])
+def test_serve_rounds_equal_launches_and_oracle(method, iters):
+    dec = L.Decoder()
+    Hr = dec.H
+    s = _span(Hr, 600, 11 + method + iters)
+    rng = np.random.default_rng(3)
+    dec.stage_span(s, max_windows=4096)
+    dec.serve_begin(method=method, max_iters=iters, max_windows=4096)
+    rounds = [_windows(rng, n, s.size, dec.N) for n in (1, 7, 64, 300, 1021, 5000)]
+    got = [dec.serve_windows(w) for w in rounds]
+    dec.serve_end()
+    for w, g in zip(rounds, got):
+        ref = _oracle(method, Hr, s, w, iters)
+        assert (g["packed"] == ref["packed"]).all()
+        assert (g["synd"] == ref["synd"]).all()
+        lw = dec.decode_windows(s, w, method=method, max_iters=iters)
+        assert (lw["packed"] == g["packed"]).all() and (lw["synd"] == g["synd"]).all()
+    dec.close()
+
+
+def test_serve_survives_its_deadline():
+    """A launch that ends on its deadline between rounds is replaced by the
+    next round; a decode on the context's stream afterwards is not blocked."""
+    dec = L.Decoder()
+    Hr = dec.H
+    s = _span(Hr, 200, 5)
+    rng = np.random.default_rng(8)
+    os.environ["LDPC_SERVE_DEADLINE_MS"] = "2"
+    try:
+        dec.stage_span(s, max_windows=512)
+        dec.serve_begin(method=1, max_iters=5, max_windows=512)
+        for _ in range(3):
+            w = _windows(rng, 200, s.size, dec.N)
+            g = dec.serve_windows(w)
+            ref = _oracle(1, Hr, s, w, 5)
+            assert (g["packed"] == ref["packed"]).all() and (g["synd"] == ref["synd"]).all()
+            time.sleep(0.02)  # longer than the deadline: the launch has ended
+    finally:
+        os.environ.pop("LDPC_SERVE_DEADLINE_MS", None)
+    dec.serve_end()
+    out = dec.decode(s[37:37 + 64 * 4].reshape(4, 64), method=1, max_iters=5)
+    ref = orc.decode_batch(1, Hr, s[37:37 + 64 * 4].reshape(4, 64), 5)
+    assert (out["packed"] == ref["packed"]).all()
+    dec.close()
+
+
+def test_serve_errors():
+    dec = L.Decoder()
+    s = _span(dec.H, 10, 1)
+    with pytest.raises(L.LdpcError):  # no server running
+        dec.serve_windows(np.array([0], np.int64))
+    dec.stage_span(s, max_windows=16)
+    dec.serve_begin(method=1, max_iters=5, max_windows=16)
+    with pytest.raises(L.LdpcError):  # past the span
+        dec.serve_windows(np.array([(s.size - 63) << 1], np.int64))
+    with pytest.raises(L.LdpcError):  # bit-flip: launches only
+        dec.serve_begin(method=2, max_iters=5, max_windows=16)
+    dec.close()

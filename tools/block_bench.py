@@ -17,7 +17,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-KNOBS = ("LDPC_BLOCK_WALK", "LDPC_WALK_BLOCKS_PER_CU", "LDPC_WALK_LEAD", "LDPC_BLOCK_FORK", "LDPC_BLOCK_ANCHOR", "LDPC_BLOCK_SPEC_BOTH", "LDPC_BLOCK_SPEC_DIV", "LDPC_BLOCK_BUDGET",
+KNOBS = ("LDPC_BLOCK_SERVE", "LDPC_BLOCK_WALK", "LDPC_WALK_BLOCKS_PER_CU", "LDPC_WALK_LEAD", "LDPC_BLOCK_FORK", "LDPC_BLOCK_ANCHOR", "LDPC_BLOCK_SPEC_BOTH", "LDPC_BLOCK_SPEC_DIV", "LDPC_BLOCK_BUDGET",
          "LDPC_BLOCK_MAXWANT", "LDPC_BLOCK_SEARCHES", "LDPC_BLOCK_SEARCH_FIRST", "LDPC_BLOCK_SCHEDULE")
 
 
