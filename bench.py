@@ -459,11 +459,11 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
             ("2 dB stream (sync losses)", 2.0, args.iters, cpu_frames // 2, None),
             # make(method) as the reference builds it: 5 iterations (:40)
             ("make(1) defaults, 5 iterations, 4 dB", 4.0, 5, cpu_frames, None),
-            # the same stream through the block's other path, the device-side
-            # frame loop (LDPC_BLOCK_WALK=1; the default is the host planner)
-            ("make(1) defaults, 5 iterations, 4 dB, device walk", 4.0, 5, cpu_frames, "1"))
+            # the same stream with a launch per round instead of the call's
+            # window server (LDPC_BLOCK_SERVE=0: the A/B of the server)
+            ("make(1) defaults, 5 iterations, 4 dB, launch per round", 4.0, 5, cpu_frames, "0"))
     last_ref = None
-    for name, ebn0, iters, n_cpu, walk in runs:
+    for name, ebn0, iters, n_cpu, serve in runs:
         dec = L.Decoder(device=dev.index or 0)
         y, _ = synth_device(L, torch, dec, (reps + 1) * B, ebn0, args.seed + 77, dev,
                             check_frames=0)
@@ -472,19 +472,19 @@ def block_variant(L, torch, blocks, dev, args, d_y, B, reps=4, cpu_frames=1024):
         stream = np.zeros(2 * y.numel(), np.float32)
         stream[0::2] = y.cpu().numpy().ravel()
         cx = stream.view(np.complex64)
-        if walk is not None:
-            os.environ["LDPC_BLOCK_WALK"] = walk
+        if serve is not None:
+            os.environ["LDPC_BLOCK_SERVE"] = serve
         try:
             blk = blocks.ldpc_decoder_cb(1, iterations=iters, precision=0, device=dev.index or 0)
         finally:
-            os.environ.pop("LDPC_BLOCK_WALK", None)
+            os.environ.pop("LDPC_BLOCK_SERVE", None)
         dt, made, calls, launches, windows = drive_stream(blk, cx, B)
         out[name] = {"Mbit/s": round(made * 8 / dt / 1e6, 2), "calls": calls,
                      "ms_per_call": round(dt / max(1, calls) * 1e3, 4),
                      "launches_per_call": round(launches / max(1, calls), 2),
                      "windows_per_output_frame": round(windows / max(1, made // 4), 2),
                      "bytes_out": int(made)}
-        if walk is not None and last_ref is not None:  # the earlier run's CPU restatement, same stream
+        if serve is not None and last_ref is not None:  # the earlier run's CPU restatement, same stream
             gpu_bytes = drive_stream.last_out
             out[name]["bytes_equal_cpu_prefix"] = bool(
                 gpu_bytes.size >= last_ref.size and (gpu_bytes[:last_ref.size] == last_ref).all())

@@ -11,9 +11,11 @@
  * position.  Here the loop is replayed exactly over a memo of decoded
  * windows; when it reaches a window not decoded yet, a dry run of the same
  * loop goes ahead on guesses and collects every window it touches, and all of
- * them are decoded in ONE GPU launch (ldpc_decode_windows: any positions,
- * either polarity, one staged copy of the input).  The exact replay then goes
- * on; a wrong guess only means another launch.
+ * them are decoded in ONE round (any positions, either polarity, one staged
+ * copy of the input): a round of the call's window server (ldpc_serve_windows:
+ * one persistent launch per call, started right behind the span's copy), or
+ * one launch (ldpc_decode_windows) for codes and methods the server does not
+ * take.  The exact replay then goes on; a wrong guess only means another round.
  *
  * The guesses follow the stream's grid: the phase (mod N) where two frames in
  * a row last passed in sync.  A window on the grid passes, any other fails --
@@ -27,11 +29,8 @@
  * its budget (128 positions) widens x4 per launch.  Measured on one MI355X
  * (profiles/round2/block/block_plans.txt): 4 dB stream 32 -> 75 Mbit/s, 2 dB
  * 11 -> 19 Mbit/s against guessing that every frame in sync passes.
- * A launch costs one window's latency plus the host round trip
- * ("The drop-in block's own throughput"), as much as
- * thousands of extra windows, so optional branch speculation
- * (LDPC_BLOCK_FORK=1: the windows needed if a search position syncs) is off
- * at 50 iterations: it saves launches only as fast as it adds windows.
+ * A round costs one window's latency plus the host round trip
+ * (DESIGN.md section 9), as much as thousands of extra windows.
  *
  * The H is the reference's default (make(method)), or a runtime H (dense,
  * reordered like the reference's constructor; CSR; or an alist file).
@@ -71,13 +70,11 @@ namespace {
 // Per launch at most kWindowSamples samples of windows (1 << 17 windows of
 // the reference's N = 64; a DVB-S2-size code gets ~130), which bounds the
 // staging memory and the launch for any N; the out-of-sync search starts
-// with at most d_search_first (128) positions and widens x4 per launch.
+// with at most kSearchFirst (128) positions and widens x4 per round.
 const int64_t kWindowSamples = (int64_t)64 << 17;
 int max_windows(unsigned N) {
   return (int)std::max<int64_t>(16, std::min<int64_t>((int64_t)1 << 17, kWindowSamples / (int64_t)N));
 }
-const int kForkFrames = 13;       // frames a guessed sync at a search position is followed for
-const int kForkSearch = 3;        // x N: the search after such a sync is lost, per fork
 const size_t kDenseMax = (size_t)1 << 22;  // alist codes up to M N entries go dense
 
 void print_method(int method) {
@@ -184,13 +181,6 @@ void ldpc_decoder_cb_impl::adopt(ldpc_ctx *ctx) {
         "ldpc_decoder_cb: the block emits M/8 bytes of information bits per frame "
         "(lib/ldpc_decoder_cb_impl.cc:141, :209-219); this H has N - M < 8 (M/8)");
   }
-  // A/B knobs for the window launches: LDPC_BLOCK_TP=1 the throughput build
-  // (four waves per SIMD), LDPC_BLOCK_WPC waves per CU
-  if (getenv("LDPC_BLOCK_TP") && getenv("LDPC_BLOCK_TP")[0] == '1')
-    (void)ldpc_set_launch_mode(ctx, LDPC_MODE_THROUGHPUT);
-  if (getenv("LDPC_BLOCK_WPC")) (void)ldpc_set_waves_per_cu(ctx, atoi(getenv("LDPC_BLOCK_WPC")));
-  // A/B knob: LDPC_BLOCK_SCHEDULE=1|2 forces the one-wave / workgroup form for every launch
-  if (getenv("LDPC_BLOCK_SCHEDULE")) (void)ldpc_set_schedule(ctx, atoi(getenv("LDPC_BLOCK_SCHEDULE")));
   d_ctx = ctx;
   d_M = (unsigned)M;
   d_N = (unsigned)N;
@@ -219,18 +209,6 @@ void ldpc_decoder_cb_impl::adopt(ldpc_ctx *ctx) {
   } else {
     d_serve = false;
   }
-  // a walk that may run: load its kernel now, with one window of zeros (its
-  // first launch costs milliseconds; a call's timing should not)
-  if (d_walk_mode == 1 || (d_walk_mode < 0 && d_iterations <= 10)) {
-    std::vector<float> z((size_t)2 * N, 0.0f);
-    std::vector<uint8_t> o((size_t)std::max(d_out_bytes, 1)), m(64);
-    ldpc_walk_io io{};
-    io.last_pass = INT64_MIN / 4;
-    io.anchor_pos = -1;
-    const int rc = ldpc_walk_span(ctx, d_method, (int)d_iterations, d_precision, z.data(),
-                                  2 * (int64_t)N, 2, 0, d_out_bytes, &io, o.data(), m.data(), 64);
-    if (rc == LDPC_EUNSUPPORTED) d_walk = false;
-  }
 }
 
 ldpc_decoder_cb_impl::ldpc_decoder_cb_impl(int method, int iterations, ldpc_block_backend_fn fn,
@@ -251,18 +229,6 @@ int ldpc_decoder_cb_impl::Stager::run() {
 void ldpc_decoder_cb_impl::stage_async(const float *in, int64_t n_floats, int max_windows) {
   Stager &sg = d_stager;
   const bool serve = d_serve && (d_method == 0 || d_method == 1);
-  if (!d_stage_thread) {
-    sg.ctx = d_ctx;
-    sg.in = in;
-    sg.n = n_floats;
-    sg.max_windows = max_windows;
-    sg.serve = serve;
-    sg.method = d_method;
-    sg.iterations = (int)d_iterations;
-    sg.precision = d_precision;
-    sg.rc = sg.run();
-    return;
-  }
   if (!sg.th.joinable())
     sg.th = std::thread([&sg]() {
       std::unique_lock<std::mutex> lk(sg.mu);
@@ -292,7 +258,7 @@ void ldpc_decoder_cb_impl::stage_async(const float *in, int64_t n_floats, int ma
 
 int ldpc_decoder_cb_impl::stage_wait() {
   Stager &sg = d_stager;
-  if (d_stage_thread) {
+  {
     std::unique_lock<std::mutex> lk(sg.mu);
     sg.cv.wait(lk, [&sg]() { return !sg.busy; });
   }
@@ -313,12 +279,6 @@ ldpc_decoder_cb_impl::~ldpc_decoder_cb_impl() {
     }
     d_stager.th.join();
   }
-  if (d_profile && d_walk_calls)
-    fprintf(stderr,
-            "ldpc_decoder_cb walk profile: %lld calls (%lld fell back to the host planner); host "
-            "%.3f ms, device loop %.3f ms, of it waiting %.3f ms\n",
-            (long long)d_walk_calls, (long long)d_walk_fallbacks, 1e-3 * d_walk_prof[0],
-            1e-3 * d_walk_prof[1], 1e-3 * d_walk_prof[2]);
   if (d_profile)
     fprintf(stderr,
             "ldpc_decoder_cb profile: %lld launches; general_work %.3f ms = exact replay %.3f + "
@@ -389,28 +349,6 @@ void ldpc_decoder_cb_impl::want(int64_t pos, int pol, int nin) {
   if (m == -1) {
     m = -2;  // pending: wanted by this launch
     d_want.push_back((pos << 1) | pol);
-  }
-}
-
-void ldpc_decoder_cb_impl::fork(int64_t q, int nin) {
-  // The search position q may pass (the check's threshold of M/8 unsatisfied
-  // rows lets misaligned windows through now and then).  The loop would then
-  // stay "in sync" on q's grid until 11 frames fail (:169-176), retry at the
-  // other polarity and search again from one sample on (:178-198): decode
-  // that branch's windows in the same launch, at both polarities.
-  const int64_t N = d_N;
-  for (int j = 1; j <= kForkFrames; ++j) {
-    want(q + N * j, 0, nin);
-    want(q + N * j, 1, nin);
-  }
-  int64_t end = q + 11 * N + kForkSearch * N;
-  if (d_anchor >= 0) {  // the search ends on the grid, at most 2 frames later than 11 failures
-    const int64_t s0 = q + 13 * N + 1;
-    end = s0 + (((d_anchor - (d_abs + s0)) % N) + N) % N;
-  }
-  for (int64_t p = q + 11 * N + 1; p <= end; ++p) {
-    want(p, 0, nin);
-    want(p, 1, nin);
   }
 }
 
@@ -485,21 +423,19 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       if (exact) return STALLED;
       want(pos, pol, nin);
       const bool on_grid = d_anchor < 0 || (d_abs + pos) % N == d_anchor;
-      pass = d_anchor_guess ? (on_grid && (r.state != STATE_OUT_OF_SYNC || d_anchor >= 0))
-                            : r.state != STATE_OUT_OF_SYNC;
+      pass = on_grid && (r.state != STATE_OUT_OF_SYNC || d_anchor >= 0);
       // the same samples known to pass at the other polarity: this one fails
       // (the complement of a codeword leaves every odd-weight row unsatisfied:
       // 20 of the default H's 32)
-      if (pass && d_opposite) {
+      if (pass) {
         const int32_t o = d_memo[pol ^ 1][slot(pos)];
         if (o >= 0 && d_rsynd[o] <= thr) pass = false;
       }
       guessed_out = !pass;
       // a frame in sync is also wanted at the other polarity when its result
       // decides a sync loss's "-tx" retry (:178-187)
-      if (pass && (d_spec_both == 1 || (d_spec_both > 1 && grid_fails_often())))
+      if (pass && grid_fails_often())
         want(pos, pol ^ 1, nin);
-      if (!pass && r.state == STATE_OUT_OF_SYNC) d_forks.push_back(pos);
     }
     if (exact && pass && r.state != STATE_OUT_OF_SYNC) {
       // two frames in a row pass in sync: their grid is the stream's (a
@@ -533,7 +469,6 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
           if (exact) return STALLED;
           want(pos, pol ^ 1, nin);
           guessed_out = true;  // a retry that fails mostly
-          if (use >= 0 && r.state == STATE_OUT_OF_SYNC) d_forks.push_back(pos);
         }
         if (pass2) {
           n.state = STATE_IN_SYNC_INVERTED;
@@ -571,78 +506,6 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
   return DONE;
 }
 
-// One call's loop on the device (ldpc_walk_span): the same bytes, messages,
-// consumption and state as the replay below, without host round trips.
-// False: the walk did not run (unsupported code, or a wait passed its
-// deadline), and the caller plans the call on the host instead.
-bool ldpc_decoder_cb_impl::walk_call(const float *in, int nin, int noutput_items,
-                                     unsigned char *out, int &produced) {
-  const double t0 = now_s();
-  const int N = (int)d_N;
-  ldpc_walk_io io{};
-  io.state = d_state;
-  io.errors = (int32_t)d_errors;
-  // the last in-sync pass, relative to this span (far below 0: none seen)
-  io.last_pass = d_last_pass >= 0 ? d_last_pass - d_abs : INT64_MIN / 4;
-  io.anchor_pos = d_anchor >= 0 ? ((d_anchor - d_abs) % N + N) % N : -1;
-  const int cap = std::max(64, nin / 4 + 64);  // messages: one sync event per few frames at most
-  if ((int)d_walk_msgs.size() < cap) d_walk_msgs.resize((size_t)cap);
-  const int rc = ldpc_walk_span(d_ctx, d_method, (int)d_iterations, d_precision, in,
-                                2 * (int64_t)nin, 2, 0, noutput_items, &io, out,
-                                d_walk_msgs.data(), cap);
-  if (rc == LDPC_EUNSUPPORTED) {
-    d_walk = false;  // this code stays on the host planner
-    return false;
-  }
-  if (rc == LDPC_ETIMEOUT) {
-    if (d_walk_fallbacks++ == 0)
-      std::cerr << "ldpc_decoder_cb: device walk timed out; planning this call on the host"
-                << std::endl;
-    return false;
-  }
-  if (rc != LDPC_OK)
-    throw std::runtime_error(std::string("ldpc_decoder_cb: walk failed: ") + ldpc_last_error(d_ctx));
-  for (int i = 0; i < io.n_msgs; ++i) {
-    const int m = d_walk_msgs[(size_t)i];
-    if (m == LDPC_WALK_MSG_LOST)
-      std::cout << "MAX ERRORS; OUT OF SYNC" << std::endl;
-    else if (m == LDPC_WALK_MSG_INVERTED)
-      std::cout << "IN SYNC; PHASE INVERTED" << std::endl;
-    else
-      std::cout << "IN SYNC" << std::endl;
-  }
-  d_state = io.state;
-  d_errors = (unsigned)io.errors;
-  if (io.last_pass > INT64_MIN / 8) d_last_pass = d_abs + io.last_pass;
-  if (io.anchor_pos >= 0) d_anchor = (int)((d_abs + io.anchor_pos) % N);
-  d_grid_frames += io.grid_frames;
-  d_grid_fails += io.grid_fails;
-  while (d_grid_frames > 4096) {
-    d_grid_frames *= 0.5;
-    d_grid_fails *= 0.5;
-  }
-  d_abs += io.consumed;
-  d_frames_decoded += io.requests;
-  d_launches += 1;
-  d_walk_calls += 1;
-  consume_each((int)io.consumed);
-  produced = io.produced;
-  if (d_profile) {
-    const double dt = now_s() - t0;
-    d_prof[0] += dt;
-    d_walk_prof[0] += 1e6 * dt;
-    d_walk_prof[1] += io.walk_us;
-    d_walk_prof[2] += io.wait_us;
-    if (getenv("LDPC_BLOCK_PROFILE")[0] == '2')
-      fprintf(stderr,
-              "general_work walk: %.1f us = device loop %.1f (waiting %.1f) + rest; %d windows, "
-              "%d unplanned, %d steps, %d restarts, %lld items\n",
-              1e6 * dt, io.walk_us, io.wait_us, io.requests, io.surprises, io.steps, io.restarts,
-              (long long)io.consumed);
-  }
-  return true;
-}
-
 int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_items,
                                        gr_vector_const_void_star &input_items,
                                        gr_vector_void_star &output_items) {
@@ -651,15 +514,6 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   unsigned char *out = (unsigned char *)output_items[0];
   const int N = (int)d_N;
   const int nin = ninput_items[0];
-  const bool walk = pick_walk();
-  const double t_pick = d_walk_mode < 0 ? now_s() : 0.0;
-  if (walk) {
-    int produced = 0;
-    if (walk_call(in, nin, noutput_items, out, produced)) {
-      if (d_walk_mode < 0) note_cost(true, 1e6 * (now_s() - t_pick), produced);
-      return produced;
-    }
-  }
   const size_t npos = (size_t)std::max(nin - N + 1, 0);
   // the memo and the jump table keep their size between calls: only the
   // entries the last call set go back to "not decoded" (a full reset was
@@ -708,7 +562,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
     stage_async(in, 2 * (int64_t)nin, max_windows(d_N));
     staged = join_stage.pending = true;
   }
-  const int search_first = std::min(std::max(d_search_first, 1), max_windows(d_N));
+  const int search_first = std::min(kSearchFirst, max_windows(d_N));
   int out_budget = search_first;  // out-of-sync positions one launch may guess past
   bool first = true, last_out = false;
   double t0 = d_profile ? now_s() : 0.0;
@@ -723,7 +577,6 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       out_budget = search_first;
     last_out = now_out;
     d_want.clear();
-    d_forks.clear();
     Replay dry = r;
     if (d_profile) t0 = now_s();
     // how many windows one dry run may collect: a launch of up to ~1024
@@ -741,14 +594,6 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
     d_searches_now = d_searches >= 0 ? d_searches
                                      : (d_iterations <= 10 && !grid_fails_often() ? 4 : 0);
     replay(dry, false, nin, noutput_items, nullptr, out_budget, (size_t)cap);
-    // then the branches where a search position passes, nearest first, while
-    // the launch has room: windows up to about one per wave slot of the GPU
-    // cost little more than the launch's latency (50 iterations of one frame)
-    if (d_fork)
-      for (int64_t q : d_forks) {
-        if (d_want.size() >= (size_t)std::min(d_budget, max_windows(d_N))) break;
-        fork(q, nin);
-      }
     if (d_debug)
       std::cerr << "ldpc_decoder_cb: stall at " << r.consumed << " state " << r.state
                 << " errors " << r.errors << " grid " << d_anchor << ": launch " << d_want.size()
@@ -781,7 +626,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   if (d_profile) {
     d_prof[1] += now_s() - t0;
     d_prof[0] += now_s() - t_call;
-    if (getenv("LDPC_BLOCK_PROFILE")[0] == '2') {  // a line per call
+    if (d_profile_calls) {  // a line per call
       static double last[4] = {0, 0, 0, 0};
       fprintf(stderr,
               "general_work call: %.1f us = replay %.1f + dry runs %.1f + decode launches %.1f\n",
@@ -799,26 +644,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   d_errors = r.errors;
   d_abs += r.consumed;
   consume_each(r.consumed);
-  if (d_walk_mode < 0 && !walk) note_cost(false, 1e6 * (now_s() - t_pick), r.produced);
   return r.produced;
-}
-
-bool ldpc_decoder_cb_impl::pick_walk() {
-  if (d_backend || !d_walk || d_walk_mode == 0) return false;
-  if (d_walk_mode == 1) return true;
-  if (d_iterations > 10) return false;
-  ++d_auto_calls;
-  if (d_cost[0] == 0.0) return false;  // the planner first (the first call also acquires)
-  if (d_cost[1] == 0.0) return true;
-  const bool better = d_cost[1] < d_cost[0];
-  return d_auto_calls % 32 == 0 ? !better : better;
-}
-
-void ldpc_decoder_cb_impl::note_cost(bool walk, double us, int produced) {
-  if (produced < 256) return;  // a short call says little
-  const double c = us / produced;
-  double &e = d_cost[walk ? 1 : 0];
-  e = e == 0.0 ? c : 0.75 * e + 0.25 * c;
 }
 
 }  // namespace ldpc_ece535a

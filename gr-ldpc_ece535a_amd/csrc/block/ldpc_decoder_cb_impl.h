@@ -44,11 +44,10 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   int64_t d_launches = 0;
   // A worker thread stages each call's span (ldpc_stage_span: the real parts
   // copied into pinned memory and sent to the device) while general_work
-  // plans its first launch; joined before that launch.  LDPC_BLOCK_STAGE_THREAD=0:
-  // staged inline.
-  // With the window server (ldpc_serve_begin: one persistent launch serves
-  // every round of the call) the worker also starts the launch, right behind
-  // the span's copy in the context's stream.
+  // plans its first round, and then starts the call's window server
+  // (ldpc_serve_begin: one persistent launch serves every round of the call)
+  // right behind the span's copy in the context's stream; joined before the
+  // first round.
   struct Stager {
     std::thread th;
     std::mutex mu;
@@ -64,87 +63,52 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
     int serve_rc = 0;            // ldpc_serve_begin's result
     int run();                   // stage (+ serve); returns the staging result
   } d_stager;
-  bool d_stage_thread = !(getenv("LDPC_BLOCK_STAGE_THREAD") && getenv("LDPC_BLOCK_STAGE_THREAD")[0] == '0');
   // Rounds of windows through the window server (ldpc_serve_*), one launch
-  // per call; false: a launch per round (ldpc_decode_windows), and for codes
+  // per call; false: a launch per round (ldpc_decode_windows), also for codes
   // or methods the server does not take (LDPC_BLOCK_SERVE=0 forces it, A/B).
   bool d_serve = !(getenv("LDPC_BLOCK_SERVE") && getenv("LDPC_BLOCK_SERVE")[0] == '0');
   bool d_serving = false;  // this call's server is running
   void stage_async(const float *in, int64_t n_floats, int max_windows);
   int stage_wait();
-  // Two ways to run a call, same outputs: the host planner below (dry-run
-  // replay + window launches; the default) or the whole frame loop as one
-  // device launch (ldpc_walk_span; LDPC_BLOCK_WALK=1).  LDPC_BLOCK_WALK=auto:
-  // at iteration caps <= 10 the block times both on its own stream and keeps
-  // the faster, trying the other again every 32 calls (measured: the two tie
-  // at 4 dB, the planner is 3x faster at 2 dB, and the probes cost more than
-  // they gain over a short stream -- profiles/round4/block/walk/).  A backend,
-  // or a code the walk does not take: the planner.
-  int d_walk_mode = !getenv("LDPC_BLOCK_WALK")              ? 0
-                    : getenv("LDPC_BLOCK_WALK")[0] == '1'   ? 1
-                    : getenv("LDPC_BLOCK_WALK")[0] == 'a'   ? -1
-                                                            : 0;
-  bool d_walk = true;              // the walk takes this code (until it says otherwise)
-  double d_cost[2] = {0.0, 0.0};   // auto: us per output byte, planner / walk (decayed)
-  int64_t d_auto_calls = 0;
-  bool pick_walk();
-  void note_cost(bool walk, double us, int produced);
-  std::vector<uint8_t> d_walk_msgs;
-  int64_t d_walk_calls = 0, d_walk_fallbacks = 0;
-  double d_walk_prof[3] = {0, 0, 0};  // host call, device loop, device waits (us)
-  bool walk_call(const float *in, int nin, int noutput_items, unsigned char *out, int &produced);
-  bool d_debug = getenv("LDPC_BLOCK_DEBUG") != nullptr;  // one line per launch on stderr
+  bool d_debug = getenv("LDPC_BLOCK_DEBUG") != nullptr;  // one line per round on stderr
   // LDPC_BLOCK_PROFILE: host time split of general_work, printed when destroyed
+  // (=2: also a line per call)
   bool d_profile = getenv("LDPC_BLOCK_PROFILE") != nullptr;
-  double d_prof[4] = {0, 0, 0, 0};  // total, exact replay, dry runs, decode launches
+  bool d_profile_calls = d_profile && getenv("LDPC_BLOCK_PROFILE")[0] == '2';
+  double d_prof[4] = {0, 0, 0, 0};  // total, exact replay, dry runs, decode rounds
   static double now_s();
   // In-sync frames guessed to pass are also wanted at the other polarity
-  // (LDPC_BLOCK_SPEC_BOTH):
-  // 0: never, 1: always, otherwise (default) when more than 1 in d frames on
-  // the grid fail (then sync losses, and their retries, are frequent; the
-  // reference's 4 dB stream fails 1 in 4..8, 2 dB more than 1 in 2).
-  // d = LDPC_BLOCK_SPEC_DIV, default 4 (was 8: at 4 dB / 5 iterations it
-  // requested every grid frame twice, 9.1 windows per output frame)
-  int d_spec_both = getenv("LDPC_BLOCK_SPEC_BOTH") ? atoi(getenv("LDPC_BLOCK_SPEC_BOTH")) : 2;
-  int d_spec_div = getenv("LDPC_BLOCK_SPEC_DIV") ? std::max(1, atoi(getenv("LDPC_BLOCK_SPEC_DIV"))) : 4;
-  bool grid_fails_often() const { return d_spec_div * d_grid_fails > d_grid_frames; }
+  // when more than 1 in 4 frames on the grid fail (then sync losses, and
+  // their "-tx" retries, are frequent; the reference's 4 dB stream fails 1 in
+  // 4..8, 2 dB more than 1 in 2).  (1 in 8 requested every grid frame twice at
+  // 4 dB / 5 iterations: 9.1 windows per output frame.)
+  bool grid_fails_often() const { return 4 * d_grid_fails > d_grid_frames; }
   double d_grid_frames = 0, d_grid_fails = 0;  // decayed counts of in-sync frames
-  // A/B knob: LDPC_BLOCK_FORK=1 also decodes the branches where a search position syncs
-  bool d_fork = getenv("LDPC_BLOCK_FORK") && getenv("LDPC_BLOCK_FORK")[0] == '1';
-  // A/B knob: LDPC_BLOCK_ANCHOR=0 guesses every in-sync window passes
-  bool d_anchor_guess = !(getenv("LDPC_BLOCK_ANCHOR") && getenv("LDPC_BLOCK_ANCHOR")[0] == '0');
   // A/B knob: LDPC_BLOCK_SEARCHES=k stops a dry run at its (k+1)-th guessed
   // search (0: no limit).  Each search passes a misaligned window somewhere
   // with high probability (~1 % per window, ~126 windows) and the searches
-  // after such a false sync move, yet a limit of 1 or 2 costs more launches
+  // after such a false sync move, yet a limit of 1 or 2 costs more rounds
   // than the windows it saves (tools/block_policy_sim.py)
   // Default (unset): 4 for short windows (iterations <= 10) while the grid
   // rarely fails, no limit otherwise: at 4 dB / 5 iterations 26 launches of
   // 3.7 windows per output frame beat 14 of 9.1 (128 vs 119 and
-  // 123 vs 117.5 Mbit/s on two boxes, profiles/round4/block/ab_spec_searches.txt); where a launch costs a
+  // 123 vs 117.5 Mbit/s on two boxes, profiles/round4/block/ab_spec_searches.txt); where a round costs a
   // 50-iteration window's latency, or searches are frequent, the extra
-  // launches cost more than the windows they save
+  // rounds cost more than the windows they save
   int d_searches = getenv("LDPC_BLOCK_SEARCHES") ? atoi(getenv("LDPC_BLOCK_SEARCHES")) : -1;
   int d_searches_now = 0;  // this dry run's limit
-  // out-of-sync positions a dry run may guess past in a row before the launch
-  // (LDPC_BLOCK_SEARCH_FIRST, default 128; x4 per launch while the search goes on)
-  int d_search_first = getenv("LDPC_BLOCK_SEARCH_FIRST") ? atoi(getenv("LDPC_BLOCK_SEARCH_FIRST"))
-                                                         : 128;
-  // A/B knob: LDPC_BLOCK_OPPOSITE=0 ignores, when guessing a window, that the
-  // same samples at the other polarity are known to pass
-  bool d_opposite = !(getenv("LDPC_BLOCK_OPPOSITE") && getenv("LDPC_BLOCK_OPPOSITE")[0] == '0');
-  // windows a launch is filled up to with branch speculation (LDPC_BLOCK_BUDGET)
-  int d_budget = getenv("LDPC_BLOCK_BUDGET") ? atoi(getenv("LDPC_BLOCK_BUDGET")) : 3072;
+  // out-of-sync positions a dry run may guess past in a row before the round
+  // (x4 per round while the search goes on)
+  static const int kSearchFirst = 128;
   // A/B knob: LDPC_BLOCK_MAXWANT=n stops a dry run once it has collected n
-  // windows; -1: the launch limit, max_windows(N), always; 0 (default): 1024
-  // while grid frames rarely fail, else the launch limit
+  // windows; -1: the round limit, max_windows(N), always; 0 (default): 1024
+  // while grid frames rarely fail, else the round limit
   int d_max_want = getenv("LDPC_BLOCK_MAXWANT") ? atoi(getenv("LDPC_BLOCK_MAXWANT")) : 0;
   // grid: absolute sample index of the call's first input item; the phase
   // (mod N) of the last two consecutive frames that passed in sync (-1: none yet)
   int64_t d_abs = 0;
   int d_anchor = -1;
   int64_t d_last_pass = -1;  // absolute position of the last window passing in sync
-  std::vector<int64_t> d_forks;  // dry run: search positions guessed to fail
 
   // general_work's decode memo for the current call: the result of window
   // (position p, polarity) -- p in samples from the call's first input item,
@@ -187,8 +151,6 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   int pass_run(int pol, int pos, int nin);
   // Dry run: adds window (pos, pol) to d_want unless decoded or wanted (memo -2)
   void want(int64_t pos, int pol, int nin);
-  // Dry run: the windows the loop needs if search position q syncs
-  void fork(int64_t q, int nin);
   // Decodes the windows d_want of the call's input into the memo (one
   // launch on the GPU; the test seam decodes runs of equally spaced windows).
   void decode_wanted(const float *in, int nin, bool first);

@@ -60,15 +60,6 @@ struct ldpc_ctx {
   int64_t *h_win = nullptr;
   size_t h_win_bytes = 0;
   int64_t span_samples = 0;
-  // ldpc_walk_span (ldpc_walk.hip): [ctl | res | req] on the device,
-  // zeroed when (re)allocated and when the epoch wraps; summary, messages and
-  // output bytes in mapped pinned memory the walker writes directly
-  void *d_walk = nullptr;
-  size_t walk_bytes = 0;
-  int64_t walk_cap = 0;  // positions per polarity
-  uint32_t walk_epoch = 0;
-  uint8_t *h_walk = nullptr;
-  size_t h_walk_bytes = 0;
   // the window server (ldpc_serve.hip, ldpc_serve_*): mapped pinned memory
   // [round word | keys | result granules] for srv_cap windows, the device
   // copy of the round word, and the running launch's parameters
@@ -76,17 +67,18 @@ struct ldpc_ctx {
   uint8_t *h_srv = nullptr;
   int64_t srv_cap = 0;
   uint64_t *d_srv_ctl = nullptr;
+  int64_t *d_srv_keys = nullptr;  // the round's keys as the poller copies them
   uint32_t srv_epoch = 0;  // the last round posted (grows across launches)
   int srv_method = 0, srv_iters = 0, srv_prec = 0;
   int srv_launches = 0, srv_rounds = 0;
   int srv_workgroups = 0;  // decoder workgroups of the running launch
+  double dbg[4] = {0, 0, 0, 0};  // LDPC_SERVE_DEBUG: rounds, host us, key-read us, done us
   // in-flight stream set for throughput callers (ldpc_ctx_streams): streams
   // verified to run concurrently, i.e. on distinct hardware queues
   std::vector<hipStream_t> tp_streams;
   uint32_t *d_probe = nullptr;
-  // large-code min-sum: 2 narrow-chunk pipeline (ldpc_graph_msn.hip), 0 the
-  // edge-message passes (ldpc_graph.hip)
-  int ms_mode = 2;
+  // large-code min-sum runs on the narrow-chunk pipeline (ldpc_graph_msn.hip)
+  bool narrow = false;  // large code with the min-sum pipeline's tables (M <= kMsnMaxRows)
   ldpc::MsnTables msn;  // storage order of the narrow pipeline
   int32_t *d_msn[4] = {nullptr, nullptr, nullptr, nullptr};  // rx cx corig cpos
   ldpc::MsnDesc *d_msnd[2] = {nullptr, nullptr};                               // rdesc cdesc
@@ -214,8 +206,8 @@ void kernel_shape(int nw, int slots, int dc_max, int dv_max, int &dcn, int &dvn,
 }
 
 // Edge / column / row tables of the decoder's H (see ldpc_kernels.hpp), at
-// the cells and positions plan_layout chooses (LDPC_LAYOUT=0: the plain CSR
-// layout, for A/B runs).
+// the cells and positions plan_layout chooses (search false: the plain CSR
+// layout, LDPC_FLAG_PLAIN_LAYOUT).
 int build_tables(ldpc_ctx *ctx, std::vector<EdgeRowRec> &erecs, std::vector<EdgeColRec> &crecs,
                  std::vector<ColRec> &cols, std::vector<uint64_t> &rowmask,
                  std::vector<uint16_t> &lane_col, std::vector<uint8_t> &col_lane,
@@ -260,9 +252,8 @@ int build_tables(ldpc_ctx *ctx, std::vector<EdgeRowRec> &erecs, std::vector<Edge
   int dcn, dvn;
   bool cols_k;
   kernel_shape(ctx->nw, ctx->slots, ctx->dc_max, ctx->dv_max, dcn, dvn, cols_k);
-  const char *lv = getenv("LDPC_LAYOUT");
   const ldpc::EdgeLayout lay = ldpc::plan_layout(M, N, erow, ecol, ctx->slots, ctx->nw, dcn, dvn,
-                                                 cols_k, search && !(lv && lv[0] == '0'));
+                                                 cols_k, search);
   const std::vector<int> &cell = lay.slot, &pos = lay.pos;
   if (cell_out) *cell_out = cell;
   ctx->layout_model[0] = lay.searched ? 1 : 0;
@@ -328,10 +319,15 @@ size_t srv_bytes(int64_t cap) { return srv_res_off(cap) + (size_t)cap * 8; }
 
 // Posts round word (epoch << 32) | B after the keys (x86 stores are ordered;
 // the device reads the keys only after it has seen the round word).
+// Round word (ldpc_kernels.hpp): (epoch << 32) | (session << 20) | B; the
+// session tells a launch still polling after its quit round was overwritten
+// that the rounds are no longer its own.
 void serve_post(ldpc_ctx *ctx, uint32_t B) {
   ++ctx->srv_epoch;  // < 2^23: ldpc_serve_begin restarts the epochs well before
   __atomic_store_n(reinterpret_cast<uint64_t *>(ctx->h_srv),
-                   ((uint64_t)ctx->srv_epoch << 32) | B, __ATOMIC_RELEASE);
+                   ((uint64_t)ctx->srv_epoch << 32) | ((uint64_t)(ctx->srv_launches & 0xFFF) << 20) |
+                       (B & ldpc::kServeB),
+                   __ATOMIC_RELEASE);
 }
 
 // Ends a running window server: posts its quit round and waits for the
@@ -339,7 +335,7 @@ void serve_post(ldpc_ctx *ctx, uint32_t B) {
 // behind a launch that polls for rounds.
 void serve_stop(ldpc_ctx *ctx) {
   if (!ctx || !ctx->serving) return;
-  serve_post(ctx, ldpc::kServeQuit);
+  serve_post(ctx, ldpc::kServeB);
   ctx->serving = false;
   (void)hipStreamSynchronize(ctx->stream);
 }
@@ -496,8 +492,12 @@ ldpc::CodeView code_view(const ldpc_ctx *ctx) {
 int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int precision, void *st) {
   const ldpc::GraphView g = graph_view(ctx);
   const bool want_post = a.llr != nullptr;
-  if (method == 0 && ctx->ms_mode == 2) {
+  if (method == 0) {
     // min-sum: narrow chunks, gathered state L2-resident per XCD
+    if (!ctx->narrow)
+      return set_err(ctx, LDPC_EUNSUPPORTED,
+                     "large-code min-sum needs M <= " + std::to_string(ldpc::kMsnMaxRows) +
+                         " check rows (the narrow-chunk pipeline's limit)");
     ldpc::MsnView v;
     v.rx = ctx->d_msn[0];
     v.cx = ctx->d_msn[1];
@@ -513,7 +513,7 @@ int decode_graph(ldpc_ctx *ctx, const ldpc::DecodeArgs &a, int method, int preci
     v.KB = g.KB;
     v.dc_max = g.dc_max;
     v.dv_max = g.dv_max;
-    v.out_var = ctx->msn.out_var && !getenv("LDPC_MSN_POST") ? 1 : 0;
+    v.out_var = ctx->msn.out_var ? 1 : 0;
     int C = ldpc::msn_default_chunks();
     const int need_c = (a.B + ldpc::kMsnFrames - 1) / ldpc::kMsnFrames;
     if (need_c < C) C = need_c >= 8 ? (need_c + 7) / 8 * 8 : need_c;
@@ -857,13 +857,9 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     return nullptr;
   }
   ctx->device = device;
-  {  // A/B knob: LDPC_MS_PIPELINE=0 edge-message passes, 2 (default) the
-     // narrow-chunk pipeline
-    const char *v = getenv("LDPC_MS_PIPELINE");
-    ctx->ms_mode = v && v[0] == '0' ? 0 : 2;
-    // the narrow pipeline packs a row and an edge's place in it in 32 bits
-    if (ctx->graph && ctx->ms_mode == 2 && (ctx->M >= (1 << 24) || ctx->dc_max > 128)) ctx->ms_mode = 0;
-    if (ctx->graph && ctx->ms_mode == 2) {
+  {  // large-code min-sum: the narrow-chunk pipeline's tables
+    ctx->narrow = ctx->graph && ctx->M <= ldpc::kMsnMaxRows;
+    if (ctx->narrow) {
       try {
         ldpc::msn_build(ctx->M, ctx->N, ctx->rp, ctx->ci, ctx->msn);
       } catch (const std::exception &ex) {
@@ -883,7 +879,7 @@ ldpc_ctx *finish_create(ldpc_ctx *ctx, int flags, int device) {
     upload(ctx, &ctx->d_cp, cp, "upload(col_ptr)", what, e);
     upload(ctx, &ctx->d_ce, ce, "upload(col_edges)", what, e);
     upload(ctx, &ctx->d_cr, cr, "upload(col_rows)", what, e);
-    if (ctx->ms_mode == 2) {
+    if (ctx->narrow) {
       const std::vector<int32_t> *t[4] = {&ctx->msn.rx, &ctx->msn.cx, &ctx->msn.corig,
                                           &ctx->msn.cpos};
       for (int i = 0; i < 4; ++i) upload(ctx, &ctx->d_msn[i], *t[i], "upload(storage order)", what, e);
@@ -970,8 +966,6 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->h_ctrl) (void)hipHostFree(ctx->h_ctrl);
   if (ctx->d_wstage) (void)hipFree(ctx->d_wstage);
   if (ctx->h_win) (void)hipHostFree(ctx->h_win);
-  if (ctx->d_walk) (void)hipFree(ctx->d_walk);
-  if (ctx->h_walk) (void)hipHostFree(ctx->h_walk);
   if (ctx->h_srv) (void)hipHostFree(ctx->h_srv);
   for (hipStream_t t : ctx->tp_streams) {
     (void)hipStreamSynchronize(t);
@@ -979,6 +973,7 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   }
   if (ctx->d_probe) (void)hipFree(ctx->d_probe);
   if (ctx->d_srv_ctl) (void)hipFree(ctx->d_srv_ctl);
+  if (ctx->d_srv_keys) (void)hipFree(ctx->d_srv_keys);
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
     if (p) (void)hipFree(p);
@@ -1035,7 +1030,7 @@ int ldpc_ctx_path(const ldpc_ctx *ctx) {
 
 int ldpc_ctx_pipeline(const ldpc_ctx *ctx, int *frames_per_chunk, int *chunks) {
   if (!ctx) return LDPC_EINVAL;
-  const bool narrow = ctx->graph && ctx->ms_mode == 2;
+  const bool narrow = ctx->narrow;
   if (frames_per_chunk) *frames_per_chunk = narrow ? ldpc::kMsnFrames : 0;
   if (chunks) *chunks = narrow ? ldpc::msn_default_chunks() : 0;
   return narrow ? 1 : 0;
@@ -1239,10 +1234,8 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   a.ticket_base = ctx->queues[q].base;
   a.waves = 0;
   // short frames (iteration cap <= 10): fixed frame stride, no queue atomics
-  // (ldpc_kernels.hpp DecodeArgs::static_stride; LDPC_STATIC_ITERS overrides)
-  static const int static_iters =
-      getenv("LDPC_STATIC_ITERS") ? atoi(getenv("LDPC_STATIC_ITERS")) : 10;
-  a.static_stride = max_iters <= static_iters ? 1 : 0;
+  // (ldpc_kernels.hpp DecodeArgs::static_stride)
+  a.static_stride = max_iters <= 10 ? 1 : 0;
   a.fair_cycles = ctx->fair_cycles;
   rc = ldpc::launch_decode(code_view(ctx), a, method, precision, ctx->slots, ctx->nw,
                            ctx->waves_per_cu, ctx->schedule, st);
@@ -1438,9 +1431,8 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   // Small codes: the kernel reads the (pinned, mapped) window list and writes
   // its packed bytes and syndrome weights into pinned memory itself -- a few
   // bytes per window over the bus, and no DMA round trip on a launch whose
-  // latency is that of one frame (LDPC_WIN_COPY=1: the copies instead)
-  static const bool copy_mode = getenv("LDPC_WIN_COPY") && getenv("LDPC_WIN_COPY")[0] == '1';
-  const bool direct = !ctx->graph && !copy_mode;
+  // latency is that of one frame
+  const bool direct = !ctx->graph;
   if (direct) {
     void *dv = nullptr;
     if ((e = hipHostGetDevicePointer(&dv, ctx->h_win, 0)) != hipSuccess)
@@ -1473,17 +1465,10 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
     ctx->win_prof[1] += t1 - t0;
     t0 = t1;
   }
-  // wait for the launch; polling instead of hipStreamSynchronize
-  // (LDPC_WIN_SPIN=1) measured no faster (profiles/round2/block/window_latency.txt)
-  static const bool no_spin = !(getenv("LDPC_WIN_SPIN") && getenv("LDPC_WIN_SPIN")[0] == '1');
-  if (no_spin) {
-    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
-      return hip_err(ctx, e, "hipStreamSynchronize");
-  } else {
-    while ((e = hipStreamQuery(ctx->stream)) == hipErrorNotReady) {
-    }
-    if (e != hipSuccess) return hip_err(ctx, e, "hipStreamQuery");
-  }
+  // wait for the launch (polling measured no faster,
+  // profiles/round2/block/window_latency.txt)
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipStreamSynchronize");
   if (ctx->win_profile) {
     const double t1 = tnow();
     ctx->win_prof[2] += t1 - t0;
@@ -1506,217 +1491,13 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
   return LDPC_OK;
 }
 
-// The walker's buffers for spans of up to `cap` positions (ldpc_walk_span).
-// request slots: each window is asked for at most once (2 per position);
-// decoders claim up to kWalkClaimSlack slots past the last request
-size_t walk_layout(int64_t cap, size_t off[4]) {
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  off[0] = 0;                                                       // ctl
-  off[1] = al((size_t)ldpc::kWalkCtlWords * 4);                     // res
-  off[2] = off[1] + al((size_t)2 * cap * 8);                        // req
-  off[3] = off[2];
-  return off[2] + al((size_t)(2 * cap + ldpc::kWalkClaimSlack) * 8);
-}
-
-int walk_span_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, const float *in,
-                   int64_t n_in_floats, int elem_stride, int reuse_span, int noutput_bytes,
-                   ldpc_walk_io *io, uint8_t *out, uint8_t *msgs, int msgs_cap) {
-  serve_stop(ctx);
-  int rc = check_decode_args(ctx, method, max_iters, 1, precision, 1, elem_stride, ctx ? ctx->N : 1);
-  if (rc != LDPC_OK) return rc;
-  const int N = ctx->N, mo = ctx->M / 8;
-  if (ctx->graph || ctx->KB > 4 || mo > 4 || mo < 1 || N > 64)
-    return set_err(ctx, LDPC_EUNSUPPORTED,
-                   "the device walk takes small codes with N <= 64, M/8 <= 4, KB <= 4");
-  if (!in || !io || (noutput_bytes > 0 && !out) || msgs_cap < 0 || (msgs_cap > 0 && !msgs) ||
-      noutput_bytes < 0)
-    return set_err(ctx, LDPC_EINVAL, "bad walk buffers");
-  if (io->state < 0 || io->state > 2 || io->errors < 0 || io->errors > 10)
-    return set_err(ctx, LDPC_EINVAL, "walk state out of range");
-  // one walk takes at most kWalkMaxSpan samples (the walker's bitmap); the
-  // loop's state carries over to the next call as the reference's does
-  const int64_t S = std::min<int64_t>((n_in_floats + elem_stride - 1) / elem_stride,
-                                      ldpc::kWalkMaxSpan);
-  const int nout = noutput_bytes / mo;
-  const int64_t anchor_in = io->anchor_pos;
-  io->consumed = 0;
-  io->produced = 0;
-  io->n_msgs = 0;
-  io->anchor_pos = -1;
-  io->grid_frames = io->grid_fails = io->requests = io->surprises = io->steps = io->restarts = 0;
-  io->walk_us = io->wait_us = 0.0;
-  if (S < N || nout == 0 || msgs_cap < 2) return LDPC_OK;  // the loop would not run (:146-147)
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  hipError_t e = hipSetDevice(ctx->device);
-  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  const auto tnow = []() {
-    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-  };
-  const double t0 = tnow();
-  // the span, as for ldpc_decode_windows
-  rc = ensure_window_stage(ctx, al((size_t)S * 4));
-  if (rc != LDPC_OK) return rc;
-  if (!(reuse_span && ctx->span_samples == S)) {
-    rc = copy_span(ctx, in, S, elem_stride, (float *)ctx->d_wstage);
-    if (rc != LDPC_OK) return rc;
-  }
-  // device buffers
-  size_t off[4];
-  bool zero = false;
-  if (S > ctx->walk_cap) {
-    const int64_t cap = std::max<int64_t>(S + S / 2, 1 << 16);
-    const size_t bytes = walk_layout(cap, off);
-    if (ctx->d_walk) {
-      (void)hipStreamSynchronize(ctx->stream);
-      (void)hipFree(ctx->d_walk);
-      ctx->d_walk = nullptr;
-      ctx->walk_cap = 0;
-    }
-    if ((e = hipMalloc(&ctx->d_walk, bytes)) != hipSuccess) return hip_err(ctx, e, "hipMalloc(walk)");
-    ctx->walk_bytes = bytes;
-    ctx->walk_cap = cap;
-    zero = true;
-  }
-  walk_layout(ctx->walk_cap, off);
-  if (++ctx->walk_epoch >= (1u << 23)) {  // tags are 23 bits: start over from zeroed buffers
-    ctx->walk_epoch = 1;
-    zero = true;
-  }
-  if (zero && (e = hipMemsetAsync(ctx->d_walk, 0, ctx->walk_bytes, ctx->stream)) != hipSuccess)
-    return hip_err(ctx, e, "hipMemsetAsync(walk)");
-  // the queue heads and the done word, every call
-  if ((e = hipMemsetAsync(ctx->d_walk, 0, (size_t)ldpc::kWalkCtlWords * 4, ctx->stream)) != hipSuccess)
-    return hip_err(ctx, e, "hipMemsetAsync(walk ctl)");
-  // mapped host memory: summary, messages, output bytes
-  const size_t h_need = al(sizeof(ldpc::WalkSummary)) + al((size_t)msgs_cap) + al((size_t)nout * mo);
-  if (h_need > ctx->h_walk_bytes) {
-    if (ctx->h_walk) {
-      (void)hipStreamSynchronize(ctx->stream);
-      (void)hipHostFree(ctx->h_walk);
-      ctx->h_walk = nullptr;
-      ctx->h_walk_bytes = 0;
-    }
-    const size_t want = std::max(h_need + h_need / 2, (size_t)1 << 16);
-    if ((e = hipHostMalloc((void **)&ctx->h_walk, want, hipHostMallocMapped | hipHostMallocCoherent)) !=
-        hipSuccess)
-      return hip_err(ctx, e, "hipHostMalloc(walk)");
-    ctx->h_walk_bytes = want;
-  }
-  void *dh = nullptr;
-  if ((e = hipHostGetDevicePointer(&dh, ctx->h_walk, 0)) != hipSuccess)
-    return hip_err(ctx, e, "hipHostGetDevicePointer(walk)");
-  char *base = (char *)ctx->d_walk;
-  ldpc::WalkArgs w{};
-  w.ctl = (uint32_t *)(base + off[0]);
-  w.res = (uint64_t *)(base + off[1]);
-  w.req = (uint64_t *)(base + off[2]);
-  w.sum = (ldpc::WalkSummary *)dh;
-  w.msgs = (uint8_t *)dh + al(sizeof(ldpc::WalkSummary));
-  w.out = w.msgs + al((size_t)msgs_cap);
-  w.cap = ctx->walk_cap;
-  w.req_cap = 2 * ctx->walk_cap + ldpc::kWalkClaimSlack;
-  w.nin = S;
-  w.N = N;
-  w.M = ctx->M;
-  w.KB = ctx->KB;
-  w.mo = mo;
-  w.thr = ctx->M / 8;  // :142
-  w.nout = nout;
-  w.msgs_cap = msgs_cap;
-  w.state = io->state;
-  w.errors = io->errors;
-  w.last_pass = io->last_pass;
-  w.anchor = anchor_in >= 0 ? anchor_in % N : -1;
-  w.epoch = ctx->walk_epoch;
-  const int lead = getenv("LDPC_WALK_LEAD") ? atoi(getenv("LDPC_WALK_LEAD")) : 512;
-  static const double deadline_ms =
-      getenv("LDPC_WALK_DEADLINE_MS") ? atof(getenv("LDPC_WALK_DEADLINE_MS")) : 200.0;
-  w.lead = std::max(lead, 1);
-  w.deadline = (uint64_t)(deadline_ms * 1e5);  // 100 MHz ticks
-  // LDPC_WALK_TRACE=2: event records of each walk into LDPC_WALK_TRACE_FILE
-  static uint64_t *d_trace = nullptr;
-  const bool tracing = getenv("LDPC_WALK_TRACE") && getenv("LDPC_WALK_TRACE")[0] == '2';
-  const int trace_cap = 1 << 16;
-  if (tracing && !d_trace && hipMalloc(&d_trace, (size_t)trace_cap * 32) != hipSuccess) d_trace = nullptr;
-  w.trace = tracing ? d_trace : nullptr;
-  w.trace_cap = trace_cap;
-  ldpc::DecodeArgs a{};
-  a.in = (const float *)ctx->d_wstage;
-  a.cw_stride = N;
-  a.elem_stride = 1;
-  a.polarity = 1.0f;
-  a.max_iters = max_iters;
-  a.et_period = 1;
-  a.fair_cycles = 0;
-  const double t1 = tnow();
-  const int lr = ldpc::launch_walk(code_view(ctx), a, w, method, precision, ctx->slots, ctx->nw, 0,
-                                   ctx->stream);
-  const double t2 = tnow();
-  if (lr == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no walk kernel for this code shape");
-  if (lr != 0) return hip_err(ctx, hipGetLastError(), "walk launch");
-  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
-    return hip_err(ctx, e, "hipStreamSynchronize(walk)");
-  const double t3 = tnow();
-  const ldpc::WalkSummary &sm = *(const ldpc::WalkSummary *)ctx->h_walk;
-  io->walk_us = (double)sm.total_ticks * 1e-2;
-  io->wait_us = (double)sm.wait_ticks * 1e-2;
-  io->requests = sm.requests;
-  io->surprises = sm.surprises;
-  io->steps = sm.steps;
-  io->restarts = sm.restarts;
-  if (tracing) {
-    uint32_t dc[2] = {0, 0};
-    if (hipMemcpy(dc, (char *)ctx->d_walk + 264 * 4, 8, hipMemcpyDeviceToHost) == hipSuccess && dc[1])
-      fprintf(stderr, "walk decoders: %u windows, %.2f us each\n", dc[1], 1e-2 * dc[0] / dc[1]);
-  }
-  if (tracing && d_trace) {
-    std::vector<uint64_t> h((size_t)trace_cap * 4);
-    if (hipMemcpy(h.data(), d_trace, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-      const char *fn = getenv("LDPC_WALK_TRACE_FILE") ? getenv("LDPC_WALK_TRACE_FILE") : "walk_trace.bin";
-      if (FILE *f = fopen(fn, "ab")) {
-        const uint64_t hdr[4] = {~0ull, (uint64_t)sm.steps, (uint64_t)sm.total_ticks, 0};
-        fwrite(hdr, 8, 4, f);
-        // records up to the first unwritten one (zero first word)
-        size_t n = 0;
-        while (n < (size_t)trace_cap && h[n * 4] != 0) ++n;
-        fwrite(h.data(), 8, n * 4, f);
-        fclose(f);
-      }
-    }
-    (void)hipMemset(d_trace, 0, (size_t)trace_cap * 32);
-  }
-  if (getenv("LDPC_WALK_TRACE"))
-    fprintf(stderr,
-            "walk: %.1f us (waiting %.1f), %d steps, %d windows; surprises sync %d search %d retry "
-            "%d; guesses %d (%d wrong); restarts %d (%d behind); host: stage %.1f launch %.1f "
-            "wait %.1f us\n",
-            io->walk_us, io->wait_us, sm.steps, sm.requests, sm.diag[0], sm.diag[1], sm.diag[2],
-            sm.diag[3], sm.diag[4], sm.restarts, sm.diag[5], 1e6 * (t1 - t0), 1e6 * (t2 - t1),
-            1e6 * (t3 - t2));
-  if (sm.status != 0)
-    return set_err(ctx, LDPC_ETIMEOUT, sm.status == 2 ? "the walk's request queue ran out"
-                                                      : "a wait of the walk passed its deadline");
-  io->state = sm.state;
-  io->errors = sm.errors;
-  io->last_pass = sm.last_pass;
-  io->anchor_pos = sm.anchor_pos;
-  io->consumed = sm.consumed;
-  io->produced = sm.produced * mo;
-  io->n_msgs = sm.n_msgs;
-  io->grid_frames = sm.grid_frames;
-  io->grid_fails = sm.grid_fails;
-  const uint8_t *hm = ctx->h_walk + al(sizeof(ldpc::WalkSummary));
-  if (sm.n_msgs > 0) memcpy(msgs, hm, (size_t)sm.n_msgs);
-  if (sm.produced > 0) memcpy(out, hm + al((size_t)msgs_cap), (size_t)sm.produced * mo);
-  return LDPC_OK;
-}
-
-
 // Launches the window server for the context's parameters on its stream
 // (ctl zeroed first: it must read below every epoch the launch serves).
 int serve_launch(ldpc_ctx *ctx) {
   hipError_t e;
-  if ((e = hipMemsetAsync(ctx->d_srv_ctl, 0, 256, ctx->stream)) != hipSuccess)
+  if (!ctx->d_srv_ctl || !ctx->d_srv_keys || !ctx->h_srv)
+    return set_err(ctx, LDPC_EINVAL, "window server buffers missing");
+  if ((e = hipMemsetAsync(ctx->d_srv_ctl, 0, ldpc::kServeCtlBytes, ctx->stream)) != hipSuccess)
     return hip_err(ctx, e, "hipMemsetAsync(server ctl)");
   void *dh = nullptr;
   if ((e = hipHostGetDevicePointer(&dh, ctx->h_srv, 0)) != hipSuccess)
@@ -1725,13 +1506,17 @@ int serve_launch(ldpc_ctx *ctx) {
   sa.round = (const uint64_t *)dh;
   sa.keys = (const int64_t *)((uint8_t *)dh + srv_keys_off());
   sa.res = (uint64_t *)((uint8_t *)dh + srv_res_off(ctx->srv_cap));
+  sa.dkeys = ctx->d_srv_keys;
   sa.ctl = ctx->d_srv_ctl;
   const char *dl = getenv("LDPC_SERVE_DEADLINE_MS");
   sa.deadline = (uint64_t)((dl ? atof(dl) : 200.0) * 1e5);  // 100 MHz ticks
   sa.start_epoch = ctx->srv_epoch;
+  ctx->srv_launches += 1;  // this launch's session: the rounds posted from now on
+  sa.session = (uint32_t)ctx->srv_launches;
   // decoder workgroups per CU (capped by occupancy); 0 = as many as fit
-  static const int per_cu = getenv("LDPC_SERVE_BLOCKS_PER_CU") ? atoi(getenv("LDPC_SERVE_BLOCKS_PER_CU")) : 0;
-  sa.blocks_per_cu = per_cu;
+  const char *pc = getenv("LDPC_SERVE_BLOCKS_PER_CU");
+  sa.blocks_per_cu = pc ? atoi(pc) : 0;
+  sa.debug = getenv("LDPC_SERVE_DEBUG") ? 1 : 0;
   int wg = 0;
   ldpc::DecodeArgs a{};
   a.in = (const float *)ctx->d_wstage;
@@ -1745,7 +1530,6 @@ int serve_launch(ldpc_ctx *ctx) {
   ctx->srv_workgroups = wg;
   if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no window server for this code shape");
   if (rc != 0) return hip_err(ctx, hipGetLastError(), "window server launch");
-  ctx->srv_launches += 1;
   return LDPC_OK;
 }
 
@@ -1766,7 +1550,7 @@ int serve_begin_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, in
   }
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  if (!ctx->d_srv_ctl && (e = hipMalloc((void **)&ctx->d_srv_ctl, 256)) != hipSuccess)
+  if (!ctx->d_srv_ctl && (e = hipMalloc((void **)&ctx->d_srv_ctl, ldpc::kServeCtlBytes)) != hipSuccess)
     return hip_err(ctx, e, "hipMalloc(server ctl)");
   // a new buffer (or epochs near the end of their range) starts the epochs over:
   // the previous launch has finished first
@@ -1774,17 +1558,16 @@ int serve_begin_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, in
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->srv_cap < max_windows) {
       if (ctx->h_srv) (void)hipHostFree(ctx->h_srv);
-  for (hipStream_t t : ctx->tp_streams) {
-    (void)hipStreamSynchronize(t);
-    (void)hipStreamDestroy(t);
-  }
-  if (ctx->d_probe) (void)hipFree(ctx->d_probe);
+      if (ctx->d_srv_keys) (void)hipFree(ctx->d_srv_keys);
       ctx->h_srv = nullptr;
+      ctx->d_srv_keys = nullptr;
       ctx->srv_cap = 0;
       const int64_t cap = std::max<int64_t>(max_windows, 4096);
       if ((e = hipHostMalloc((void **)&ctx->h_srv, srv_bytes(cap),
                              hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
         return hip_err(ctx, e, "hipHostMalloc(server)");
+      if ((e = hipMalloc((void **)&ctx->d_srv_keys, (size_t)cap * 8)) != hipSuccess)
+        return hip_err(ctx, e, "hipMalloc(server keys)");
       ctx->srv_cap = cap;
     }
     memset(ctx->h_srv, 0, srv_bytes(ctx->srv_cap));
@@ -1808,14 +1591,17 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
   if (!win || !out_packed) return set_err(ctx, LDPC_EINVAL, "null buffer");
   const int N = ctx->N, KB = ctx->KB;
   for (int b = 0; b < B; ++b)
-    if (win[b] < 0 || (win[b] >> 1) + N > ctx->span_samples)
+    if (win[b] < 0 || (win[b] >> 1) + N > ctx->span_samples || win[b] >= ((int64_t)1 << 40))
       return set_err(ctx, LDPC_EINVAL, "window outside the staged span");
   int64_t *keys = (int64_t *)(ctx->h_srv + srv_keys_off());
   const uint64_t *res = (const uint64_t *)(ctx->h_srv + srv_res_off(ctx->srv_cap));
   const double timeout_s = 10.0;
   for (int b0 = 0; b0 < B; b0 += (int)ctx->srv_cap) {
     const int n = (int)std::min<int64_t>(ctx->srv_cap, B - b0);
-    memcpy(keys, win + b0, (size_t)n * 8);
+    // each key carries the epoch it is posted with (mod 2^24), so the poller
+    // can tell a slot it read before this round's write (ldpc_serve.hip)
+    const uint64_t ktag = (uint64_t)((ctx->srv_epoch + 1) & 0xFFFFFFu) << 40;
+    for (int b = 0; b < n; ++b) keys[b] = (int64_t)((uint64_t)win[b0 + b] | ktag);
     serve_post(ctx, (uint32_t)n);
     ctx->srv_rounds += 1;
     const uint32_t tag = ctx->srv_epoch & 0x7FFFFFu;
@@ -1830,17 +1616,34 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
           // the launch ended (its deadline passed between rounds): start another
           const hipError_t q = hipStreamQuery(ctx->stream);
           if (q == hipSuccess) {
+            if (getenv("LDPC_SERVE_DEBUG")) {
+              uint64_t c[8] = {0}, c0 = 0;
+              uint32_t census = 0;
+              (void)hipMemcpy(&c0, ctx->d_srv_ctl, 8, hipMemcpyDeviceToHost);
+              (void)hipMemcpy(&census, ctx->d_srv_ctl + 16 * ldpc::kServeCopies, 4, hipMemcpyDeviceToHost);
+              (void)hipMemcpy(c, ctx->d_srv_ctl + 16 * (ldpc::kServeCopies + 1), sizeof c,
+                              hipMemcpyDeviceToHost);
+              fprintf(stderr,
+                      "ldpc_serve: launch %d ended before round %u (B %d, result %d of them "
+                      "in): ctl %016llx census %u, poller exit %llu on round word %016llx, "
+                      "host round word %016llx; decoder round starts %llu (g0 saw %016llx), "
+                      "mw results %llu\n",
+                      ctx->srv_launches, ctx->srv_epoch, n, b, (unsigned long long)c0, census,
+                      (unsigned long long)c[0], (unsigned long long)c[1],
+                      (unsigned long long)*(const uint64_t *)ctx->h_srv, (unsigned long long)c[2],
+                      (unsigned long long)c[3], (unsigned long long)c[4]);
+            }
             if (++relaunches > 4) {
               ctx->serving = false;
               return set_err(ctx, LDPC_ETIMEOUT, "the window server keeps ending before its round");
             }
             ctx->srv_epoch -= 1;  // the launch serves epochs above start_epoch
             const int rc = serve_launch(ctx);
-            ctx->srv_epoch += 1;
             if (rc != LDPC_OK) {
               ctx->serving = false;
               return rc;
             }
+            serve_post(ctx, (uint32_t)n);  // the same round (epoch, tag), the new session's
           } else if (q != hipErrorNotReady) {
             ctx->serving = false;
             return hip_err(ctx, q, "window server");
@@ -1855,19 +1658,25 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
       for (int j = 0; j < KB; ++j) out_packed[(size_t)(b0 + b) * KB + j] = (uint8_t)(pk >> (8 * j));
       if (syn_weight_opt) syn_weight_opt[b0 + b] = (int32_t)((g >> 32) & 511u);
     }
+    if (getenv("LDPC_SERVE_DEBUG")) {  // device-side split of the round (100 MHz ticks)
+      const double host_us =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6;
+      uint64_t c[8] = {0};
+      uint64_t *dg = ctx->d_srv_ctl + 16 * (ldpc::kServeCopies + 1);
+      (void)hipMemcpy(c, dg, sizeof c, hipMemcpyDeviceToHost);
+      const uint64_t zero[2] = {0, 0};
+      (void)hipMemcpy(dg + 6, zero, sizeof zero, hipMemcpyHostToDevice);
+      ctx->dbg[0] += 1;
+      ctx->dbg[1] += host_us;
+      ctx->dbg[2] += 1e-2 * (double)c[6];
+      ctx->dbg[3] += 1e-2 * (double)c[7];
+    }
   }
   return LDPC_OK;
 }
 }  // namespace
 
 extern "C" {
-
-int ldpc_walk_span(ldpc_ctx *ctx, int method, int max_iters, int precision, const float *in,
-                   int64_t n_in_floats, int elem_stride, int reuse_span, int noutput_bytes,
-                   ldpc_walk_io *io, uint8_t *out, uint8_t *msgs, int msgs_cap) {
-  return walk_span_impl(ctx, method, max_iters, precision, in, n_in_floats, elem_stride,
-                        reuse_span, noutput_bytes, io, out, msgs, msgs_cap);
-}
 
 int ldpc_stage_span(ldpc_ctx *ctx, const float *in, int64_t n_in_floats, int elem_stride,
                     int max_windows) {
@@ -1899,8 +1708,16 @@ int ldpc_serve_windows(ldpc_ctx *ctx, const int64_t *windows, int B, uint8_t *ou
 
 int ldpc_serve_end(ldpc_ctx *ctx) {
   if (!ctx) return LDPC_EINVAL;
+  if (getenv("LDPC_SERVE_DEBUG") && ctx->dbg[0] > 0) {
+    fprintf(stderr,
+            "ldpc_serve: %.0f rounds: host %.1f us per round; from the poller's publication: "
+            "last key read %.1f us, last result stored %.1f us (mean over rounds)\n",
+            ctx->dbg[0], ctx->dbg[1] / ctx->dbg[0], ctx->dbg[2] / ctx->dbg[0],
+            ctx->dbg[3] / ctx->dbg[0]);
+    for (double &d : ctx->dbg) d = 0;
+  }
   if (ctx->serving) {  // the launch finishes on its own; the stream orders what follows
-    serve_post(ctx, ldpc::kServeQuit);
+    serve_post(ctx, ldpc::kServeB);
     ctx->serving = false;
   }
   return LDPC_OK;
@@ -1965,11 +1782,9 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
   // the set is complete (so the next candidate lands elsewhere), then freed.
   std::vector<hipStream_t> spare;
   int rc = LDPC_OK;
-  for (int tries = 0; (int)ctx->tp_streams.size() < n; ++tries) {
-    if (tries >= 8 * n) {
-      rc = set_err(ctx, LDPC_EDEVICE, "no set of concurrent streams of that size");
-      break;
-    }
+  // (more streams than the process has hardware queues cannot all be
+  // concurrent: after a few candidates the set's streams are handed out again)
+  for (int tries = 0; (int)ctx->tp_streams.size() < n && tries < 3 * n; ++tries) {
     hipStream_t c = nullptr;
     if ((e = hipStreamCreateWithFlags(&c, hipStreamNonBlocking)) != hipSuccess) {
       rc = hip_err(ctx, e, "hipStreamCreate");
@@ -1999,7 +1814,9 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
   }
   for (hipStream_t t : spare) (void)hipStreamDestroy(t);
   if (rc != LDPC_OK) return rc;
-  for (int i = 0; i < n; ++i) streams_out[i] = (void *)ctx->tp_streams[(size_t)i];
+  if (ctx->tp_streams.empty()) return set_err(ctx, LDPC_EDEVICE, "no stream");
+  const size_t m = ctx->tp_streams.size();
+  for (int i = 0; i < n; ++i) streams_out[i] = (void *)ctx->tp_streams[(size_t)i % m];
   return LDPC_OK;
 }
 

@@ -155,7 +155,9 @@ __device__ __forceinline__ void log_ratio_n_packed(const double (&T)[n],
                                                    const ex::ExTab *tab, double (&E)[n],
                                                    double *scratch, int lane) {
   double q[n];
-  const bool special = ex::ratio_n<n>(T, q);
+  // wave-uniform at once (a per-lane flag held across the loop below costs a
+  // VGPR and two conversions per call)
+  const bool any_special = __builtin_amdgcn_ballot_w64(ex::ratio_n<n>(T, q)) != 0;
   uint32_t pos[n];
   bool near[n];
   uint32_t base = 0;  // wave-uniform
@@ -183,7 +185,7 @@ __device__ __forceinline__ void log_ratio_n_packed(const double (&T)[n],
       if (near[i]) E[i] = scratch[pos[i]];
     asm volatile("" ::: "memory");
   }
-  if (__builtin_amdgcn_ballot_w64(special) != 0) {
+  if (any_special) {
     LDPC_EX_COLD();
     ex::ratio_fix_n<n>(T, E);
   }

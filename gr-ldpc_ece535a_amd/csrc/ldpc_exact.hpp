@@ -272,10 +272,15 @@ LDPC_HD void expm1_n(const double (&u)[n], const uint32_t (&hx)[n], double (&t)[
     ep[i] = (x[i] * (e - c[i]) - c[i]) - hxs[i];
     const double d = ep[i] - x[i];
     const int kk = k[i];
-    // per-lane constants: A, B from the table (tail_entry), 2^k exact
+    // per-lane constants: A, B from the table (tail_entry).  fma(A - d, 2^k,
+    // B) with its exact product is the exact scaling (ldexp, |k| <= 64 on
+    // moderate values) followed by the one rounded addition
     const TailEntry te = tab->tail[kk - kTailLo];
-    t[i] = fma_(te.a - d, from_hi((uint32_t)(kk + 0x3ff) << 20), te.b);
-    if (mid_possible) any_mid |= (uint32_t)(kk - 20) <= 36u;
+    t[i] = __builtin_ldexp(te.a - d, kk) + te.b;
+  }
+  if (mid_possible) {  // (a wave-uniform flag: the test stays in its branch)
+#pragma unroll
+    for (int i = 0; i < n; ++i) any_mid |= (uint32_t)(k[i] - 20) <= 36u;
   }
   if (mid_possible && LDPC_EX_ANY(any_mid)) {
     LDPC_EX_COLD();
@@ -391,12 +396,14 @@ LDPC_HD void tanh_half_n(const double (&m)[n], double (&z)[n], const ExTab *tab)
 LDPC_HD double log_main(double q, const GlLogEntry *tab) {
   const uint64_t ix = bits(q);
   const uint32_t th = (uint32_t)(ix >> 32) - 0x3fe60000u;  // high word of ix - OFF
-  const uint32_t i = (th >> (20 - kGlTabBits)) & ((1u << kGlTabBits) - 1);
   const int k = (int32_t)th >> 20;
-  // iz = ix - (tmp & 0xfff << 52): only the high word changes
-  const uint64_t iz = ((uint64_t)((uint32_t)(ix >> 32) - (th & 0xfff00000u)) << 32) | (uint32_t)ix;
-  const GlLogEntry e = tab[i];
-  const double z = dbl(iz);
+  // glibc's iz = ix - (tmp & 0xfff << 52) is q scaled by 2^-k, exactly (q and
+  // z = q 2^-k in [0x1.6p-1, 0x1.6p0) are normal): one ldexp
+  const double z = __builtin_ldexp(q, -k);
+  // entry i = bits 13..19 of th, as a byte offset (16-byte entries)
+  static_assert(sizeof(GlLogEntry) == 16, "16-byte log table entries");
+  const uint32_t off = (th >> (20 - kGlTabBits - 4)) & (((1u << kGlTabBits) - 1) << 4);
+  const GlLogEntry e = *reinterpret_cast<const GlLogEntry *>(reinterpret_cast<const char *>(tab) + off);
   const double r = fma_(z, e.invc, -1.0);
   const double kd = (double)k;
   const double w = fma_(kd, kGlLn2hi, e.logc);
@@ -443,6 +450,27 @@ LDPC_HD double log_q(double q, const GlLogEntry *tab) {
   return y;
 }
 
+// log_main with glibc's own bit arithmetic for the scaling (the ldexp above
+// needs a normal q; glibc's subnormal path hands in a pseudo-double whose
+// exponent field is below 1)
+inline double log_main_bits(uint64_t ix, const GlLogEntry *tab) {
+  const uint32_t th = (uint32_t)(ix >> 32) - 0x3fe60000u;
+  const uint32_t i = (th >> (20 - kGlTabBits)) & ((1u << kGlTabBits) - 1);
+  const int k = (int32_t)th >> 20;
+  const uint64_t iz = ((uint64_t)((uint32_t)(ix >> 32) - (th & 0xfff00000u)) << 32) | (uint32_t)ix;
+  const GlLogEntry e = tab[i];
+  const double z = dbl(iz);
+  const double r = fma_(z, e.invc, -1.0);
+  const double kd = (double)k;
+  const double w = fma_(kd, kGlLn2hi, e.logc);
+  const double hi = w + r;
+  const double lo = fma_(kd, kGlLn2lo, (w - hi) + r);
+  const double r2 = r * r;
+  const double r3 = r * r2;
+  const double p = fma_(fma_(r, kGlA[4], kGlA[3]), r2, fma_(r, kGlA[2], kGlA[1]));
+  return fma_(r3, p, fma_(r2, kGlA[0], lo)) + hi;
+}
+
 // glibc's log on every double (host reference for the tests)
 inline double log_glibc(double x, const GlLogEntry *tab) {
   uint64_t ix = bits(x);
@@ -453,6 +481,7 @@ inline double log_glibc(double x, const GlLogEntry *tab) {
     if (ix == bits(__builtin_inf())) return x;
     if ((top & 0x8000u) || (top & 0x7ff0u) == 0x7ff0u) return (x - x) / 0.0;  // NaN
     ix = bits(x * 0x1p52) - (52ull << 52);  // subnormal
+    return log_main_bits(ix, tab);
   }
   return log_main(dbl(ix), tab);
 }
@@ -501,10 +530,10 @@ LDPC_HD void ratio_fix_n(const double (&T)[n], double (&E)[n]) {
 template <int n>
 LDPC_HD void log_ratio_n(const double (&T)[n], const ExTab *tab, double (&E)[n]) {
   double q[n];
-  const bool special = ratio_n<n>(T, q);
+  const bool any_special = LDPC_EX_ANY(ratio_n<n>(T, q));
 #pragma unroll
   for (int i = 0; i < n; ++i) E[i] = log_q(q[i], tab->log);
-  if (LDPC_EX_ANY(special)) {
+  if (any_special) {
     LDPC_EX_COLD();
     ratio_fix_n<n>(T, E);
   }

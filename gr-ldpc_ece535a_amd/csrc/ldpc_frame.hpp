@@ -156,8 +156,12 @@ struct FrameResult {
   int weight;
   uint32_t byte;
 };
+// FAIR = false: a build that never manages issue priority (the throughput
+// build: fair_cycles is 0 there), so the clock reads and the state they need
+// are compiled out.
 template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax,
-          bool FIN = false, typename Real = typename Math<PREC>::Real, bool OUT = true>
+          bool FIN = false, typename Real = typename Math<PREC>::Real, bool OUT = true,
+          bool FAIR = true>
 __device__ __forceinline__ FrameResult decode_frame(const CodeView &code, const DecodeArgs &a,
                                              const int64_t b, WaveTables<S, NW> &wt,
                                              Real *tb, Real *eb, Real *rb, Real *sb,
@@ -253,7 +257,7 @@ __device__ __forceinline__ FrameResult decode_frame(const CodeView &code, const 
 #pragma unroll
       for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], t0);
     }
-    const uint32_t fair = a.fair_cycles;  // 0: no issue-priority management
+    const uint32_t fair = FAIR ? a.fair_cycles : 0u;  // 0: no issue-priority management
     uint64_t t_prev = fair ? __builtin_amdgcn_s_memtime() : 0;
     for (int h = 0; h < a.max_iters; ++h) {
       // read here, used once the row gathers below have been waited for (an

@@ -4,8 +4,8 @@
 // registers and LDS.  A DVB-S2-size code (E = 226799 edges) does not fit, so
 // this path keeps the messages in HBM and runs each iteration of the
 // reference's loop as separate grid-wide passes over the Tanner graph
-// (lib/ldpc_decoder_cb_impl.cc: min-sum :343-409, sum-product :500-553,
-// bit-flip :439-473):
+// (lib/ldpc_decoder_cb_impl.cc: sum-product :500-553, bit-flip :439-473;
+// min-sum has its own frame pipeline, ldpc_graph_msn.hip):
 //
 //   g_check   one wave = 8 check rows x 64 frames: reads each row's Q
 //             messages, writes its R messages (horizontal step), and -- from
@@ -25,9 +25,8 @@
 // transaction, and a check row's edges are adjacent blocks.  Inside a chunk that is still running every lane computes and
 // stores, stopped frames included (their messages are dead data), so no
 // store is a partial line; a stopped frame's hard decision and posterior are
-// frozen by masking instead.  Per frame-iteration the min-sum traffic is
-// 2E x sizeof(Real) read + 2E x sizeof(Real) written + 4N channel bytes: the
-// kernels are HBM-bound.  A stopped chunk costs one flag read per block.
+// frozen by masking instead.  Per frame-iteration the sum-product traffic is
+// 2E x sizeof(Real) read + 2E x sizeof(Real) written + 4N channel bytes.  A stopped chunk costs one flag read per block.
 //
 // The per-edge arithmetic is the reference's, in its order, with the same
 // Math<PREC> as the small-code kernel (ldpc_device.hpp).
@@ -157,13 +156,13 @@ __global__ void __launch_bounds__(256) g_load(GraphView g, GraphWork w_, const f
 // Horizontal step for kRowsPerWave rows x 64 frames per wave.  For h > 0 the
 // same pass evaluates checkFrame's rows (:236-253) on the hard decision of
 // iteration h-1: 64 frames per XOR of packed words.
-template <int PREC, int METHOD, int DC>
+template <int PREC, int DC>
 __global__ void __launch_bounds__(256) g_check(GraphView g, GraphWork w_, int h) {
   const GraphWork w = live(w_);
   typedef typename Math<PREC>::Real Real;
   const int k = blockIdx.y;
   __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
-  if constexpr (METHOD == 1 && Math<PREC>::kTabN > 0) {
+  if constexpr (Math<PREC>::kTabN > 0) {
     if (w.chunk_done[k]) return;  // uniform per block: no thread misses the barrier
     stage_tab<PREC>(logtab);
   }
@@ -193,42 +192,16 @@ __global__ void __launch_bounds__(256) g_check(GraphView g, GraphWork w_, int h)
     Real q[DC];
 #pragma unroll
     for (int t = 0; t < DC; ++t) q[t] = t < d ? Q[(int64_t)(e0 + t) * 64] : Real(0);
-    if constexpr (METHOD == 1) {
-      // E(j,i) = log((1+T)/(1-T)), T = prod_{k != i} tanh(M(j,k)/2) in
-      // ascending k (:503-516)
+    // E(j,i) = log((1+T)/(1-T)), T = prod_{k != i} tanh(M(j,k)/2) in
+    // ascending k (:503-516)
 #pragma unroll
-      for (int t = 0; t < DC; ++t)
-        if (t < d) q[t] = Math<PREC>::tanh_half(q[t], logtab);
-      for (int e = 0; e < d; ++e) {
-        Real T = Real(1);
+    for (int t = 0; t < DC; ++t)
+      if (t < d) q[t] = Math<PREC>::tanh_half(q[t], logtab);
+    for (int e = 0; e < d; ++e) {
+      Real T = Real(1);
 #pragma unroll
-        for (int t = 0; t < DC; ++t) T = (t != e && t < d) ? T * q[t] : T;
-        R[(int64_t)(e0 + e) * 64] = Math<PREC>::check_msg(T, logtab);
-      }
-    } else {
-      // L(r_ji) = (prod_k sign(L(q_jk))) * sign(L(q_ji)) * min_{k != i} |L(q_jk)|
-      // (:350-376).  The leave-one-out minimum is the smallest |L(q)| unless
-      // edge i holds it (first occurrence, strict <), then the second
-      // smallest; NaNs never pass the compare; DBL_MAX when no other edge.
-      int prod = 1;
-      Real m1 = Math<PREC>::max_(), m2 = Math<PREC>::max_();
-      int i1 = -1;
-#pragma unroll
-      for (int t = 0; t < DC; ++t)
-        if (t < d) {
-          prod *= sgn(q[t]);
-          const Real a = Math<PREC>::abs_(q[t]);
-          if (a < m1) {
-            m2 = m1;
-            m1 = a;
-            i1 = t;
-          } else if (a < m2) {
-            m2 = a;
-          }
-        }
-#pragma unroll
-      for (int t = 0; t < DC; ++t)
-        if (t < d) R[(int64_t)(e0 + t) * 64] = (Real)(prod * sgn(q[t])) * (t == i1 ? m2 : m1);
+      for (int t = 0; t < DC; ++t) T = (t != e && t < d) ? T * q[t] : T;
+      R[(int64_t)(e0 + e) * 64] = Math<PREC>::check_msg(T, logtab);
     }
   }
   if (h > 0 && lane == 0) w.synd_part[(int64_t)wg * chunks + k] = odd;
@@ -286,12 +259,10 @@ __global__ void __launch_bounds__(256) g_decide(GraphWork w, int h, int max_iter
   }
 }
 
-// Vertical step for kColsPerWave columns x 64 frames per wave.
-//   min-sum (:379-403): s = sum_j L(r_ji) (ascending j), L(Q) = Lci + s,
-//     vhat = L(Q) < 0, L(q_ij) = (Lci + s) - L(r_ji);
-//   sum-product: L = sum_j (E(j,i) + r) (:519-532), vhat = L <= 0, and
-//     M(j,i) = sum_{k != j} (E(k,i) + r) (:540-553), both ascending.
-template <typename Real, int METHOD, int DV>
+// Vertical step for kColsPerWave columns x 64 frames per wave (sum-product):
+// L = sum_j (E(j,i) + r) (:519-532), vhat = L <= 0, and
+// M(j,i) = sum_{k != j} (E(k,i) + r) (:540-553), both ascending.
+template <typename Real, int DV>
 __global__ void __launch_bounds__(256) g_var(GraphView g, GraphWork w_) {
   const GraphWork w = live(w_);
   const int k = blockIdx.y;
@@ -317,30 +288,18 @@ __global__ void __launch_bounds__(256) g_var(GraphView g, GraphWork w_) {
     }
     Real tot = Real(0);
     bool bit;
-    if constexpr (METHOD == 1) {
 #pragma unroll
-      for (int t = 0; t < DV; ++t)
-        if (t < d) tot = tot + (r[t] + rc);
-      bit = tot <= Real(0);
+    for (int t = 0; t < DV; ++t)
+      if (t < d) tot = tot + (r[t] + rc);
+    bit = tot <= Real(0);
 #pragma unroll
-      for (int s = 0; s < DV; ++s)
-        if (s < d) {
-          Real T = Real(0);
+    for (int s = 0; s < DV; ++s)
+      if (s < d) {
+        Real T = Real(0);
 #pragma unroll
-          for (int t = 0; t < DV; ++t) T = (t != s && t < d) ? T + (r[t] + rc) : T;
-          Q[(int64_t)e[s] * 64] = T;
-        }
-    } else {
-      Real s = Real(0);
-#pragma unroll
-      for (int t = 0; t < DV; ++t)
-        if (t < d) s = s + r[t];
-      tot = rc + s;
-      bit = tot < Real(0);
-#pragma unroll
-      for (int t = 0; t < DV; ++t)
-        if (t < d) Q[(int64_t)e[t] * 64] = tot - r[t];
-    }
+        for (int t = 0; t < DV; ++t) T = (t != s && t < d) ? T + (r[t] + rc) : T;
+        Q[(int64_t)e[s] * 64] = T;
+      }
     const uint64_t bw = __ballot(bit);
     if (lane == 0) {
       uint64_t *hw = &w.hard[(int64_t)c * chunks + k];
@@ -617,24 +576,24 @@ __global__ void __launch_bounds__(256) g_commit(GraphWork w, int used0) {
   }
 }
 
-template <int PREC, int METHOD>
+template <int PREC>
 void launch_check(const GraphView &g, const GraphWork &w, int h, dim3 grid, hipStream_t st) {
   if (g.dc_max <= 8)
-    g_check<PREC, METHOD, 8><<<grid, 256, 0, st>>>(g, w, h);
+    g_check<PREC, 8><<<grid, 256, 0, st>>>(g, w, h);
   else if (g.dc_max <= 16)
-    g_check<PREC, METHOD, 16><<<grid, 256, 0, st>>>(g, w, h);
+    g_check<PREC, 16><<<grid, 256, 0, st>>>(g, w, h);
   else
-    g_check<PREC, METHOD, 32><<<grid, 256, 0, st>>>(g, w, h);
+    g_check<PREC, 32><<<grid, 256, 0, st>>>(g, w, h);
 }
 
-template <typename Real, int METHOD>
+template <typename Real>
 void launch_var(const GraphView &g, const GraphWork &w, dim3 grid, hipStream_t st) {
   if (g.dv_max <= 4)
-    g_var<Real, METHOD, 4><<<grid, 256, 0, st>>>(g, w);
+    g_var<Real, 4><<<grid, 256, 0, st>>>(g, w);
   else if (g.dv_max <= 8)
-    g_var<Real, METHOD, 8><<<grid, 256, 0, st>>>(g, w);
+    g_var<Real, 8><<<grid, 256, 0, st>>>(g, w);
   else
-    g_var<Real, METHOD, 16><<<grid, 256, 0, st>>>(g, w);
+    g_var<Real, 16><<<grid, 256, 0, st>>>(g, w);
 }
 
 // LDPC_GRAPH_COMPACT=0 disables compaction (A/B and debugging knob).
@@ -662,16 +621,14 @@ void launch_compaction(const GraphView &g, const GraphWork &w, const DecodeArgs 
   g_commit<<<1, 256, 0, st>>>(w, used0);
 }
 
-template <int PREC, int METHOD>
-void run_soft(const GraphView &g, const GraphWork &w, const DecodeArgs &a, dim3 rgrid,
-              dim3 cgrid, hipStream_t st) {
+template <int PREC>
+void run_sp(const GraphView &g, const GraphWork &w, const DecodeArgs &a, dim3 rgrid,
+            dim3 cgrid, hipStream_t st) {
   typedef typename Math<PREC>::Real Real;
-  // min-sum has no transcendentals: both f64 modes run the same kernels
-  constexpr int CP = (METHOD == 0 && PREC == 2) ? 0 : PREC;
   for (int h = 0; h < a.max_iters; ++h) {
-    launch_check<CP, METHOD>(g, w, h, rgrid, st);
+    launch_check<PREC>(g, w, h, rgrid, st);
     if (h > 0) g_decide<<<w.chunks, 256, 0, st>>>(w, h, a.max_iters, a.et_period);
-    launch_var<Real, METHOD>(g, w, cgrid, st);
+    launch_var<Real>(g, w, cgrid, st);
     if (compaction_enabled() && w.chunks > 1 && h >= 3 && (h & 1) && h + 1 < a.max_iters)
       launch_compaction<Real>(g, w, a, a.max_iters, st);
   }
@@ -744,7 +701,8 @@ void graph_work_carve(GraphWork &w, void *base, const GraphView &g, int Bp, int 
 
 int launch_graph_decode(const GraphView &g, const GraphWork &w, const DecodeArgs &a, int method,
                         int prec, void *stream) {
-  if (g.dc_max > kGraphDcMax || g.dv_max > kGraphDvMax) return -2;
+  // min-sum runs on the narrow-chunk pipeline (ldpc_graph_msn.hip)
+  if (g.dc_max > kGraphDcMax || g.dv_max > kGraphDvMax || method == 0) return -2;
   if (a.B <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const int chunks = w.chunks;
@@ -764,20 +722,15 @@ int launch_graph_decode(const GraphView &g, const GraphWork &w, const DecodeArgs
     g_load<float, false><<<tgrid, 256, 0, st>>>(g, w, a.in, a.cw_stride, a.elem_stride,
                                                  a.polarity, a.B);
   }
-  if (method == 0) {
+  if (method == 1) {
     if (prec == 1)
-      run_soft<1, 0>(g, w, a, rgrid, cgrid, st);
-    else
-      run_soft<0, 0>(g, w, a, rgrid, cgrid, st);
-  } else if (method == 1) {
-    if (prec == 1)
-      run_soft<1, 1>(g, w, a, rgrid, cgrid, st);
+      run_sp<1>(g, w, a, rgrid, cgrid, st);
     else if (prec == 2)
-      run_soft<2, 1>(g, w, a, rgrid, cgrid, st);
+      run_sp<2>(g, w, a, rgrid, cgrid, st);
     else if (prec == 3)
-      run_soft<3, 1>(g, w, a, rgrid, cgrid, st);
+      run_sp<3>(g, w, a, rgrid, cgrid, st);
     else
-      run_soft<0, 1>(g, w, a, rgrid, cgrid, st);
+      run_sp<0>(g, w, a, rgrid, cgrid, st);
   } else if (method == 2) {
     for (int h = 0; h < a.max_iters; ++h) {
       g_check_bf<<<rgrid, 256, 0, st>>>(g, w, h);

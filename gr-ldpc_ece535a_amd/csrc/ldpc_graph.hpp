@@ -88,6 +88,9 @@ int launch_graph_decode(const GraphView &g, const GraphWork &w, const DecodeArgs
 #define LDPC_MSN_FRAMES 2
 #endif
 constexpr int kMsnFrames = LDPC_MSN_FRAMES;
+// rows the pipeline takes: the check pass's fused decision counts a chunk's
+// blocks of 256 rows in 12-bit fields (and rows fit the edge words' 24 bits)
+constexpr int kMsnMaxRows = 4095 * 256;
 
 // One wave's t-th edges (64 lanes): in the storage order every circulant of a
 // DVB-S2-style code is a shifted identity, so the 64 values are a few runs of
@@ -139,13 +142,11 @@ struct MsnTables {  // host copies of MsnView's arrays
 
 struct MsnWork {
   int S, chunks, nb_check, nb_var, check_waves, real_bytes, out_var;
-  int fuse;          // decision taken in the check pass (msn_check FUSE)
   float *L;          // chunks x N x F: Lci = -tx
   void *LQ;          // chunks x N x F Real: Lci + sum of the column's L(r)
   void *m1, *m2;     // chunks x M x F Real
   uint8_t *meta;     // chunks x M x F: (P + 1) << 6 | (i1 + 1)
   uint8_t *alpha;    // chunks x dc_max x M ([t][p]; 2 frames: nibbles, [t/2][p]): bit 2f L(q) < 0, bit 2f+1 sign 0
-  uint8_t *odd;      // chunks x check_waves: frames with an unsatisfied row
   int32_t *capsyn;   // S: syndrome weight of a frame stopping at the cap
   int32_t *it;       // S: iterations the slot's frame has executed
   int32_t *frame;    // S: the slot's frame (-1: empty); a refill's new frame after decide

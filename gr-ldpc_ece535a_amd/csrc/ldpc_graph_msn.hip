@@ -35,8 +35,7 @@
 //   the check pass of its last pass (atomic adds per wave, only at the cap).
 //
 // Per pass: msn_check (the chunk's stop / refill decision taken by the block
-// that completes the chunk; msn_decide as its own launch with
-// LDPC_MSN_FUSE=0) -> msn_var (outputs of the stopped frames, the vertical
+// that completes the chunk) -> msn_var (outputs of the stopped frames, the vertical
 // step, refills); separate msn_post / msn_cols launches for the outputs only
 // for codes outside that fast path.
 #include <hip/hip_runtime.h>
@@ -315,7 +314,7 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
 
 // One row per lane, the chunk's F frames in the lane.  Frames whose slot is
 // not live compute on stale values nobody reads.
-// mbuf: this pass's mask buffer (the decision writes the other).  FUSE: the
+// mbuf: this pass's mask buffer (the decision writes the other).  The
 // chunk's decision is taken in this launch by the block whose arrival
 // completes the chunk: 64-bit atomic adds carry the arrival (bits 0-11) and,
 // per frame f, "a row of these blocks is unsatisfied" (bits 12(f+1)..), in
@@ -328,7 +327,7 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
 #ifndef LDPC_MSN_VAR_MINB
 #define LDPC_MSN_VAR_MINB 1
 #endif
-template <int PREC, int DC, bool FUSE>
+template <int PREC, int DC>
 __global__ void __launch_bounds__(256, LDPC_MSN_CHECK_MINB) msn_check(MsnView g, MsnWork w, int mbuf, int max_iters,
                                                  int et_period, int B, int32_t *synd) {
   typedef typename Math<PREC>::Real Real;
@@ -361,7 +360,7 @@ __global__ void __launch_bounds__(256, LDPC_MSN_CHECK_MINB) msn_check(MsnView g,
     for (int t = 0; t < DC; ++t) ab[t] = t < g.dc_max ? alpha[(int64_t)t * g.M] : 0u;
   }
   if (!live) {
-    if (FUSE && bi == 0 && threadIdx.x < 64)
+    if (bi == 0 && threadIdx.x < 64)
       decide_slots(w, k, 0u, mbuf ^ 1, max_iters, et_period, B, synd);
     return;
   }
@@ -396,9 +395,7 @@ __global__ void __launch_bounds__(256, LDPC_MSN_CHECK_MINB) msn_check(MsnView g,
       asm volatile("" ::"v"(r) : "memory");
     }
   }
-  if constexpr (!FUSE) {
-    if (lane == 0) w.odd[(int64_t)k * w.check_waves + bi * 4 + (threadIdx.x >> 6)] = (uint8_t)odd;
-  } else {
+  {
     __shared__ uint32_t s_odd[4];
     __shared__ int s_last;
     __shared__ uint32_t s_tot;
@@ -487,23 +484,6 @@ __device__ __forceinline__ void decide_slots(const MsnWork &w, int k, uint32_t o
     w.live[m] = rw | fw;
     if (sw) atomicAdd(&w.ctrl[1], __popc(sw));
   }
-}
-
-// The decision launch: one block per chunk ORs the chunk's check-wave
-// parities.
-__global__ void __launch_bounds__(256) msn_decide(MsnWork w, int par, int max_iters, int et_period,
-                                                  int B, int32_t *synd) {
-  const int k = blockIdx.x;
-  __shared__ uint32_t part[4];
-  uint32_t odd = 0;
-  if (w.live[par * w.chunks + k])
-    for (int i = threadIdx.x; i < w.check_waves; i += 256) odd |= w.odd[(int64_t)k * w.check_waves + i];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) odd |= (uint32_t)__shfl_xor((int)odd, o);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = odd;
-  __syncthreads();
-  if (threadIdx.x >= 64) return;
-  decide_slots(w, k, part[0] | part[1] | part[2] | part[3], par ^ 1, max_iters, et_period, B, synd);
 }
 
 // Packed info bits (columns M.., MSB first, :207-219) and iterations of the
@@ -720,13 +700,13 @@ __global__ void msn_init(MsnWork w) {
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Pass p reads mask buffer p & 1 and decides into the other.
-template <int PREC, bool FUSE>
-void msn_pass_f(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int par, hipStream_t st) {
+template <int PREC>
+void msn_pass(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int par, hipStream_t st) {
   typedef typename Math<PREC>::Real Real;
   const int rblocks = w.nb_check * w.chunks, cblocks = w.nb_var * w.chunks, nb = par ^ 1;
   static_assert(kMsnFrames == kF, "");
 #define LDPC_MSN_CHECK(DC) \
-  msn_check<PREC, DC, FUSE><<<rblocks, 256, 0, st>>>(g, w, par, a.max_iters, a.et_period, a.B, a.synd)
+  msn_check<PREC, DC><<<rblocks, 256, 0, st>>>(g, w, par, a.max_iters, a.et_period, a.B, a.synd)
   if (g.dc_max <= 8)
     LDPC_MSN_CHECK(8);
   else if (g.dc_max <= 16)
@@ -734,7 +714,6 @@ void msn_pass_f(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int par
   else
     LDPC_MSN_CHECK(32);
 #undef LDPC_MSN_CHECK
-  if (!FUSE) msn_decide<<<w.chunks, 256, 0, st>>>(w, par, a.max_iters, a.et_period, a.B, a.synd);
   if (!w.out_var) {
     const int pb = std::min(16, (g.KB + 255) / 256);
     msn_post<<<dim3(pb, w.chunks), 256, 0, st>>>(g, w, a, nb);
@@ -748,14 +727,6 @@ void msn_pass_f(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int par
     msn_var<Real, 8><<<cblocks, 256, 0, st>>>(g, w, a, nb);
   else
     msn_var<Real, 16><<<cblocks, 256, 0, st>>>(g, w, a, nb);
-}
-
-template <int PREC>
-void msn_pass(const MsnView &g, const MsnWork &w, const DecodeArgs &a, int par, hipStream_t st) {
-  if (w.fuse)
-    msn_pass_f<PREC, true>(g, w, a, par, st);
-  else
-    msn_pass_f<PREC, false>(g, w, a, par, st);
 }
 
 }  // namespace
@@ -772,11 +743,9 @@ int msn_default_chunks() {
 
 size_t msn_work_bytes(const MsnView &g, int chunks, int prec) {
   const size_t real = prec == 1 ? 4 : 8, F = kF, C = chunks;
-  const size_t nbc = (size_t)((g.M + kIB - 1) / kIB);
   size_t n = al256(C * g.N * F * 4) + al256(C * g.N * F * real);  // L, LQ
   n += 2 * al256(C * g.M * F * real) + al256(C * g.M * F);        // m1, m2, meta
   n += al256(C * alpha_rows(g.dc_max) * g.M);                     // alpha
-  n += al256(C * nbc * 4);                                        // odd
   n += 5 * al256(C * F * 4);                                      // capsyn, it, frame, out_frame, used
   n += 4 * al256(2 * C * 4) + al256(C * 9 * 8) + al256(64);      // masks x 2, arrive, ctrl
   return n;
@@ -804,7 +773,6 @@ void msn_work_carve(MsnWork &w, void *base, const MsnView &g, int chunks, int pr
   w.m2 = take(C * g.M * F * real);
   w.meta = (uint8_t *)take(C * g.M * F);
   w.alpha = (uint8_t *)take(C * alpha_rows(g.dc_max) * g.M);
-  w.odd = (uint8_t *)take(C * (size_t)w.check_waves);
   w.capsyn = (int32_t *)take(C * F * 4);
   w.it = (int32_t *)take(C * F * 4);
   w.frame = (int32_t *)take(C * F * 4);
@@ -816,12 +784,12 @@ void msn_work_carve(MsnWork &w, void *base, const MsnView &g, int chunks, int pr
   w.fill = (uint32_t *)take(2 * C * 4);
   w.arrive = (uint64_t *)take(C * 9 * 8);
   // The decision in the check pass's last block per chunk (12-bit arrival
-  // counts) unless LDPC_MSN_FUSE=0.  One word per chunk made the 127 blocks of
-  // a chunk contend (check pass 53.5 us against 40.8 + 4.9 for the check and
+  // counts: M <= kMsnMaxRows).  One word per chunk made the 127 blocks of a
+  // chunk contend (check pass 53.5 us against 40.8 + 4.9 for the check and
   // decision launches, profiles/round3/msn/fused_decide.txt); two levels (8
-  // group words, then the chunk's) measure 2 219-2 229 against 2 207-2 212
-  // Mbit/s for the separate launch (profiles/round3/msn/ab_fuse2.txt)
-  w.fuse = w.nb_check <= 4095 && !(getenv("LDPC_MSN_FUSE") && getenv("LDPC_MSN_FUSE")[0] == '0');
+  // group words, then the chunk's) measured 2 219-2 229 against 2 207-2 212
+  // Mbit/s for a separate decision launch (profiles/round3/msn/ab_fuse2.txt),
+  // which was then removed
   w.ctrl = (int32_t *)take(64);
 }
 
@@ -1068,9 +1036,6 @@ void msn_build(int M, int N, const std::vector<int32_t> &rp0, const std::vector<
   msn_tables(M, N, rp0, ci0, rpos, cpos, qc);
   qc.order = 1;
   const long s_id = contiguity(t), s_qc = contiguity(qc);
-  if (getenv("LDPC_MSN_DEBUG"))
-    fprintf(stderr, "msn order: contiguity identity %ld, residue classes %ld (E = %d)\n", s_id, s_qc,
-            rp0[M]);
   qc.score[0] = s_id;
   qc.score[1] = s_qc;
   t.score[1] = s_qc;

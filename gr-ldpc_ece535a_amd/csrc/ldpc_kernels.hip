@@ -44,6 +44,9 @@ __device__ uint64_t g_timeline[4 * kTimelineFrames];
 // default, 1, gives the same register budget)
 #define LDPC_SMALL_MIN_BLOCKS (kWavesPerBlock >= 4 ? 1 : 12 / kWavesPerBlock)
 #endif
+#ifndef LDPC_TP_MINB
+#define LDPC_TP_MINB 4  // throughput build: waves per SIMD the register budget allows
+#endif
 // MINB = 4 (four waves per SIMD, <= 128 VGPRs): the throughput build of the
 // sum-product f64 kernel (several launches in flight share the CUs); one
 // launch at a time runs faster with the larger register budget
@@ -164,12 +167,14 @@ __global__ void __launch_bounds__(kThreads, MINB)
       bool bad = false;
 #pragma unroll
       for (int q = 0; q < NW; ++q) bad |= !__builtin_isfinite(xin[q]);
+      // the throughput build runs with fair_cycles 0 (launch_slots)
+      constexpr bool kFair = MINB != LDPC_TP_MINB;
       if (__ballot(bad) == 0)
-        decode_frame<PREC, METHOD, S, NW, DCN, DVN, true>(code, a, b, wt, tb, eb, rb, sb, lane,
-                                                           logtab, xin, colq, ppos);
+        decode_frame<PREC, METHOD, S, NW, DCN, DVN, true, Real, true, kFair>(
+            code, a, b, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
       else
-        decode_frame<PREC, METHOD, S, NW, DCN, DVN, false>(code, a, b, wt, tb, eb, rb, sb, lane,
-                                                            logtab, xin, colq, ppos);
+        decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, true, kFair>(
+            code, a, b, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
     } else {
       decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane, logtab,
                                                   xin, colq, ppos);
@@ -324,9 +329,6 @@ static int launch_mw_slots(const CodeView &code, const DecodeArgs &a, int slots,
   }
 }
 
-#ifndef LDPC_TP_MINB
-#define LDPC_TP_MINB 4  // throughput build: waves per SIMD the register budget allows
-#endif
 template <int PREC, int METHOD, int NW>
 static int launch_slots(const CodeView &code, const DecodeArgs &a, int slots, hipStream_t st) {
   // low-degree codes (dc <= 6, dv <= 3: the reference's H) with one column

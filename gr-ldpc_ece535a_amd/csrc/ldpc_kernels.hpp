@@ -110,82 +110,28 @@ struct DecodeArgs {
 };
 
 // ---------------------------------------------------------------------------
-// The block walker (ldpc_walk.hip): one persistent launch runs the
-// reference's frame loop (lib/ldpc_decoder_cb_impl.cc:146-226) over a whole
-// staged span.  Wave 0 of workgroup 0 walks the loop; every other wave decodes
-// the windows it asks for (a window = the N samples at a position, at one
-// polarity), pulled from a request queue.  Hand-offs are 8-byte granules
-// {tag, value} written by one agent-scope (sc1) store and polled with sc1
-// loads (MI355X_MICROARCH.md, inter-workgroup visibility, R2).
-// ---------------------------------------------------------------------------
-constexpr int kWalkDone = 256;  // ctl word set when the walker has finished
-constexpr int kWalkCtlWords = 272;
-constexpr int64_t kWalkClaimSlack = 16384;  // request slots past the walker's last one
-constexpr int kWalkLdsBytes = 96 << 10;     // the walker's bitmap of windows asked for
-constexpr int64_t kWalkMaxSpan = (int64_t)kWalkLdsBytes * 4;  // samples per walk (2 bits each)  // zeroed per launch: 8 queue heads (one per 128 B) + done
-enum { kWalkMsgLost = 1, kWalkMsgInverted = 2, kWalkMsgSync = 3 };
-
-struct WalkSummary {
-  int64_t consumed;     // samples the loop consumed
-  int64_t last_pass;    // position of the last window that passed in sync (relative)
-  int64_t anchor_pos;   // a position on the newest grid (two in-sync passes N apart), -1: none
-  int32_t produced;     // frames output
-  int32_t state, errors;
-  int32_t status;       // 0 ok; 1 a wait passed the deadline
-  int32_t n_msgs;
-  int32_t grid_frames, grid_fails;  // in-sync frames seen, and those that failed
-  int32_t requests, surprises, waits;
-  int32_t steps, restarts;  // walker loop turns, speculation restarts
-  int32_t diag[6];          // see Walk (ldpc_walk.hip)
-  int32_t pad;
-  int64_t wait_ticks, total_ticks;  // 100 MHz ticks spent waiting / in the walker
-};
-
-struct alignas(16) WalkArgs {
-  uint64_t *res;        // [2][cap] result granules: hi = (epoch << 9) | syndrome weight, lo = packed bytes
-  uint64_t *req;        // request granules: hi = epoch, lo = (position << 1) | polarity
-  uint32_t *ctl;        // kWalkCtlWords, zeroed per launch
-  uint8_t *out;         // output bytes (mo per frame)
-  uint8_t *msgs;        // message codes, in order
-  WalkSummary *sum;
-  int64_t cap;          // positions per polarity in res
-  int64_t req_cap;      // request slots
-  int64_t nin;          // samples in the span
-  int N, M, KB, mo, thr;
-  int nout;             // frames that fit the output
-  int msgs_cap;
-  int state, errors;
-  int64_t last_pass;
-  int64_t anchor;       // a position on the stream's grid, -1: none known
-  uint32_t epoch;       // 1 .. 2^23 - 1
-  int lead;             // frames the speculation may run ahead of the loop
-  uint64_t *trace;      // diagnostics (LDPC_WALK_TRACE=2): event records, null = off
-  int trace_cap;        // records (4 words each)
-  uint64_t deadline;    // ticks one wait may take before the walk gives up
-};
-
-// Launch the walker (host side, ldpc_walk.hip); `blocks` workgroups of
-// kThreads (0: as many as are resident at once).  a.in is the span (elem
-// stride 1); a.max_iters / a.et_period as for launch_decode.
-int launch_walk(const CodeView &code, const DecodeArgs &a, const WalkArgs &w, int method,
-                int prec, int slots, int nw, int blocks, void *stream);
-
-// ---------------------------------------------------------------------------
 // The block's window server (ldpc_serve.hip): one persistent launch per
 // general_work call serves rounds of windows of the staged span.  The host
 // writes a round's keys, then the round word (epoch << 32) | B; results come
 // back as 8-byte granules {(epoch mod 2^23) << 9 | syndrome weight, packed
 // bytes}.  Epochs only grow; a launch serves epochs above start_epoch.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kServeQuit = 0xFFFFFFFFu;  // B of the round that ends the launch
+// Round word: epoch (bits 32..63), the launch's session (20..31, mod 2^12),
+// B (0..19; kServeB: the round that ends the launch).
+constexpr uint32_t kServeB = 0xFFFFFu;
+constexpr int kServeCopies = 32;  // lines of ctl the poller writes the round to
+constexpr size_t kServeCtlBytes = 128 * (kServeCopies + 2);  // + census line, diagnostics line
 struct alignas(16) ServeArgs {
   const uint64_t *round;  // host-mapped round word
-  const int64_t *keys;    // host-mapped window keys, (position << 1) | polarity
+  const int64_t *keys;    // host-mapped window keys (epoch mod 2^24 << 40) | (position << 1) | polarity
+  int64_t *dkeys;         // device: the round's keys, copied by the poller
   uint64_t *res;          // host-mapped result granules
-  uint64_t *ctl;          // device: the round as the poller published it (zeroed per launch)
+  uint64_t *ctl;          // device, kServeCtlBytes: round copies, census, diagnostics (zeroed per launch)
   uint64_t deadline;      // 100 MHz ticks without a new round before the launch ends
   uint32_t start_epoch;   // the last epoch posted before this launch
+  uint32_t session;       // this launch's session id (the host's count of launches)
   int blocks_per_cu;      // decoder workgroups per CU (capped by occupancy; 0: occupancy)
+  int debug;              // LDPC_SERVE_DEBUG: counters in ctl words 24..28
 };
 // *workgroups_out: the launch's decoder workgroups
 int launch_serve(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, int method,

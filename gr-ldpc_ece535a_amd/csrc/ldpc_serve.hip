@@ -21,9 +21,11 @@
 //     decode of the same samples) and publishes each result as one 8-byte
 //     granule {(epoch << 9) | syndrome weight, packed bytes} in host-mapped
 //     memory, which the host polls;
-//   * B = kServeQuit ends the launch; so does a deadline (no round for
-//     `deadline` ticks of the 100 MHz clock), after which the host relaunches
-//     the server if it still wants a round.
+//   * B = kServeB ends the launch, and so does a round of a later launch's
+//     session (the host overwrote the quit round before the poller saw it);
+//     so does a deadline (no round for `deadline` ticks of the 100 MHz
+//     clock), after which the host relaunches the server if it still wants a
+//     round.
 // Visibility: the device reads host memory with system-scope loads (the
 // round word, then the keys, which the host wrote before it), writes results
 // with one system-scope 8-byte store per window, and hands the round word to
@@ -35,7 +37,6 @@ namespace ldpc {
 namespace {
 
 typedef __attribute__((address_space(1))) uint64_t gu64;
-typedef __attribute__((address_space(1))) int64_t gi64;
 
 __device__ __forceinline__ uint64_t ticks() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ uint64_t agent_load(const uint64_t *p) {
@@ -47,9 +48,6 @@ __device__ __forceinline__ void agent_store(uint64_t *p, uint64_t v) {
 __device__ __forceinline__ uint64_t sys_load(const uint64_t *p) {
   return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ int64_t sys_load_i64(const int64_t *p) {
-  return __hip_atomic_load((const gi64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 __device__ __forceinline__ void sys_store(uint64_t *p, uint64_t v) {
   __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -59,51 +57,137 @@ __device__ __forceinline__ void sys_store(uint64_t *p, uint64_t v) {
 // census (one atomic add, once per launch) when it starts; the windows of a
 // round go to the decoders counted when the round was published -- running,
 // so no window waits on a workgroup that is not resident.  Host epochs stay
-// below 2^23 (ldpc_serve_begin restarts them).
+// below 2^23 (ldpc_serve_begin restarts them).  The poller writes the round
+// to kCopies lines of ctl, and decoder g polls copy g % kCopies: a thousand
+// decoders polling one line queue behind each other for microseconds.
 constexpr uint64_t kQuitRound = ~0ull;  // epoch all ones: every decoder leaves
 __device__ __forceinline__ uint64_t ctl_word(uint32_t ep, uint32_t live, uint32_t B) {
   return ((uint64_t)ep << 40) | ((uint64_t)(live & 0xFFFFFu) << 20) | (B & 0xFFFFFu);
 }
+__device__ __forceinline__ uint64_t *ctl_copy(uint64_t *ctl, int i) { return ctl + 16 * i; }
+__device__ __forceinline__ uint32_t *census_word(uint64_t *ctl) {
+  return reinterpret_cast<uint32_t *>(ctl + 16 * kServeCopies);
+}
+__device__ __forceinline__ uint64_t *diag(uint64_t *ctl, int j) { return ctl + 16 * (kServeCopies + 1) + j; }
+enum { kDiagExit, kDiagExitRound, kDiagStarts, kDiagG0, kDiagResults, kDiagPub, kDiagKey, kDiagDone };
 __device__ __forceinline__ uint32_t census_load(uint64_t *ctl) {
-  return __hip_atomic_load((const __attribute__((address_space(1))) uint32_t *)(ctl + 16),
+  return __hip_atomic_load((const __attribute__((address_space(1))) uint32_t *)census_word(ctl),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t census_take(uint64_t *ctl) {
-  return __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t *)(ctl + 16), 1u,
+  return __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t *)census_word(ctl), 1u,
                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void dbg_max(uint64_t *p, uint64_t v) {
+  __hip_atomic_fetch_max((__attribute__((address_space(1))) uint64_t *)p, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void dbg_add(uint64_t *p) {
+  __hip_atomic_fetch_add((__attribute__((address_space(1))) uint64_t *)p, (uint64_t)1,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+__device__ __forceinline__ uint64_t wave_uniform(uint64_t v) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+}
 
-// Workgroup 0: the poller (one lane).  Others: decoders.  A round of at most
-// as many windows as there are decoder workgroups is decoded one window per
-// workgroup (mw_frame: S waves, one edge per lane, the lowest latency); a
-// bigger round one window per wave (decode_frame, the batch kernels' one-wave
-// form: fewer issue slots per window), windows w, w + W, ... for wave w of W.
-// The two forms share the workgroup's LDS (never at the same time).
+// The poller (wave 0 of workgroup 0): lane 0 reads the round word, lanes
+// 1..63 the first 63 key slots in the same instruction (host memory, one PCIe
+// round trip); a new round's keys -- each tagged with its epoch by the host,
+// so a slot read before the host rewrote it is read again -- go to device
+// memory (dkeys, agent-scope stores), then, behind the wave's vmcnt(0), the
+// round word to the ctl copies.
+__device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
+  uint32_t last = s.start_epoch;
+  const uint64_t t_start = ticks();
+  uint64_t t_last = t_start;
+  const uint64_t kKeyMask = (1ull << 40) - 1;
+  for (;;) {
+    const uint64_t v = sys_load(lane == 0 ? s.round : (const uint64_t *)s.keys + (lane - 1));
+    const uint64_t r = lane_bcast(v, 0);
+    const uint32_t ep = (uint32_t)(r >> 32);
+    if (ep != last) {
+      // a round of a later launch (this launch's quit round was overwritten
+      // before it was seen) ends this launch too
+      const bool quit = ((uint32_t)r & kServeB) == kServeB ||
+                        (((uint32_t)r >> 20) & 0xFFFu) != (s.session & 0xFFFu);
+      const int64_t B = quit ? 0 : (int64_t)((uint32_t)r & kServeB);
+      const uint64_t tag = (uint64_t)(ep & 0xFFFFFFu);
+      const uint64_t t_keys = ticks();
+      bool lost = false;  // a key slot that never showed this epoch (the host is gone)
+      for (int64_t c = -1; c < B && !lost; c += 64) {  // key slot c + lane (chunk -1: this read)
+        const int64_t b = c + lane;
+        const bool in = b >= 0 && b < B;
+        uint64_t k = c < 0 ? v : (in ? sys_load((const uint64_t *)s.keys + b) : 0);
+        while (__ballot(in && (k >> 40) != tag)) {
+          if (in && (k >> 40) != tag) k = sys_load((const uint64_t *)s.keys + b);
+          if (ticks() - t_keys > s.deadline) {
+            lost = true;
+            break;
+          }
+        }
+        if (in) agent_store((uint64_t *)s.dkeys + b, k & kKeyMask);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lost) {
+        if (lane < kServeCopies) agent_store(ctl_copy(s.ctl, lane), kQuitRound);
+        if (lane == 0) agent_store(diag(s.ctl, kDiagExit), 3);
+        return;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the decoders that have started by now share the round: all of them
+      // (every workgroup is resident) or, if some never start while this
+      // launch runs, those counted 20 us after the launch began -- at least
+      // one
+      uint32_t live = census_load(s.ctl);
+      while (!quit && live < gridDim.x - 1 && (live == 0 || ticks() - t_start < 2000)) {
+        __builtin_amdgcn_s_sleep(2);
+        live = census_load(s.ctl);
+        if (ticks() - t_start > s.deadline) break;  // (no decoder at all: give up below)
+      }
+      live = (uint32_t)__builtin_amdgcn_readfirstlane((int)live);
+      const uint64_t w = quit ? kQuitRound : ctl_word(ep, live, (uint32_t)B);
+      if (lane < kServeCopies) agent_store(ctl_copy(s.ctl, lane), w);
+      if (s.debug && lane == 0) agent_store(diag(s.ctl, kDiagPub), ticks());
+      last = ep;
+      t_last = ticks();
+      if (quit) {  // diagnostics: why, and the round word seen
+        if (lane == 0) {
+          agent_store(diag(s.ctl, kDiagExit), 1);
+          agent_store(diag(s.ctl, kDiagExitRound), r);
+        }
+        return;
+      }
+    } else if (ticks() - t_last > s.deadline) {
+      if (lane < kServeCopies) agent_store(ctl_copy(s.ctl, lane), kQuitRound);
+      if (lane == 0) {
+        agent_store(diag(s.ctl, kDiagExit), 2);
+        agent_store(diag(s.ctl, kDiagExitRound), r);
+      }
+      return;
+    }
+  }
+}
+
+// Workgroup 0: the poller (wave 0).  Others: decoders.  A round of at most as
+// many windows as there are decoders is decoded one window per workgroup
+// (mw_frame: S waves, one edge per lane, the lowest latency); a bigger round
+// one window per wave (decode_frame, the batch kernels' one-wave form: fewer
+// issue slots per window), windows w, w + W, ... for wave w of W.  The two
+// forms share the workgroup's LDS (never at the same time).
 template <int PREC, int METHOD, int S, int NW, int DCN, int DVN>
 __global__ void __launch_bounds__(64 * S, 3) serve_kernel(CodeView code, DecodeArgs a, ServeArgs s) {
   typedef typename Math<PREC>::Real Real;
   extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ int64_t sslot[2];  // the round, the window key (mw form)
+  __shared__ int64_t sslot[2];  // the round, the window key (workgroup form)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (blockIdx.x == 0) {
-    if (tid != 0) return;
-    uint32_t last = s.start_epoch;
-    uint64_t t_last = ticks();
-    for (;;) {
-      const uint64_t r = sys_load(s.round);
-      const uint32_t ep = (uint32_t)(r >> 32);
-      if (ep != last) {
-        // the decoders that have started by now share the round
-        const uint32_t live = census_load(s.ctl);
-        agent_store(s.ctl, (uint32_t)r == kServeQuit ? kQuitRound : ctl_word(ep, live, (uint32_t)r));
-        last = ep;
-        t_last = ticks();
-        if ((uint32_t)r == kServeQuit) return;
-      } else if (ticks() - t_last > s.deadline) {
-        agent_store(s.ctl, kQuitRound);
-        return;
-      }
-    }
+    if (wave == 0) poll_rounds(s, lane);
+    return;
   }
   __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
   if constexpr (METHOD == 1) stage_tab<PREC>(logtab);
@@ -125,6 +209,7 @@ __global__ void __launch_bounds__(64 * S, 3) serve_kernel(CodeView code, DecodeA
   if (tid == 0) sslot[1] = (int64_t)census_take(s.ctl);
   __syncthreads();
   const int64_t g = sslot[1];  // this decoder's place among those that started
+  const uint64_t *poll = ctl_copy(s.ctl, (int)(g % kServeCopies));
   // epochs only grow (ctl is zeroed before the launch, below start_epoch)
   uint32_t last = s.start_epoch;
   uint64_t idle = ticks();
@@ -132,7 +217,7 @@ __global__ void __launch_bounds__(64 * S, 3) serve_kernel(CodeView code, DecodeA
     if (tid == 0) {  // the next round
       uint64_t r;
       for (int spins = 0;; ++spins) {
-        r = agent_load(s.ctl);
+        r = agent_load(poll);
         if ((uint32_t)(r >> 40) > last) break;
         if ((spins & 15) == 15 && ticks() - idle > s.deadline) {
           r = kQuitRound;
@@ -148,12 +233,17 @@ __global__ void __launch_bounds__(64 * S, 3) serve_kernel(CodeView code, DecodeA
     const uint32_t ep = (uint32_t)(r >> 40), B = (uint32_t)r & 0xFFFFFu;
     const int64_t G = (int64_t)((r >> 20) & 0xFFFFFu);
     const uint64_t tag = (uint64_t)((ep & 0x7FFFFFu) << 9) << 32;
+    if (s.debug && tid == 0) {  // diagnostics: rounds seen by decoders
+      dbg_add(diag(s.ctl, kDiagStarts));
+      if (g == 0) agent_store(diag(s.ctl, kDiagG0), r);
+    }
     if ((int64_t)B <= G) {
       // one window per workgroup
       if (g < (int64_t)B) {
         if (tid == 0) {
-          sslot[1] = sys_load_i64(s.keys + g);
+          sslot[1] = (int64_t)agent_load((const uint64_t *)s.dkeys + g);
           mtb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();  // (the LDS is shared)
+          if (s.debug) dbg_max(diag(s.ctl, kDiagKey), ticks() - agent_load(diag(s.ctl, kDiagPub)));
         }
         __syncthreads();  // (mw_frame's first barrier orders the key's readers)
         const int64_t key = sslot[1];
@@ -171,7 +261,13 @@ __global__ void __launch_bounds__(64 * S, 3) serve_kernel(CodeView code, DecodeA
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             pk |= ((uint32_t)__builtin_amdgcn_readlane((int)o, j) & 255u) << (8 * j);
-          if (lane == 0) sys_store(s.res + g, tag | ((uint64_t)(uint32_t)weight << 32) | pk);
+          if (lane == 0) {
+            sys_store(s.res + g, tag | ((uint64_t)(uint32_t)weight << 32) | pk);
+            if (s.debug) {
+              dbg_add(diag(s.ctl, kDiagResults));
+              dbg_max(diag(s.ctl, kDiagDone), ticks() - agent_load(diag(s.ctl, kDiagPub)));
+            }
+          }
         }
         wave_lds_sync();
       }
@@ -179,9 +275,7 @@ __global__ void __launch_bounds__(64 * S, 3) serve_kernel(CodeView code, DecodeA
       // one window per wave
       const int64_t W = G * S;
       for (int64_t b = g * S + wave; b < (int64_t)B && g < G; b += W) {
-        const uint64_t kv = (uint64_t)sys_load_i64(s.keys + b);  // (one request for the wave)
-        const int64_t key = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(kv >> 32)) << 32) |
-                                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)kv));
+        const int64_t key = (int64_t)wave_uniform(agent_load((const uint64_t *)s.dkeys + b));
         const float *src = a.in + (key >> 1);
         const float sgn = (key & 1) ? -1.0f : 1.0f;
         float xin[NW];
@@ -193,13 +287,13 @@ __global__ void __launch_bounds__(64 * S, 3) serve_kernel(CodeView code, DecodeA
 #pragma unroll
           for (int q = 0; q < NW; ++q) bad |= !__builtin_isfinite(xin[q]);
           if (__ballot(bad) == 0)
-            fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, true, Real, false>(
+            fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, true, Real, false, false>(
                 code, a, 0, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
           else
-            fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, false>(
+            fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, false, false>(
                 code, a, 0, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
         } else {
-          fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, false>(
+          fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, false, false>(
               code, a, 0, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
         }
         uint32_t pk = 0;

@@ -23,19 +23,7 @@ PATH_SMALL, PATH_GRAPH = 0, 1
 MODE_LATENCY, MODE_THROUGHPUT = 0, 1
 ERRORS = {0: "LDPC_OK", -1: "LDPC_EINVAL", -2: "LDPC_EUNSUPPORTED", -3: "LDPC_EDEVICE",
           -4: "LDPC_ESINGULAR", -5: "LDPC_ENOMEM", -6: "LDPC_ETIMEOUT"}
-WALK_MSGS = {1: "MAX ERRORS; OUT OF SYNC", 2: "IN SYNC; PHASE INVERTED", 3: "IN SYNC"}
 
-
-class WalkIO(ctypes.Structure):
-    """ldpc_walk_io (include/ldpc_hip.h)."""
-    _fields_ = [("state", ctypes.c_int32), ("errors", ctypes.c_int32),
-                ("last_pass", ctypes.c_int64), ("anchor_pos", ctypes.c_int64),
-                ("consumed", ctypes.c_int64), ("produced", ctypes.c_int32),
-                ("n_msgs", ctypes.c_int32), ("grid_frames", ctypes.c_int32),
-                ("grid_fails", ctypes.c_int32), ("requests", ctypes.c_int32),
-                ("surprises", ctypes.c_int32), ("steps", ctypes.c_int32),
-                ("restarts", ctypes.c_int32), ("walk_us", ctypes.c_double),
-                ("wait_us", ctypes.c_double)]
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _i32p = ctypes.POINTER(ctypes.c_int32)
@@ -82,8 +70,6 @@ SIGNATURES = {
     "ldpc_serve_windows": (_i, [_vp, ctypes.POINTER(ctypes.c_int64), _i, _u8p, _i32p]),
     "ldpc_serve_end": (_i, [_vp]),
     "ldpc_ctx_streams": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_void_p)]),
-    "ldpc_walk_span": (_i, [_vp, _i, _i, _i, _f32p, _i64, _i, _i, _i, ctypes.c_void_p, _u8p,
-                            _u8p, _i]),
     "ldpc_alist_read": (_i, [ctypes.c_char_p, _i32p, _i32p, _i32p, _i32p, _i64]),
     "ldpc_set_waves_per_cu": (_i, [_vp, _i]),
     "ldpc_set_launch_mode": (_i, [_vp, _i]),
@@ -371,25 +357,6 @@ class Decoder:
 
     def serve_end(self):
         _check(lib().ldpc_serve_end(self._ctx), self._ctx)
-
-    def walk_span(self, samples, noutput_bytes, method=METHOD_SUMPRODUCT, max_iters=5,
-                  precision=PREC_F64, elem_stride=1, state=0, errors=0, last_pass=-(1 << 60),
-                  msgs_cap=None):
-        """ldpc_walk_span: the decoder block's frame loop over one sample span
-        on the device.  Returns dict(out (bytes), msgs (list of str), io
-        (WalkIO)); raises on LDPC_ETIMEOUT like any other error."""
-        x = np.ascontiguousarray(samples, np.float32).reshape(-1)
-        n = (x.size + elem_stride - 1) // elem_stride
-        cap = int(msgs_cap) if msgs_cap is not None else max(64, n // 4 + 64)
-        out = np.zeros(max(int(noutput_bytes), 1), np.uint8)
-        msgs = np.zeros(max(cap, 1), np.uint8)
-        io = WalkIO(state=int(state), errors=int(errors), last_pass=int(last_pass), anchor_pos=-1)
-        _check(lib().ldpc_walk_span(self._ctx, int(method), int(max_iters), int(precision),
-                                    _p(x, _f32p), x.size, int(elem_stride), 0,
-                                    int(noutput_bytes), ctypes.byref(io), _p(out, _u8p),
-                                    _p(msgs, _u8p), cap), self._ctx)
-        return dict(out=out[:io.produced].tobytes(),
-                    msgs=[WALK_MSGS[int(m)] for m in msgs[:io.n_msgs]], io=io)
 
     def decode_device(self, d_in, B, d_packed, method=METHOD_SUMPRODUCT, max_iters=50,
                       et_period=1, precision=PREC_F64, polarity=1.0, cw_stride=None,

@@ -276,51 +276,6 @@ int ldpc_serve_windows(ldpc_ctx *ctx, const int64_t *windows, int B, uint8_t *ou
                        int32_t *syn_weight_opt);
 int ldpc_serve_end(ldpc_ctx *ctx);
 
-/* The decoder block's whole frame loop over one host span, on the device
- * (reference general_work lib/ldpc_decoder_cb_impl.cc:146-226: every decode,
- * the sync state machine, the output bytes and the sync messages).  One
- * persistent launch: one wave steps the loop exactly while the other waves
- * decode the windows it and its speculation ask for.  Small codes only
- * (the context's small-code kernels, N <= 64, KB <= 4 and M/8 <= 4: the
- * reference's default H and QA H); other codes return LDPC_EUNSUPPORTED.
- *
- * io (in): state (0 out of sync, 1 in sync, 2 in sync inverted), errors,
- *   last_pass = the position, relative to this span, of the last window that
- *   passed in sync (e.g. -N for the last frame of the previous call, or a
- *   large negative value for none); anchor_pos = a position (>= 0, relative)
- *   whose phase is the stream's frame grid, -1 if none is known (a hint for
- *   the speculation only: results do not depend on it).
- * io (out): the same three after the loop, consumed (input items),
- *   produced (output bytes, written to out), n_msgs message codes in msgs
- *   (LDPC_WALK_MSG_*: print "MAX ERRORS; OUT OF SYNC", "IN SYNC; PHASE
- *   INVERTED", "IN SYNC" in this order), anchor_pos (a position on the newest
- *   grid: two windows N apart that both passed in sync; -1 none) and
- *   diagnostics.  The loop stops early (consumed < what the reference would
- *   consume) only when msgs_cap is reached; the caller then continues with
- *   the next call, as the reference's loop state carries over.
- * Returns LDPC_OK, LDPC_EUNSUPPORTED, or LDPC_ETIMEOUT when a wait inside the
- * launch passed its deadline (io and out are then not valid; the caller
- * redoes the span another way).  Sample i of the span is in[i*elem_stride];
- * reuse_span as for ldpc_decode_windows.  Synchronous. */
-#define LDPC_WALK_MSG_LOST 1
-#define LDPC_WALK_MSG_INVERTED 2
-#define LDPC_WALK_MSG_SYNC 3
-typedef struct {
-  int32_t state, errors;
-  int64_t last_pass;
-  int64_t anchor_pos;
-  int64_t consumed;
-  int32_t produced;
-  int32_t n_msgs;
-  int32_t grid_frames, grid_fails; /* in-sync frames seen / failing */
-  int32_t requests, surprises;     /* windows decoded / asked for unplanned */
-  int32_t steps, restarts;         /* walker loop turns / speculation restarts */
-  double walk_us, wait_us;         /* device time in the loop / waiting for results */
-} ldpc_walk_io;
-int ldpc_walk_span(ldpc_ctx *ctx, int method, int max_iters, int precision, const float *in,
-                   int64_t n_in_floats, int elem_stride, int reuse_span, int noutput_bytes,
-                   ldpc_walk_io *io, uint8_t *out, uint8_t *msgs, int msgs_cap);
-
 /* Device-resident buffers (already in HBM); enqueues on `hip_stream`
  * (hipStream_t, NULL = the context's own stream) and returns without
  * synchronising -- except min-sum on a large-code context, whose pass loop
@@ -341,7 +296,9 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
  * several ldpc_decode_device calls in flight (LDPC_MODE_THROUGHPUT): n
  * (1..16) streams that run concurrently -- each on its own hardware queue,
  * checked by a probe launch pair when the set is first made -- owned by the
- * context (destroyed by ldpc_destroy).  A caller's own streams may share a
+ * context (destroyed by ldpc_destroy); with fewer hardware queues than n
+ * (GPU_MAX_HW_QUEUES), the concurrent ones are handed out again in turn.  A
+ * caller's own streams may share a
  * hardware queue, depending on the streams the process made before them, and
  * then serialise their launches.  (Replaces nothing in the reference: its
  * decode runs on the calling thread, lib/ldpc_decoder_cb_impl.cc:155-164.) */

@@ -132,24 +132,33 @@ def test_block_low_snr_streams_match_restated_general_work(Hr, method, iters, ch
 
 
 @pytest.mark.parametrize("ebn0", [1.0, 3.0])
-def test_grid_guesses_exact_and_fewer_windows(Hr, ebn0, monkeypatch):
-    """The dry run's grid guesses (ldpc_decoder_cb_impl.cc header) change
-    only which windows are decoded, never the stream: both plans give the
-    restated general_work's output, the grid plan with fewer windows."""
+def test_plans_exact_and_windows_bounded(Hr, ebn0, monkeypatch):
+    """The dry run's plan (ldpc_decoder_cb_impl.cc header; the A/B knobs
+    LDPC_BLOCK_MAXWANT and LDPC_BLOCK_SEARCHES) changes only which windows
+    are decoded, never the stream: every plan gives the restated
+    general_work's output, and the default plan's grid guesses decode at most
+    a few times the reference loop's own decodes."""
     import bench
     y, _ = bench.synth(Hr, 192, ebn0, 31)
     x = np.zeros(2 * y.size, np.float32)
     x[0::2] = y.ravel()
     s = x.view(np.complex64)
-    exp = orc.run_stream(1, Hr, s, iterations=5, chunks=[64 * 48] * 4)
+    stats = {}
+    exp = orc.run_stream(1, Hr, s, iterations=5, chunks=[64 * 48] * 4, stats=stats)
+    plans = {"default": {}, "maxwant64": {"LDPC_BLOCK_MAXWANT": "64"},
+             "searches1": {"LDPC_BLOCK_SEARCHES": "1"}, "whole": {"LDPC_BLOCK_MAXWANT": "-1",
+                                                                 "LDPC_BLOCK_SEARCHES": "0"}}
     decoded = {}
-    for plan in ("0", "1"):
-        monkeypatch.setenv("LDPC_BLOCK_ANCHOR", plan)
+    for plan, env in plans.items():
+        for k in ("LDPC_BLOCK_MAXWANT", "LDPC_BLOCK_SEARCHES"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         blk = L.ldpc_decoder_cb(1, _backend=oracle_backend(1, Hr))
         tb = fg.top_block(chunk=64 * 48, out_space=4 * 48)
         src, dst = fg.vector_source_c(s), fg.vector_sink_b()
         tb.connect(src, blk, dst)
         tb.run()
-        assert (dst.array() == exp).all()
+        assert (dst.array() == exp).all(), plan
         decoded[plan] = blk.frames_decoded
-    assert decoded["1"] < decoded["0"]
+    assert decoded["default"] <= 16 * stats["decodes"], (decoded, stats["decodes"])

@@ -12,13 +12,18 @@ from ldpc_ece535a import flowgraph as fg
 pytestmark = pytest.mark.gpu
 
 
-PATHS = {"serve": {}, "launch": {"LDPC_BLOCK_SERVE": "0"}, "walk": {"LDPC_BLOCK_WALK": "1"}}
+PATHS = {"serve": {}, "launch": {"LDPC_BLOCK_SERVE": "0"},
+         # the planner's A/B knobs: short dry runs, one search per round
+         "plan": {"LDPC_BLOCK_MAXWANT": "64", "LDPC_BLOCK_SEARCHES": "1"},
+         # every diagnostic knob on: stderr lines only, the same bytes
+         "diag": {"LDPC_BLOCK_DEBUG": "2", "LDPC_BLOCK_PROFILE": "2", "LDPC_WIN_PROFILE": "2",
+                  "LDPC_SERVE_DEBUG": "1"}}
 
 
 def _block(method, path, **kw):
     """The block with its rounds through the window server (default), a
-    launch per round (LDPC_BLOCK_SERVE=0), or the frame loop on the device
-    (LDPC_BLOCK_WALK=1)."""
+    launch per round (LDPC_BLOCK_SERVE=0), another dry-run plan, or every
+    diagnostic on."""
     import os
     env = PATHS[path]
     os.environ.update(env)

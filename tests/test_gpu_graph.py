@@ -143,44 +143,33 @@ def test_dvbs2_like_other_methods_vs_sparse_oracle(dvb, method, prec):
 def test_dvbs2_like_full_batch_roundtrip(dvb):
     """Config-4 batch (1024 frames at 2 dB): every frame decodes to its info
     bits with a zero syndrome, f64 and f32; all 1024 f64 frames (packed
-    bytes, iterations, syndromes) equal the sparse oracle's -- on the
-    narrow-chunk pipeline (the default) and the edge-message passes
-    (LDPC_MS_PIPELINE=0)."""
-    import os
-    import ldpc_ece535a as L
-    from oracle import oracle as orc
+    bytes, iterations, syndromes) equal the sparse oracle's."""
     csr, d = dvb
     M, N, rp, ci = csr
     info, y = _noisy(csr, 1024, 2, seed=4)
     want = np.packbits(info, axis=1)
+    from oracle import oracle as orc
     ref = orc.decode_batch_sparse(0, rp, ci, M, N, y, 50, nthreads=16, want_bits=False)
-    others = []
-    for mode in ("0",):
-        os.environ["LDPC_MS_PIPELINE"] = mode
-        try:
-            others.append(L.Decoder(csr=csr))
-        finally:
-            del os.environ["LDPC_MS_PIPELINE"]
-    for dec, name in ((d, "narrow"), (others[0], "edge passes")):
-        for prec in (0, 1):
-            out = dec.decode(y, method=0, max_iters=50, precision=prec, want_bits=False)
-            assert (out["synd"] == 0).all(), name
-            assert (out["packed"] == want).all(), name
-            if prec == 0:
-                for k in ("packed", "iters", "synd"):
-                    np.testing.assert_array_equal(out[k], ref[k], err_msg="%s %s" % (name, k))
-    for o in others:
-        o.close()
+    for prec in (0, 1):
+        out = d.decode(y, method=0, max_iters=50, precision=prec, want_bits=False)
+        assert (out["synd"] == 0).all()
+        assert (out["packed"] == want).all()
+        if prec == 0:
+            for k in ("packed", "iters", "synd"):
+                np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
 
 
-@pytest.mark.parametrize("method,db", [(0, 2), (1, 2), (0, 4), (1, 1)])
-def test_graph_path_repeated_compaction(method, db):
+@pytest.mark.parametrize("method,db,compact", [(0, 2, "1"), (1, 2, "1"), (0, 4, "1"), (1, 1, "1"),
+                                               (1, 2, "0")])
+def test_graph_path_repeated_compaction(method, db, compact, monkeypatch):
     """Thousands of frames on the large-code kernels: running frames are
-    compacted several times as others stop; every output (bits, iterations,
+    compacted several times as others stop (sum-product's edge-message
+    passes; LDPC_GRAPH_COMPACT=0: never); every output (bits, iterations,
     syndromes, posteriors) must still be the oracle's."""
     import bench
     import ldpc_ece535a as L
     from oracle import oracle as orc
+    monkeypatch.setenv("LDPC_GRAPH_COMPACT", compact)
     d = L.Decoder(force_graph=True)
     y, _ = bench.synth(d.H, 4096, db, 50 + db)
     out = d.decode(y, method=method, max_iters=50, precision=0, want_llr=True)

@@ -1,12 +1,11 @@
-"""Large-code min-sum has two implementations (ldpc_capi.hip decode_graph):
-the narrow-chunk frame pipeline with compressed check messages
-(ldpc_graph_msn.hip, the default, LDPC_MS_PIPELINE=2) and the edge-message
-passes (ldpc_graph.hip, LDPC_MS_PIPELINE=0), chosen at context creation.
-Both must reproduce the oracle exactly: the reference's
-fixtures on its own H forced onto the large-code path (hard decisions, packed
-bytes, iterations, syndromes, posteriors), the DVB-S2-like code against the
-sparse restatement, non-finite samples, et_period 5, and batches far larger
-than the pipeline's slots (every slot recycled many times)."""
+"""Large-code min-sum runs on the narrow-chunk frame pipeline with
+compressed check messages (ldpc_graph_msn.hip).  It must reproduce the
+oracle exactly: the reference's fixtures on its own H forced onto the
+large-code path (hard decisions, packed bytes, iterations, syndromes,
+posteriors), the DVB-S2-like code against the sparse restatement, non-finite
+samples, et_period 5, batches far larger than the pipeline's slots (every
+slot recycled many times), and each knob and code shape that picks another
+of its paths."""
 import os
 
 import numpy as np
@@ -15,26 +14,24 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-MODES = ["2", "0"]
-IDS = ["narrow", "edge"]
-
-
-def _decoder(mode, **kw):
+def _decoder(env=None, **kw):
     import ldpc_ece535a as L
-    old = os.environ.get("LDPC_MS_PIPELINE")
-    os.environ["LDPC_MS_PIPELINE"] = mode
+    env = env or {}
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         return L.Decoder(**kw)
     finally:
-        if old is None:
-            del os.environ["LDPC_MS_PIPELINE"]
-        else:
-            os.environ["LDPC_MS_PIPELINE"] = old
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
-@pytest.fixture(scope="module", params=MODES, ids=IDS)
-def gdec(request):
-    return _decoder(request.param, force_graph=True)
+@pytest.fixture(scope="module")
+def gdec():
+    return _decoder(force_graph=True)
 
 
 @pytest.mark.parametrize("db", [0, 2, 4])
@@ -80,12 +77,11 @@ def test_non_finite(gdec):
     np.testing.assert_array_equal(out["llr"], ref["post"])
 
 
-@pytest.mark.parametrize("mode", MODES, ids=IDS)
-def test_dvbs2_like_vs_sparse_oracle(mode):
+def test_dvbs2_like_vs_sparse_oracle():
     from ldpc_ece535a import codes
     from oracle import oracle as orc
     csr = codes.dvbs2_like(0)
-    d = _decoder(mode, csr=csr)
+    d = _decoder(csr=csr)
     M, N, rp, ci = csr
     rng = np.random.Generator(np.random.PCG64(77))
     info = rng.integers(0, 2, size=(160, N - M), dtype=np.uint8)
@@ -97,51 +93,72 @@ def test_dvbs2_like_vs_sparse_oracle(mode):
         np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
 
 
-@pytest.mark.parametrize("env", [{"LDPC_MSN_POST": "1"}, {"LDPC_MSN_ORDER": "0"},
-                                 {"LDPC_MSN_ORDER": "1"}, {"LDPC_MSN_CHUNKS": "5"},
-                                 {"LDPC_MSN_CHUNKS": "8"}, {"LDPC_MSN_FUSE": "0"},
-                                 {"LDPC_MSN_FUSE": "0", "LDPC_MSN_POST": "1"}],
-                         ids=["post-kernels", "identity-order", "residue-order", "5-chunks",
-                              "8-chunks", "decision-launch", "decision-launch-post-kernels"])
+def _dvb_noisy(csr, B, seed, db):
+    from ldpc_ece535a import codes
+    M, N = csr[0], csr[1]
+    rng = np.random.Generator(np.random.PCG64(seed))
+    info = rng.integers(0, 2, size=(B, N - M), dtype=np.uint8)
+    x = 2.0 * codes.ira_encode(csr, info) - 1.0
+    return (x + np.sqrt(10 ** (-db / 10)) * rng.standard_normal(x.shape)).astype(np.float32)
+
+
+@pytest.mark.parametrize("env", [{"LDPC_MSN_ORDER": "0"}, {"LDPC_MSN_ORDER": "1"},
+                                 {"LDPC_MSN_CHUNKS": "5"}, {"LDPC_MSN_CHUNKS": "8"}],
+                         ids=["identity-order", "residue-order", "5-chunks", "8-chunks"])
 def test_narrow_variants_dvbs2(env):
-    """The narrow-chunk pipeline's alternate paths on the DVB-S2-like code:
-    outputs from the separate post / column kernels instead of the variable
-    pass, the decision as its own launch instead of in the check pass's
-    last block per chunk, the identity storage order instead of the residue-class order (and
-    the residue order forced), a chunk count that is not a multiple of 8 (no
-    XCD placement) and a single chunk per XCD.  Packed bytes, bits,
-    iterations and syndromes equal the sparse oracle's; posteriors equal the
-    edge-message passes' bit for bit."""
+    """The pipeline's knobs on the DVB-S2-like code: the identity storage
+    order instead of the residue-class order (and the residue order forced),
+    a chunk count that is not a multiple of 8 (no XCD placement) and a single
+    chunk per XCD.  Packed bytes, bits, iterations and syndromes equal the
+    sparse oracle's; posteriors equal the default settings' bit for bit (the
+    posteriors themselves are pinned by test_fixtures)."""
     from ldpc_ece535a import codes
     from oracle import oracle as orc
     csr = codes.dvbs2_like(0)
     M, N, rp, ci = csr
-    rng = np.random.Generator(np.random.PCG64(91))
-    info = rng.integers(0, 2, size=(96, N - M), dtype=np.uint8)
-    x = 2.0 * codes.ira_encode(csr, info) - 1.0
-    y = (x + np.sqrt(10 ** (-1.5 / 10)) * rng.standard_normal(x.shape)).astype(np.float32)
-    saved = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        d = _decoder("2", csr=csr)
-        out = d.decode(y, method=0, max_iters=30, want_llr=True)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+    y = _dvb_noisy(csr, 96, 91, 1.5)
+    out = _decoder(env, csr=csr).decode(y, method=0, max_iters=30, want_llr=True)
     ref = orc.decode_batch_sparse(0, rp, ci, M, N, y, 30, nthreads=16)
     for k in ("bits", "packed", "iters", "synd"):
         np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
-    edge = _decoder("0", csr=csr).decode(y, method=0, max_iters=30, want_llr=True)
-    np.testing.assert_array_equal(out["llr"].view(np.uint32), edge["llr"].view(np.uint32))
+    base = _decoder(csr=csr).decode(y, method=0, max_iters=30, want_llr=True)
+    np.testing.assert_array_equal(out["llr"].view(np.uint32), base["llr"].view(np.uint32))
+
+
+def test_post_kernels_info_first_order():
+    """The DVB-S2-like code with its columns in the ETSI order (information
+    first): the staircase columns move in the residue-class storage order,
+    so the outputs come from the separate msn_post / msn_cols kernels
+    instead of the variable pass.  Equal to the sparse oracle; posteriors
+    equal the same frames through the parity-first code (the same graph, its
+    columns renamed)."""
+    import ldpc_ece535a as L
+    from ldpc_ece535a import codes
+    from oracle import oracle as orc
+    csr = codes.dvbs2_like(0)
+    M, N, rp, ci = csr
+    K = N - M
+    newcol = np.where(ci >= M, ci - M, ci + K).astype(np.int64)  # parity -> K.., info -> 0..
+    rows = np.repeat(np.arange(M), np.diff(rp))
+    order = np.lexsort((newcol, rows))
+    ci2 = newcol[order].astype(np.int32)
+    csr2 = (M, N, rp, ci2)
+    r = L._capi.plan_storage_order(csr2)
+    assert r["order"] == 1 and not np.array_equal(r["cpos"][M:], np.arange(M, N))
+    y = _dvb_noisy(csr, 96, 17, 1.5)
+    y2 = np.concatenate([y[:, M:], y[:, :M]], axis=1)  # the same frames, columns renamed
+    out = _decoder(csr=csr2).decode(y2, method=0, max_iters=30, want_llr=True)
+    ref = orc.decode_batch_sparse(0, rp, ci2, M, N, y2, 30, nthreads=16)
+    for k in ("bits", "packed", "iters", "synd"):
+        np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
+    base = _decoder(csr=csr).decode(y, method=0, max_iters=30, want_llr=True)
+    llr1 = np.concatenate([base["llr"][:, M:], base["llr"][:, :M]], axis=1)
+    np.testing.assert_array_equal(out["llr"].view(np.uint32), llr1.view(np.uint32))
 
 
 @pytest.mark.parametrize("hi_groups,hi_deg,dc", [(3, 8, 14), (5, 12, 20)],
                          ids=["dc14", "dc20"])
-@pytest.mark.parametrize("mode", MODES, ids=IDS)
-def test_high_check_degree_vs_sparse_oracle(mode, hi_groups, hi_deg, dc):
+def test_high_check_degree_vs_sparse_oracle(hi_groups, hi_deg, dc):
     """Rate-3/4 IRA codes in the DVB-S2 style (N = 7200, 360-column groups)
     whose rows have 13-14 and 19-20 edges: the narrow pipeline's check pass
     then runs its 16- and 32-slot bodies with the slots past each block's
@@ -155,7 +172,7 @@ def test_high_check_degree_vs_sparse_oracle(mode, hi_groups, hi_deg, dc):
     csr = codes.ira_from_table(table, 5400, 7200)
     M, N, rp, ci = csr
     assert int(np.diff(rp).max()) == dc
-    d = _decoder(mode, csr=csr)
+    d = _decoder(csr=csr)
     rng = np.random.Generator(np.random.PCG64(hi_deg))
     info = rng.integers(0, 2, size=(200, N - M), dtype=np.uint8)
     x = 2.0 * codes.ira_encode(csr, info) - 1.0

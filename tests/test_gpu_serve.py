@@ -58,6 +58,32 @@ def test_serve_rounds_equal_launches_and_oracle(method, iters):
     dec.close()
 
 
+@pytest.mark.parametrize("env", [{"LDPC_SERVE_BLOCKS_PER_CU": "1"}, {"LDPC_SERVE_DEBUG": "1"}],
+                         ids=["one-workgroup-per-cu", "debug-counters"])
+def test_serve_knobs(env):
+    """The server's knobs (read per launch): one decoder workgroup per CU --
+    rounds of 300 and 5000 windows then take the one-wave form, a round of
+    one the workgroup form -- and the debug counters change no result."""
+    dec = L.Decoder()
+    Hr = dec.H
+    s = _span(Hr, 400, 21)
+    rng = np.random.default_rng(4)
+    os.environ.update(env)
+    try:
+        dec.stage_span(s, max_windows=8192)
+        dec.serve_begin(method=1, max_iters=5, max_windows=8192)
+        rounds = [_windows(rng, n, s.size, dec.N) for n in (1, 300, 5000)]
+        got = [dec.serve_windows(w) for w in rounds]
+        dec.serve_end()
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+    for w, g in zip(rounds, got):
+        ref = _oracle(1, Hr, s, w, 5)
+        assert (g["packed"] == ref["packed"]).all() and (g["synd"] == ref["synd"]).all()
+    dec.close()
+
+
 def test_serve_survives_its_deadline():
     """A launch that ends on its deadline between rounds is replaced by the
     next round; a decode on the context's stream afterwards is not blocked."""

@@ -6,7 +6,7 @@ Mbit/s, launches per call and decoded windows per output frame for each launch
 plan (the block's LDPC_BLOCK_* knobs, read when a block is made).
 
     python tools/block_bench.py [--batch 4096] [--reps 4] [--ebn0 4,2]
-        [--plans "default:,nofork:LDPC_BLOCK_FORK=0"]
+        [--plans "default:,launch:LDPC_BLOCK_SERVE=0"]
 (under rocprofv3 --kernel-trace --stats for the per-kernel split)"""
 import argparse
 import os
@@ -17,8 +17,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-KNOBS = ("LDPC_BLOCK_SERVE", "LDPC_BLOCK_WALK", "LDPC_WALK_BLOCKS_PER_CU", "LDPC_WALK_LEAD", "LDPC_BLOCK_FORK", "LDPC_BLOCK_ANCHOR", "LDPC_BLOCK_SPEC_BOTH", "LDPC_BLOCK_SPEC_DIV", "LDPC_BLOCK_BUDGET",
-         "LDPC_BLOCK_MAXWANT", "LDPC_BLOCK_SEARCHES", "LDPC_BLOCK_SEARCH_FIRST", "LDPC_BLOCK_SCHEDULE")
+KNOBS = ("LDPC_BLOCK_SERVE", "LDPC_BLOCK_MAXWANT", "LDPC_BLOCK_SEARCHES")
 
 
 def main():

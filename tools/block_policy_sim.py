@@ -10,7 +10,7 @@ block's outputs are compared with the restated general_work.  Planning knobs
 are the block's LDPC_BLOCK_* environment variables, so one table serves an A/B
 of several plans:
 
-    python tools/block_policy_sim.py --frames 512 --ebn0 4,2 --plans base:,nofork:LDPC_BLOCK_FORK=0
+    python tools/block_policy_sim.py --frames 512 --ebn0 4,2 --plans base:,searches1:LDPC_BLOCK_SEARCHES=1
 """
 import argparse
 import ctypes
@@ -138,7 +138,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=512, help="frames of input per call")
-    ap.add_argument("--plans", default="base:,nofork:LDPC_BLOCK_FORK=0")
+    ap.add_argument("--plans", default="base:,searches1:LDPC_BLOCK_SEARCHES=1")
     ap.add_argument("--child", default="")
     ap.add_argument("--cache", default="/tmp/blkpol")
     a = ap.parse_args()
