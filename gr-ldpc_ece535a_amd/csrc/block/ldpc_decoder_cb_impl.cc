@@ -337,7 +337,7 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
       throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
                                ldpc_last_error(d_ctx));
   }
-  for (int b = 0; b < B; ++b) d_memo[d_want[b] & 1][slot(d_want[b] >> 1)] = (int32_t)(base + b);
+  for (int b = 0; b < B; ++b) d_memo[(size_t)d_want[b]] = (int32_t)(base + b);
   d_touched.insert(d_touched.end(), d_want.begin(), d_want.end());
   d_frames_decoded += B;
   d_launches += 1;
@@ -345,7 +345,7 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
 
 void ldpc_decoder_cb_impl::want(int64_t pos, int pol, int nin) {
   if (pos < 0 || pos + (int64_t)d_N > nin || d_want.size() >= (size_t)max_windows(d_N)) return;
-  int32_t &m = d_memo[pol][slot(pos)];
+  int32_t &m = d_memo[mi(pos, pol)];
   if (m == -1) {
     m = -2;  // pending: wanted by this launch
     d_want.push_back((pos << 1) | pol);
@@ -358,11 +358,10 @@ int ldpc_decoder_cb_impl::pass_run(int pol, int pos, int nin) {
   // a call, so a run stays a run), and the path is compressed to its end
   const int N = (int)d_N, thr = (int)d_M / 8;
   int32_t *skip = d_skip[pol].data();
-  const int32_t *memo = d_memo[pol].data();
   int p = pos;
   while (p + N <= nin) {
     const int64_t s = slot(p);
-    const int32_t u = memo[s];
+    const int32_t u = d_memo[mi(p, pol)];
     if (u < 0 || d_rsynd[u] > thr) break;
     p = skip[s] > p ? skip[s] : p + N;
   }
@@ -397,7 +396,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
           d_grid_frames += k;
           for (int i = 0; i < k; ++i)
             std::memcpy(out + r.produced + (size_t)i * mo,
-                        &d_rpacked[(size_t)d_memo[pol][slot(pos + i * N)] * KB], (size_t)mo);
+                        &d_rpacked[(size_t)d_memo[mi(pos + i * N, pol)] * KB], (size_t)mo);
           // two frames in a row pass in sync: their grid is the stream's
           if (k > 1 || d_last_pass == d_abs + pos - N) d_anchor = (int)((d_abs + pos) % N);
           d_last_pass = d_abs + pos + (int64_t)(k - 1) * N;
@@ -407,12 +406,46 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
         out_run = 0;
         continue;
       }
+      if (!exact && (d_anchor < 0 || (d_abs + pos) % N == d_anchor)) {
+        // dry run, in sync on the grid, windows not decoded yet: each is
+        // guessed to pass (the general step below), so the run of them goes
+        // in one tight loop -- the same wants in the same order, the same
+        // position -- up to the first decoded window or one known to pass at
+        // the other polarity (those take the general step)
+        const bool both = grid_fails_often();
+        const size_t maxw = (size_t)max_windows(d_N);
+        int32_t *mm = d_memo.data();
+        int p = pos, prod = r.produced;
+        while (nin - p >= N && noutput - prod >= mo && d_want.size() < max_want) {
+          int32_t *m0 = mm + mi(p, pol), *m1 = mm + mi(p, pol ^ 1);
+          if (*m0 >= 0) break;
+          const int32_t o = *m1;
+          if (o >= 0 && d_rsynd[o] <= thr) break;
+          if (*m0 == -1 && d_want.size() < maxw) {
+            *m0 = -2;
+            d_want.push_back(((int64_t)p << 1) | pol);
+          }
+          if (both && o == -1 && d_want.size() < maxw) {
+            *m1 = -2;
+            d_want.push_back(((int64_t)p << 1) | (pol ^ 1));
+          }
+          p += N;
+          prod += mo;
+        }
+        if (p > pos) {
+          r.consumed = p;
+          r.produced = prod;
+          out_run = 0;
+          if (d_want.size() >= max_want) return STALLED;
+          continue;
+        }
+      }
     }
     Replay n = r;
     bool guessed_out = false, lost = false, inverted = false, synced = false;
     // checkFrame(vhat, M/8) > M/8 (:166-168); it stops counting past the
     // threshold, so comparing the full weight gives the same decision
-    int32_t use = d_memo[pol][slot(pos)];
+    int32_t use = d_memo[mi(pos, pol)];
     // the dry run's guess: a window on the grid the stream was last seen in
     // sync on passes, any other fails (a misaligned window passes ~1 % of the
     // time); with no grid seen yet, frames in sync pass
@@ -428,7 +461,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       // (the complement of a codeword leaves every odd-weight row unsatisfied:
       // 20 of the default H's 32)
       if (pass) {
-        const int32_t o = d_memo[pol ^ 1][slot(pos)];
+        const int32_t o = d_memo[mi(pos, pol ^ 1)];
         if (o >= 0 && d_rsynd[o] <= thr) pass = false;
       }
       guessed_out = !pass;
@@ -461,7 +494,7 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
         }
       }
       if (n.state == STATE_OUT_OF_SYNC) {  // the "-tx" retry, :178-198
-        const int32_t i2 = d_memo[pol ^ 1][slot(pos)];
+        const int32_t i2 = d_memo[mi(pos, pol ^ 1)];
         bool pass2 = false;
         if (i2 >= 0) {
           pass2 = d_rsynd[i2] <= thr;
@@ -490,9 +523,11 @@ ldpc_decoder_cb_impl::Outcome ldpc_decoder_cb_impl::replay(Replay &r, bool exact
       n.produced += mo;
     }
     if (exact) {
-      if (lost) std::cout << "MAX ERRORS; OUT OF SYNC" << std::endl;
-      if (inverted) std::cout << "IN SYNC; PHASE INVERTED" << std::endl;
-      if (synced) std::cout << "IN SYNC" << std::endl;
+      // the reference's messages (:174, :190, :202); flushed once per call
+      // (general_work's end), not per line: a flush is a write syscall
+      if (lost) std::cout << "MAX ERRORS; OUT OF SYNC\n";
+      if (inverted) std::cout << "IN SYNC; PHASE INVERTED\n";
+      if (synced) std::cout << "IN SYNC\n";
     }
     if (!exact && d_searches_now > 0 && guessed_out && n.state == STATE_OUT_OF_SYNC &&
         out_run == 0 && searches++ >= d_searches_now)
@@ -518,7 +553,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
   // the memo and the jump table keep their size between calls: only the
   // entries the last call set go back to "not decoded" (a full reset was
   // 2 x 4 bytes per input sample per call)
-  for (int64_t key : d_touched) d_memo[key & 1][slot(key >> 1)] = -1;
+  for (int64_t key : d_touched) d_memo[(size_t)key] = -1;
   for (int64_t key : d_skip_touched) d_skip[key & 1][slot(key >> 1)] = 0;
   d_touched.clear();
   d_skip_touched.clear();
@@ -530,10 +565,8 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
     d_nshift = -1;
     for (int sh = 0; sh < 31; ++sh)
       if ((1 << sh) == N) d_nshift = sh;
-    for (int pl = 0; pl < 2; ++pl) {
-      d_memo[pl].assign((size_t)N * (size_t)d_rows, -1);
-      d_skip[pl].assign((size_t)N * (size_t)d_rows, 0);
-    }
+    d_memo.assign((size_t)2 * N * (size_t)d_rows, -1);
+    for (int pl = 0; pl < 2; ++pl) d_skip[pl].assign((size_t)N * (size_t)d_rows, 0);
   }
   d_rsynd.clear();
   d_rpacked.clear();
@@ -635,6 +668,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       for (int i = 0; i < 4; ++i) last[i] = d_prof[i];
     }
   }
+  std::cout.flush();
   join_stage();  // no launch this call: the staging must still finish
   if (d_serving) {  // the call's window server may finish (no wait)
     d_serving = false;

@@ -112,15 +112,18 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
 
   // general_work's decode memo for the current call: the result of window
   // (position p, polarity) -- p in samples from the call's first input item,
-  // polarity 0 = +tx, 1 = -tx -- is entry d_memo[pol][slot(p)] of d_rsynd /
-  // d_rpacked (-1: not decoded, -2: wanted by the launch being planned).  Keys are (p << 1) | pol.
-  std::vector<int32_t> d_memo[2];
+  // polarity 0 = +tx, 1 = -tx -- is entry d_memo[mi(p, pol)] = d_memo[key] of
+  // d_rsynd / d_rpacked (-1: not decoded, -2: wanted by the round being
+  // planned), key = (p << 1) | pol: position-major, both polarities of a
+  // position side by side, as the out-of-sync search reads them
+  std::vector<int32_t> d_memo;
+  static size_t mi(int64_t p, int pol) { return (size_t)((p << 1) | pol); }
   std::vector<int32_t> d_rsynd;
-  // d_skip[pol][slot(p)] > p: frames p, p + N, ... before it are decoded and pass
+  // d_skip[pol][slot(p)] > p: frames p, p + N, ... before it are decoded and
+  // pass.  Stored grid-major -- position p at (p mod N) * d_rows + p / N -- so
+  // a run of frames on one grid reads consecutive words instead of one word
+  // every N
   std::vector<int32_t> d_skip[2];
-  // memo and jump entries are stored grid-major -- position p at
-  // (p mod N) * d_rows + p / N -- so a run of frames on one grid reads
-  // consecutive words instead of one word every N
   int64_t d_rows = 0;
   int d_nshift = -1;  // log2(N) when N is a power of two
   int64_t slot(int64_t p) const {

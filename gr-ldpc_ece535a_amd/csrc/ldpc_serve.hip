@@ -101,6 +101,7 @@ __device__ __forceinline__ uint64_t wave_uniform(uint64_t v) {
 // so a slot read before the host rewrote it is read again -- go to device
 // memory (dkeys, agent-scope stores), then, behind the wave's vmcnt(0), the
 // round word to the ctl copies.
+constexpr int kKeyLoads = 8;
 __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
   uint32_t last = s.start_epoch;
   const uint64_t t_start = ticks();
@@ -119,18 +120,27 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
       const uint64_t tag = (uint64_t)(ep & 0xFFFFFFu);
       const uint64_t t_keys = ticks();
       bool lost = false;  // a key slot that never showed this epoch (the host is gone)
-      for (int64_t c = -1; c < B && !lost; c += 64) {  // key slot c + lane (chunk -1: this read)
-        const int64_t b = c + lane;
-        const bool in = b >= 0 && b < B;
-        uint64_t k = c < 0 ? v : (in ? sys_load((const uint64_t *)s.keys + b) : 0);
-        while (__ballot(in && (k >> 40) != tag)) {
-          if (in && (k >> 40) != tag) k = sys_load((const uint64_t *)s.keys + b);
-          if (ticks() - t_keys > s.deadline) {
-            lost = true;
-            break;
-          }
+      // key slot c + 64 j + lane; kKeyLoads loads in flight per lane, so a
+      // round of up to 64 kKeyLoads keys costs one PCIe round trip (the
+      // first slot group, c = -1 and j = 0, is the read above)
+      for (int64_t c = -1; c < B && !lost; c += 64 * kKeyLoads) {
+        uint64_t k[kKeyLoads];
+        bool in[kKeyLoads];
+#pragma unroll
+        for (int j = 0; j < kKeyLoads; ++j) {
+          const int64_t b = c + 64 * j + lane;
+          in[j] = b >= 0 && b < B;
+          k[j] = (c < 0 && j == 0) ? v : (in[j] ? sys_load((const uint64_t *)s.keys + b) : 0);
         }
-        if (in) agent_store((uint64_t *)s.dkeys + b, k & kKeyMask);
+#pragma unroll
+        for (int j = 0; j < kKeyLoads; ++j) {
+          const int64_t b = c + 64 * j + lane;
+          while (!lost && __ballot(in[j] && (k[j] >> 40) != tag)) {
+            if (in[j] && (k[j] >> 40) != tag) k[j] = sys_load((const uint64_t *)s.keys + b);
+            if (ticks() - t_keys > s.deadline) lost = true;
+          }
+          if (in[j]) agent_store((uint64_t *)s.dkeys + b, k[j] & kKeyMask);
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lost) {
