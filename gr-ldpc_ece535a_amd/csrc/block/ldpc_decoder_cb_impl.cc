@@ -631,7 +631,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       std::cerr << "ldpc_decoder_cb: stall at " << r.consumed << " state " << r.state
                 << " errors " << r.errors << " grid " << d_anchor << ": launch " << d_want.size()
                 << " windows, dry run to " << dry.consumed << " state " << dry.state << std::endl;
-    if (d_debug && getenv("LDPC_BLOCK_DEBUG")[0] == '2') {  // what the launch holds
+    if (d_debug == 2) {  // what the round holds
       int64_t on_grid[2] = {0, 0}, off_grid[2] = {0, 0}, lo = INT64_MAX, hi = -1;
       for (int64_t w : d_want) {
         const int64_t p = w >> 1;

@@ -70,7 +70,9 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   bool d_serving = false;  // this call's server is running
   void stage_async(const float *in, int64_t n_floats, int max_windows);
   int stage_wait();
-  bool d_debug = getenv("LDPC_BLOCK_DEBUG") != nullptr;  // one line per round on stderr
+  // LDPC_BLOCK_DEBUG: one line per round on stderr (=2: also what it holds);
+  // read once, when the block is made
+  int d_debug = !getenv("LDPC_BLOCK_DEBUG") ? 0 : getenv("LDPC_BLOCK_DEBUG")[0] == '2' ? 2 : 1;
   // LDPC_BLOCK_PROFILE: host time split of general_work, printed when destroyed
   // (=2: also a line per call)
   bool d_profile = getenv("LDPC_BLOCK_PROFILE") != nullptr;

@@ -76,6 +76,7 @@ def child(cache):
     packed, synd, its, x, Hr = d["packed"], d["synd"], d["its"], d["x"], d["Hr"]
     base = x.ctypes.data
     per_launch = {}
+    per_launch_it = {}
     st = {"launches": 0, "windows": 0, "iters": 0, "max_iter_sum": 0}
 
     def fn(user, inp, n_floats, cw_stride, elem_stride, polarity, B, pk, sy):
@@ -89,6 +90,7 @@ def child(cache):
         st["iters"] += int(its[pol, pos].sum())
         k = blk.launches  # the launch this run of windows belongs to
         per_launch[k] = per_launch.get(k, 0) + B
+        per_launch_it[k] = per_launch_it.get(k, 0) + int(its[pol, pos].sum())
         return 0
 
     blk = L.ldpc_decoder_cb(1, _backend=fn)
@@ -105,6 +107,7 @@ def child(cache):
                 first = False
                 l0, w0, i0, m0 = blk.launches, st["windows"], st["iters"], len(made)
                 per_launch.clear()
+                per_launch_it.clear()
             o, used = blk.general_work(chunk // 16, cx[pos:pos + chunk])
             made.append(o)
             pos += used
@@ -120,7 +123,16 @@ def child(cache):
     # kernel floor) plus a cost per window (5 iterations on one MI355X:
     # "56,12.8", profiles/round4/block/)
     lin = os.environ.get("LDPC_SIM_MODEL")
-    if lin:
+    srv = os.environ.get("LDPC_SIM_SERVER")
+    if srv:
+        # window server: a round costs its latency (fixed + the slowest
+        # window's iterations) plus its window-iterations at the decode
+        # throughput: "round_us,per_iter_us,window_iter_ns"
+        r0, ri, wn = (float(v) for v in srv.split(","))
+        t = 0.0
+        for k, W in per_launch.items():
+            t += r0 + ri * int(d["iters_cap"]) + per_launch_it[k] * wn / 1e3
+    elif lin:
         lu, wn = (float(v) for v in lin.split(","))
         t = sum(lu + W * wn / 1e3 for W in per_launch.values())
     else:
@@ -156,7 +168,8 @@ def main():
             t = time.time()
             packed, synd, its = table(Hr, x, x.size // 2 - 64 + 1, a.iters, a.procs)
             ref = orc.run_stream(1, Hr, x.view(np.complex64), iterations=a.iters)
-            np.savez(cache, packed=packed, synd=synd, its=its, x=x, Hr=Hr, chunk=a.chunk, ref=ref)
+            np.savez(cache, packed=packed, synd=synd, its=its, x=x, Hr=Hr, chunk=a.chunk, ref=ref,
+                     iters_cap=a.iters)
             print("table %g dB: %d windows in %.1f s" % (db, synd.size, time.time() - t), flush=True)
         ref = np.load(cache)["ref"]
         for spec in a.plans.split(","):
