@@ -228,7 +228,7 @@ int ldpc_decoder_cb_impl::Stager::run() {
 
 void ldpc_decoder_cb_impl::stage_async(const float *in, int64_t n_floats, int max_windows) {
   Stager &sg = d_stager;
-  const bool serve = d_serve && (d_method == 0 || d_method == 1);
+  const bool serve = d_serve && d_serve_mode == 1 && (d_method == 0 || d_method == 1);
   if (!sg.th.joinable())
     sg.th = std::thread([&sg]() {
       std::unique_lock<std::mutex> lk(sg.mu);
@@ -297,7 +297,7 @@ void ldpc_decoder_cb_impl::forecast(int noutput_items, gr_vector_int &ninput_ite
   ninput_items_required[0] = noutput_items * d_N;
 }
 
-void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
+void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first, bool first_round) {
   const int KB = (int)(d_N - d_M + 7) / 8;
   const int B = (int)d_want.size();
   // results land straight at the end of the memo's result arrays
@@ -324,23 +324,42 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first) {
       if (rc < 0) throw std::runtime_error("ldpc_decoder_cb: decode failed: backend error");
       i = j;
     }
-  } else if (d_serving) {
-    const int rc = ldpc_serve_windows(d_ctx, d_want.data(), B, packed, synd);
-    if (rc < 0)
-      throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
-                               ldpc_last_error(d_ctx));
   } else {
-    const int rc = ldpc_decode_windows(d_ctx, d_method, (int)d_iterations, 1, d_precision, in,
-                                       2 * (int64_t)nin, 2, first ? 0 : 1, d_want.data(), B,
-                                       packed, synd);
-    if (rc < 0)
-      throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
-                               ldpc_last_error(d_ctx));
+    const bool small = d_serve && (d_serve_mode == 1 || (int64_t)B * d_iterations <= kServeWork);
+    if (small && !d_serving) serve_start();
+    if (small && d_serving) {
+      const int rc = ldpc_serve_windows(d_ctx, d_want.data(), B, packed, synd);
+      if (rc < 0)
+        throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
+                                 ldpc_last_error(d_ctx));
+    } else {
+      d_serving = false;  // (ldpc_decode_windows ends a running server first)
+      const int rc = ldpc_decode_windows(d_ctx, d_method, (int)d_iterations, 1, d_precision, in,
+                                         2 * (int64_t)nin, 2, first ? 0 : 1, d_want.data(), B,
+                                         packed, synd);
+      if (rc < 0)
+        throw std::runtime_error(std::string("ldpc_decoder_cb: decode failed: ") +
+                                 ldpc_last_error(d_ctx));
+      // after a call's first round (the grid, usually big) the rounds are
+      // mostly small: the server's launch goes behind this one now and starts
+      // while the next round is planned; later, a small round starts it
+      if (d_serve && d_serve_mode == 2 && first_round) serve_start();
+    }
   }
   for (int b = 0; b < B; ++b) d_memo[(size_t)d_want[b]] = (int32_t)(base + b);
   d_touched.insert(d_touched.end(), d_want.begin(), d_want.end());
   d_frames_decoded += B;
   d_launches += 1;
+}
+
+void ldpc_decoder_cb_impl::serve_start() {
+  const int rc = ldpc_serve_begin(d_ctx, d_method, (int)d_iterations, d_precision, max_windows(d_N));
+  if (rc == LDPC_OK)
+    d_serving = true;
+  else if (rc == LDPC_EUNSUPPORTED)
+    d_serve = false;  // this code / method: launches
+  else
+    throw std::runtime_error(std::string("ldpc_decoder_cb: window server: ") + ldpc_last_error(d_ctx));
 }
 
 void ldpc_decoder_cb_impl::want(int64_t pos, int pol, int nin) {
@@ -648,7 +667,7 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       t0 = t1;
     }
     join_stage();  // the span is on its way to the device before the launch
-    decode_wanted(in, nin, first && !staged);
+    decode_wanted(in, nin, first && !staged, first);
     if (d_profile) {
       const double t1 = now_s();
       d_prof[3] += t1 - t0;

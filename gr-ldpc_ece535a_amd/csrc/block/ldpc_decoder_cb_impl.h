@@ -63,11 +63,25 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
     int serve_rc = 0;            // ldpc_serve_begin's result
     int run();                   // stage (+ serve); returns the staging result
   } d_stager;
-  // Rounds of windows through the window server (ldpc_serve_*), one launch
-  // per call; false: a launch per round (ldpc_decode_windows), also for codes
-  // or methods the server does not take (LDPC_BLOCK_SERVE=0 forces it, A/B).
-  bool d_serve = !(getenv("LDPC_BLOCK_SERVE") && getenv("LDPC_BLOCK_SERVE")[0] == '0');
-  bool d_serving = false;  // this call's server is running
+  // How a round of windows is decoded: through the window server
+  // (ldpc_serve_*: one persistent launch serves the call's rounds) or by a
+  // launch of its own (ldpc_decode_windows).  The server answers a small
+  // round sooner; a big one (windows x iterations above kServeWork) runs
+  // faster as a launch, with the batch kernels' full throughput
+  // (profiles/round5/serve_latency*.txt).  LDPC_BLOCK_SERVE=0: launches only,
+  // =1: the server for every round (A/B); default: by round size.  Codes or
+  // methods the server does not take: launches.
+  int d_serve_mode = !getenv("LDPC_BLOCK_SERVE")           ? 2
+                     : getenv("LDPC_BLOCK_SERVE")[0] == '0' ? 0
+                     : getenv("LDPC_BLOCK_SERVE")[0] == '1' ? 1
+                                                            : 2;
+  // windows x iterations of the biggest round the server takes: the
+  // crossovers measured at ~700 windows of 5 iterations and ~150 of 50
+  // (profiles/round5/serve_latency.txt)
+  static const int64_t kServeWork = 4096;
+  bool d_serve = d_serve_mode != 0;  // the server takes this code and method (until it says otherwise)
+  bool d_serving = false;  // a server is running for this call
+  void serve_start();
   void stage_async(const float *in, int64_t n_floats, int max_windows);
   int stage_wait();
   // LDPC_BLOCK_DEBUG: one line per round on stderr (=2: also what it holds);
@@ -158,7 +172,8 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   void want(int64_t pos, int pol, int nin);
   // Decodes the windows d_want of the call's input into the memo (one
   // launch on the GPU; the test seam decodes runs of equally spaced windows).
-  void decode_wanted(const float *in, int nin, bool first);
+  // first: the span is not staged yet (copy it); first_round: the call's first round
+  void decode_wanted(const float *in, int nin, bool first, bool first_round);
   void adopt(ldpc_ctx *ctx);  // takes M, N from the context; checks the output shape
 
  public:

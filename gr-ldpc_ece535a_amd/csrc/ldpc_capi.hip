@@ -88,8 +88,11 @@ struct ldpc_ctx {
   struct Queue {
     void *stream;
     uint32_t base;  // counter value at the start of the next launch
+    int32_t *order = nullptr;  // longest-first order of the stream's launches (ldpc_set_frame_order)
+    int64_t order_cap = 0;
   };
   std::vector<Queue> queues;
+  int frame_order = 0;  // ldpc_set_frame_order
   // large-code path: the workspace is shared, so launches on a different
   // stream than the previous one first wait for it (graph_done)
   void *graph_stream = nullptr;
@@ -975,6 +978,8 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->d_srv_ctl) (void)hipFree(ctx->d_srv_ctl);
   if (ctx->d_srv_keys) (void)hipFree(ctx->d_srv_keys);
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
+  for (auto &qq : ctx->queues)
+    if (qq.order) (void)hipFree(qq.order);
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
     if (p) (void)hipFree(p);
   for (int32_t *p : ctx->d_msn)
@@ -1224,11 +1229,32 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
               hipSuccess ||
           (e = hipDeviceSynchronize()) != hipSuccess)
         return hip_err(ctx, e, "ticket reset");
+      for (auto &qq : ctx->queues)
+        if (qq.order) (void)hipFree(qq.order);
       ctx->queues.clear();
       q = 0;
     }
     // slots are handed out in order from zeroed memory (creation, reset)
-    ctx->queues.push_back({st, 0u});
+    ctx->queues.push_back({st, 0u, nullptr, 0});
+  }
+  a.order = nullptr;
+  if (ctx->frame_order == 1 && !d_win && pm_half == 0 && B > 1 && (method == 0 || method == 1)) {
+    ldpc_ctx::Queue &qq = ctx->queues[q];
+    if (qq.order_cap < B) {
+      // grown on the stream's own schedule: earlier launches of this stream
+      // may still read the old buffer
+      if (qq.order && (e = hipStreamSynchronize((hipStream_t)st)) != hipSuccess)
+        return hip_err(ctx, e, "hipStreamSynchronize");
+      if (qq.order) (void)hipFree(qq.order);
+      qq.order = nullptr;
+      qq.order_cap = 0;
+      if ((e = hipMalloc((void **)&qq.order, (size_t)B * sizeof(int32_t))) != hipSuccess)
+        return hip_err(ctx, e, "hipMalloc(frame order)");
+      qq.order_cap = B;
+    }
+    if (ldpc::launch_longest_first(d_in, cw_stride, elem_stride, ctx->N, B, qq.order, st) != 0)
+      return set_err(ctx, LDPC_EDEVICE, "frame order launch failed");
+    a.order = qq.order;
   }
   a.ticket = ctx->d_tickets + q * LDPC_TICKET_STRIDE;
   a.ticket_base = ctx->queues[q].base;
@@ -1837,6 +1863,13 @@ int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode) {
   // priority games
   ctx->waves_per_cu = mode == LDPC_MODE_THROUGHPUT ? 4 : 0;
   ctx->fair_cycles = mode == LDPC_MODE_THROUGHPUT ? 0 : 1800;
+  return LDPC_OK;
+}
+
+int ldpc_set_frame_order(ldpc_ctx *ctx, int order) {
+  if (!ctx || order < 0 || order > 1)
+    return set_err(ctx, LDPC_EINVAL, "order must be 0 (queue order) or 1 (longest first)");
+  ctx->frame_order = order;
   return LDPC_OK;
 }
 

@@ -894,12 +894,15 @@ __device__ __forceinline__ void mw_setup(const CodeView &code, int tid, MwTables
   }
 }
 
-// One frame: samples src[colq] * pol.  Leaves the hard decisions (by lane
+// One frame: samples src[colq] * pol.  DCN / DVN: row neighbours / column
+// entries the loops visit (>= dc_max - 1 / dv_max; the records' unused
+// fields are kNone).  Leaves the hard decisions (by lane
 // position) and posteriors in every wave; returns the syndrome weight and
 // the iterations used.  Starts with a workgroup barrier (the caller's LDS
 // reads of the previous frame must be done when it is entered: every caller
 // ends a frame with __syncthreads).  tb[64 S] must hold the identity.
-template <int PREC, int METHOD, int S, int NW, typename Real = typename Math<PREC>::Real>
+template <int PREC, int METHOD, int S, int NW, int DCN = kDcMax - 1, int DVN = kDvMax,
+          typename Real = typename Math<PREC>::Real>
 __device__ __forceinline__ int mw_frame(const CodeView &code, int max_iters, int et_period,
                                         MwTables<NW> &t, Real *tb, Real *eb, Real *rb, Real *sb,
                                         const typename Math<PREC>::Tab *logtab, const float *src,
@@ -931,23 +934,23 @@ __device__ __forceinline__ int mw_frame(const CodeView &code, int max_iters, int
     else
       tb[tid] = msg;
     __syncthreads();
-    Real nb[kDcMax - 1];
+    Real nb[DCN];
 #pragma unroll
-    for (int k = 0; k < kDcMax - 1; ++k) {
+    for (int k = 0; k < DCN; ++k) {
       const int n = field(t.rn, k);
       nb[k] = tb[n == kNone ? kDummy : n];
     }
     if constexpr (METHOD == 1) {
       Real T = Real(1);  // ascending column; dummies are exact 1.0 (:506-511)
 #pragma unroll
-      for (int k = 0; k < kDcMax - 1; ++k) T = T * nb[k];
+      for (int k = 0; k < DCN; ++k) T = T * nb[k];
       eb[tid] = Math<PREC>::check_msg(T, logtab);  // :513
     } else {
       const int self = sgn(msg);  // :350-376
       int prod = self;
       Real lo = Math<PREC>::max_();
 #pragma unroll
-      for (int k = 0; k < kDcMax - 1; ++k) {
+      for (int k = 0; k < DCN; ++k) {
         prod *= sgn(nb[k]);
         const Real beta = Math<PREC>::abs_(nb[k]);
         lo = beta < lo ? beta : lo;
@@ -961,9 +964,9 @@ __device__ __forceinline__ int mw_frame(const CodeView &code, int max_iters, int
     for (int q = 0; q < NW; ++q) {
       opaque(t.ce[q]);
       const int c = lane + 64 * q;
-      Real ev[kDvMax];
+      Real ev[DVN];
 #pragma unroll
-      for (int k = 0; k < kDvMax; ++k) {
+      for (int k = 0; k < DVN; ++k) {
         const int n = field(t.ce[q], k);
         ev[k] = eb[n == kNone ? kDummy : n];
       }
@@ -972,13 +975,13 @@ __device__ __forceinline__ int mw_frame(const CodeView &code, int max_iters, int
       bool bit;
       if constexpr (METHOD == 1) {  // :519-532
 #pragma unroll
-        for (int k = 0; k < kDvMax; ++k)
+        for (int k = 0; k < DVN; ++k)
           acc = field(t.ce[q], k) != kNone ? acc + (ev[k] + rc) : acc;
         bit = acc <= Real(0);
         post[q] = acc;
       } else {  // :379-403
 #pragma unroll
-        for (int k = 0; k < kDvMax; ++k)
+        for (int k = 0; k < DVN; ++k)
           acc = field(t.ce[q], k) != kNone ? acc + ev[k] : acc;
         const Real LQ = rc + acc;
         sb[c] = LQ;
@@ -1000,15 +1003,15 @@ __device__ __forceinline__ int mw_frame(const CodeView &code, int max_iters, int
     if ((h + 1) % et_period == 0 && weight == 0) break;
     if constexpr (METHOD == 1) {  // :540-553
       const Real rc = rb[t.col];
-      Real cv[kDvMax - 1];
+      Real cv[DVN - 1];
 #pragma unroll
-      for (int k = 0; k < kDvMax - 1; ++k) {
+      for (int k = 0; k < DVN - 1; ++k) {
         const int n = field(t.cn, k);
         cv[k] = eb[n == kNone ? kDummy : n];
       }
       Real acc = Real(0);
 #pragma unroll
-      for (int k = 0; k < kDvMax - 1; ++k)
+      for (int k = 0; k < DVN - 1; ++k)
         acc = field(t.cn, k) != kNone ? acc + (cv[k] + rc) : acc;
       msg = acc;
     } else {

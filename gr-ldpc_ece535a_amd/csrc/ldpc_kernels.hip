@@ -142,9 +142,11 @@ __global__ void __launch_bounds__(kThreads, MINB)
   // after the first frame, when the loads have long completed
   float pf[NW];
   {
-    const int64_t pb = (int64_t)a.waves + b;
+    int64_t pb = (int64_t)a.waves + b;
+    pb = pb < a.B ? pb : b;
+    if (a.order) pb = a.order[pb];
     float ppol;
-    const float *ps = frame_src(a, pb < a.B ? pb : b, ppol);
+    const float *ps = frame_src(a, pb, ppol);
     (void)ppol;  // the prefetch only pulls the samples into L2
 #pragma unroll
     for (int q = 0; q < NW; ++q) pf[q] = colq[q] >= 0 ? ps[(int64_t)colq[q] * a.elem_stride] : 0.0f;
@@ -156,10 +158,12 @@ __global__ void __launch_bounds__(kThreads, MINB)
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     const uint64_t c_start = __builtin_amdgcn_s_memtime();
 #endif
+    // the frame at queue position b (a.order: longest-first order)
+    const int64_t f = a.order ? (int64_t)a.order[b] : b;
     // the frame's channel samples, one load per lane and column position
     // (a permutation of the frame's N samples); positions past N are 0
     float xin[NW], pol;
-    const float *src = frame_src(a, b, pol);
+    const float *src = frame_src(a, f, pol);
 #pragma unroll
     for (int q = 0; q < NW; ++q)
       xin[q] = colq[q] >= 0 ? src[(int64_t)colq[q] * a.elem_stride] * pol : 0.0f;
@@ -171,12 +175,12 @@ __global__ void __launch_bounds__(kThreads, MINB)
       constexpr bool kFair = MINB != LDPC_TP_MINB;
       if (__ballot(bad) == 0)
         decode_frame<PREC, METHOD, S, NW, DCN, DVN, true, Real, true, kFair>(
-            code, a, b, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
+            code, a, f, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
       else
         decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, true, kFair>(
-            code, a, b, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
+            code, a, f, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
     } else {
-      decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, b, wt, tb, eb, rb, sb, lane, logtab,
+      decode_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a, f, wt, tb, eb, rb, sb, lane, logtab,
                                                   xin, colq, ppos);
     }
 #ifndef LDPC_NO_PREFETCH

@@ -107,6 +107,9 @@ struct DecodeArgs {
   // issue-priority threshold in core clocks for waves whose last iteration
   // was slow (0: off); see decode_frame
   uint32_t fair_cycles;
+  // frame order (ldpc_set_frame_order): queue position b decodes frame
+  // order[b] (null: frame b).  Outputs go to the frame's own index.
+  const int32_t *order;
 };
 
 // ---------------------------------------------------------------------------

@@ -189,8 +189,21 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
 // one window per wave (decode_frame, the batch kernels' one-wave form: fewer
 // issue slots per window), windows w, w + W, ... for wave w of W.  The two
 // forms share the workgroup's LDS (never at the same time).
+// Register budget (__launch_bounds__' second operand: waves per SIMD): three
+// waves per SIMD (<= 168 VGPRs).  Four (<= 128, the batch kernels' throughput
+// build) spill and made every round slower -- one window of 5 iterations 16.9
+// against 15.4 us, a round of 4096 windows 107 against 83 us
+// (profiles/round5/serve_latency.txt).  Big rounds go to launches instead
+// (the block's hybrid, ldpc_decoder_cb_impl.h).
+constexpr int kServeWavesPerSimd = 3;
+// bytes of the two forms' overlaid frame regions
+template <typename Real, int METHOD, int S, int NW, int DVN>
+__host__ __device__ size_t serve_lds_main() {
+  const size_t a = MwLayout<Real, S, NW>().total, b = (size_t)S * Layout<Real, METHOD, S, NW, DVN>::per_wave;
+  return align16(a > b ? a : b);
+}  // (__launch_bounds__' second operand: waves per SIMD)
 template <int PREC, int METHOD, int S, int NW, int DCN, int DVN>
-__global__ void __launch_bounds__(64 * S, 3) serve_kernel(CodeView code, DecodeArgs a, ServeArgs s) {
+__global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeView code, DecodeArgs a, ServeArgs s) {
   typedef typename Math<PREC>::Real Real;
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int64_t sslot[2];  // the round, the window key (workgroup form)
@@ -260,7 +273,7 @@ __global__ void __launch_bounds__(64 * S, 3) serve_kernel(CodeView code, DecodeA
         uint64_t hard[NW];
         Real post[NW];
         int used = 0;
-        const int weight = mw_frame<PREC, METHOD, S, NW>(code, a.max_iters, 1, mt, mtb, meb, mrb,
+        const int weight = mw_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a.max_iters, 1, mt, mtb, meb, mrb,
                                                          msb, logtab, a.in + (key >> 1),
                                                          (key & 1) ? -1.0f : 1.0f, 1, hard, post,
                                                          used);
@@ -334,8 +347,7 @@ int launch_s(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, hipS
              int *wg) {
   typedef typename Math<PREC>::Real Real;
   // the two forms' LDS, overlaid
-  const size_t lds = std::max(MwLayout<Real, S, NW>().total,
-                              (size_t)S * Layout<Real, METHOD, S, NW, DVN>::per_wave);
+  const size_t lds = serve_lds_main<Real, METHOD, S, NW, DVN>();
   const void *fn = (const void *)serve_kernel<PREC, METHOD, S, NW, DCN, DVN>;
   static int per_cu = 0;  // resident decoder workgroups per CU
   if (!per_cu) {
@@ -349,7 +361,7 @@ int launch_s(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, hipS
     // MI355X_MICROARCH.md "Residency"): workgroups past the resident ones
     // only start once the launch ends, and rounds go to the decoders that
     // started (the census), so this is a speed matter only
-    per_cu = std::min(n, 8);
+    per_cu = std::min(n, 4 * kServeWavesPerSimd / S);
   }
   const int blocks = (s.blocks_per_cu > 0 ? std::min(per_cu, s.blocks_per_cu) : per_cu) *
                      cus_of_device();

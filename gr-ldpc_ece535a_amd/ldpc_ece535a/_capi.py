@@ -74,6 +74,7 @@ SIGNATURES = {
     "ldpc_set_waves_per_cu": (_i, [_vp, _i]),
     "ldpc_set_launch_mode": (_i, [_vp, _i]),
     "ldpc_set_schedule": (_i, [_vp, _i]),
+    "ldpc_set_frame_order": (_i, [_vp, _i]),
     "ldpc_synchronize": (_i, [_vp]),
 }
 
@@ -391,6 +392,10 @@ class Decoder:
     def set_schedule(self, mode):
         """0 auto, 1 one wave per frame, 2 one workgroup per frame."""
         _check(lib().ldpc_set_schedule(self._ctx, int(mode)), self._ctx)
+
+    def set_frame_order(self, order):
+        """0 queue order, 1 longest first (ascending sum |y| per 4096 frames)."""
+        _check(lib().ldpc_set_frame_order(self._ctx, int(order)), self._ctx)
 
     def synchronize(self):
         _check(lib().ldpc_synchronize(self._ctx), self._ctx)

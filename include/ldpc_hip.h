@@ -328,6 +328,17 @@ int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode);
  * 89 us), else 1.  Results are identical across schedules. */
 int ldpc_set_schedule(ldpc_ctx *ctx, int schedule);
 
+/* Tuning: frame order of small-code min-sum / sum-product decodes of
+ * device-resident frames (ldpc_decode_device, ldpc_decode).  0 (default):
+ * frames start in index order.  1: longest first -- a short kernel ahead of
+ * each launch sorts groups of 256 frames by ascending sum |y| and interleaves
+ * them rank by rank (the least reliable frames, which tend to need the most
+ * iterations, start first; DESIGN section 6 has the measured A/B).  Results
+ * are identical. */
+#define LDPC_ORDER_QUEUE 0
+#define LDPC_ORDER_LONGEST_FIRST 1
+int ldpc_set_frame_order(ldpc_ctx *ctx, int order);
+
 /* Large-code path: device workspace cap in bytes (0 = default 8 GiB).  A
  * batch larger than the cap allows is decoded in consecutive groups. */
 int ldpc_set_work_limit(ldpc_ctx *ctx, int64_t bytes);

@@ -12,7 +12,7 @@ from ldpc_ece535a import flowgraph as fg
 pytestmark = pytest.mark.gpu
 
 
-PATHS = {"serve": {}, "launch": {"LDPC_BLOCK_SERVE": "0"},
+PATHS = {"serve": {}, "launch": {"LDPC_BLOCK_SERVE": "0"}, "serve-all": {"LDPC_BLOCK_SERVE": "1"},
          # the planner's A/B knobs: short dry runs, one search per round
          "plan": {"LDPC_BLOCK_MAXWANT": "64", "LDPC_BLOCK_SEARCHES": "1"},
          # every diagnostic knob on: stderr lines only, the same bytes
@@ -21,9 +21,9 @@ PATHS = {"serve": {}, "launch": {"LDPC_BLOCK_SERVE": "0"},
 
 
 def _block(method, path, **kw):
-    """The block with its rounds through the window server (default), a
-    launch per round (LDPC_BLOCK_SERVE=0), another dry-run plan, or every
-    diagnostic on."""
+    """The block with its small rounds through the window server and big ones
+    by launch (default), a launch per round (LDPC_BLOCK_SERVE=0), the server
+    for every round (=1), another dry-run plan, or every diagnostic on."""
     import os
     env = PATHS[path]
     os.environ.update(env)
@@ -66,9 +66,12 @@ def test_qa_loopback_default_h(method):
     assert dec.state == L.STATE_IN_SYNC
 
 
+@pytest.mark.parametrize("iters", [5, 50])
 @pytest.mark.parametrize("path", sorted(PATHS))
-def test_gpu_block_long_random_stream(golden, path):
-    """A longer mixed stream: results equal the restated general_work."""
+def test_gpu_block_long_random_stream(golden, path, iters):
+    """A longer mixed stream: results equal the restated general_work.  At
+    50 iterations the default path decodes its first, big rounds by launch
+    and the small ones after them through the window server."""
     import sys
     from oracle import oracle as orc
     Hr = golden("frames_default.npz")["H_reordered"]
@@ -79,9 +82,10 @@ def test_gpu_block_long_random_stream(golden, path):
     s = np.concatenate([rng.standard_normal(29).astype(np.float32), x[:150].ravel(),
                         rng.standard_normal(64 * 13).astype(np.float32), -x[150:].ravel()])
     s = s.astype(np.complex64)
-    exp = orc.run_stream(1, Hr, s, iterations=5)
-    blk = _block(1, path)
-    tb = fg.top_block(chunk=1000, out_space=64)
+    exp = orc.run_stream(1, Hr, s, iterations=iters)
+    blk = _block(1, path, iterations=iters)
+    tb = fg.top_block(chunk=[1000, 20000] if iters == 50 else 1000,
+                      out_space=4096 if iters == 50 else 64)
     src, dst = fg.vector_source_c(s), fg.vector_sink_b()
     tb.connect(src, blk, dst)
     tb.run()
