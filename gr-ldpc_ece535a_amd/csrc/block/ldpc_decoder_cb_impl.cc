@@ -281,10 +281,10 @@ ldpc_decoder_cb_impl::~ldpc_decoder_cb_impl() {
   }
   if (d_profile)
     fprintf(stderr,
-            "ldpc_decoder_cb profile: %lld launches; general_work %.3f ms = exact replay %.3f + "
-            "dry runs %.3f + decode launches %.3f (GPU round trips) + rest\n",
+            "ldpc_decoder_cb profile: %lld rounds; general_work %.3f ms = exact replay %.3f + "
+            "dry runs %.3f + staging wait %.3f + first rounds %.3f + other rounds %.3f + rest\n",
             (long long)d_launches, 1e3 * d_prof[0], 1e3 * d_prof[1], 1e3 * d_prof[2],
-            1e3 * d_prof[3]);
+            1e3 * d_prof[3], 1e3 * d_prof[4], 1e3 * d_prof[5]);
   ldpc_destroy(d_ctx);
 }
 
@@ -667,10 +667,15 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
       t0 = t1;
     }
     join_stage();  // the span is on its way to the device before the launch
-    decode_wanted(in, nin, first && !staged, first);
     if (d_profile) {
       const double t1 = now_s();
       d_prof[3] += t1 - t0;
+      t0 = t1;
+    }
+    decode_wanted(in, nin, first && !staged, first);
+    if (d_profile) {
+      const double t1 = now_s();
+      d_prof[first ? 4 : 5] += t1 - t0;
       t0 = t1;
     }
     first = false;
@@ -679,12 +684,14 @@ int ldpc_decoder_cb_impl::general_work(int noutput_items, gr_vector_int &ninput_
     d_prof[1] += now_s() - t0;
     d_prof[0] += now_s() - t_call;
     if (d_profile_calls) {  // a line per call
-      static double last[4] = {0, 0, 0, 0};
+      static double last[6] = {0, 0, 0, 0, 0, 0};
       fprintf(stderr,
-              "general_work call: %.1f us = replay %.1f + dry runs %.1f + decode launches %.1f\n",
+              "general_work call: %.1f us = replay %.1f + dry runs %.1f + staging wait %.1f + "
+              "first round %.1f + other rounds %.1f\n",
               1e6 * (d_prof[0] - last[0]), 1e6 * (d_prof[1] - last[1]),
-              1e6 * (d_prof[2] - last[2]), 1e6 * (d_prof[3] - last[3]));
-      for (int i = 0; i < 4; ++i) last[i] = d_prof[i];
+              1e6 * (d_prof[2] - last[2]), 1e6 * (d_prof[3] - last[3]),
+              1e6 * (d_prof[4] - last[4]), 1e6 * (d_prof[5] - last[5]));
+      for (int i = 0; i < 6; ++i) last[i] = d_prof[i];
     }
   }
   std::cout.flush();

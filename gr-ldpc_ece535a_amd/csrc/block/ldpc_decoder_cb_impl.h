@@ -91,7 +91,9 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
   // (=2: also a line per call)
   bool d_profile = getenv("LDPC_BLOCK_PROFILE") != nullptr;
   bool d_profile_calls = d_profile && getenv("LDPC_BLOCK_PROFILE")[0] == '2';
-  double d_prof[4] = {0, 0, 0, 0};  // total, exact replay, dry runs, decode rounds
+  // total, exact replay, dry runs, waiting for the span's staging, the
+  // call's first round, the other rounds
+  double d_prof[6] = {0, 0, 0, 0, 0, 0};
   static double now_s();
   // In-sync frames guessed to pass are also wanted at the other polarity
   // when more than 1 in 4 frames on the grid fail (then sync losses, and

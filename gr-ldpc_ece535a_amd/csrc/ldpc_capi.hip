@@ -11,9 +11,14 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <exception>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ldpc_hip.h"
@@ -26,6 +31,66 @@ using ldpc::ColRec;
 using ldpc::EdgeColRec;
 using ldpc::EdgeRowRec;
 using ldpc::kNone;
+
+// Host threads that gather a span's samples into pinned memory (copy_span):
+// the block's spans are gr_complex, and taking the real parts of 4096 frames
+// (2 MB read) on one thread is ~100-180 us in front of the call's first round.
+// Pieces are handed out by an atomic counter; the calling thread gathers too
+// and sends each piece to the device, in order, once it is ready.
+struct GatherPool {
+  static constexpr int kThreads = 3;      // helpers (plus the calling thread)
+  static constexpr int64_t kPiece = 1 << 14;  // samples per piece gathered
+  // samples per copy to the device: a copy costs ~8 us of its own (64 KB
+  // copies, one per gathered piece, took 16 x 15.6 us for a 1 MB span,
+  // profiles/round5/block_trace.txt)
+  static constexpr int64_t kCopy = 1 << 18;
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t gen = 0;
+  bool quit = false;
+  const float *in = nullptr;
+  float *h = nullptr;
+  int64_t S = 0, npieces = 0;
+  int stride = 1;
+  std::atomic<int64_t> next{0};
+  std::unique_ptr<std::atomic<uint64_t>[]> ready;
+  int64_t ready_cap = 0;
+  void gather(int64_t p) const {
+    const int64_t i0 = p * kPiece, i1 = std::min(S, i0 + kPiece);
+    if (stride == 1)
+      memcpy(h + i0, in + i0, (size_t)(i1 - i0) * 4);
+    else if (stride == 2)  // gr_complex real parts: a constant stride vectorises
+      for (int64_t i = i0; i < i1; ++i) h[i] = in[2 * i];
+    else
+      for (int64_t i = i0; i < i1; ++i) h[i] = in[i * stride];
+  }
+  void worker() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return quit || gen != seen; });
+        if (quit) return;
+        seen = gen;
+      }
+      for (;;) {
+        const int64_t p = next.fetch_add(1);
+        if (p >= npieces) break;
+        gather(p);
+        ready[p].store(seen, std::memory_order_release);
+      }
+    }
+  }
+  ~GatherPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      quit = true;
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+  }
+};
 
 struct ldpc_ctx {
   // LDPC_WIN_PROFILE=1: host time split of ldpc_decode_windows, printed by
@@ -50,6 +115,7 @@ struct ldpc_ctx {
   void *d_stage = nullptr;
   size_t stage_bytes = 0;
   float *h_stage = nullptr;  // pinned host staging of host-buffer decodes
+  std::unique_ptr<GatherPool> gather;  // copy_span's helpers (made on first use)
   size_t h_stage_bytes = 0;
   bool h_stage_busy = false;  // a copy out of h_stage may still be running (ldpc_stage_span)
   int32_t *h_ctrl = nullptr;  // pinned progress words of the min-sum pipeline
@@ -72,7 +138,10 @@ struct ldpc_ctx {
   int srv_method = 0, srv_iters = 0, srv_prec = 0;
   int srv_launches = 0, srv_rounds = 0;
   int srv_workgroups = 0;  // decoder workgroups of the running launch
-  double dbg[4] = {0, 0, 0, 0};  // LDPC_SERVE_DEBUG: rounds, host us, key-read us, done us
+  // LDPC_SERVE_DEBUG: rounds, host us, poller's sight -> publication, ->
+  // last key read, -> last result stored (us)
+  double dbg[6] = {0, 0, 0, 0, 0, 0};  // ... and the host's sight of the first result
+  bool srv_debug = getenv("LDPC_SERVE_DEBUG") != nullptr;
   // in-flight stream set for throughput callers (ldpc_ctx_streams): streams
   // verified to run concurrently, i.e. on distinct hardware queues
   std::vector<hipStream_t> tp_streams;
@@ -1369,8 +1438,55 @@ int copy_span(ldpc_ctx *ctx, const float *in, int64_t S, int elem_stride, float 
   int rc = ensure_host_stage(ctx, (size_t)S * 4);
   if (rc != LDPC_OK) return rc;
   float *h = ctx->h_stage;
+  if (S >= ((int64_t)1 << 17)) {
+    // big spans: gathered by the pool, each piece sent once ready
+    if (!ctx->gather) {
+      ctx->gather.reset(new GatherPool);
+      for (int t = 0; t < GatherPool::kThreads; ++t)
+        ctx->gather->th.emplace_back([g = ctx->gather.get()] { g->worker(); });
+    }
+    GatherPool &g = *ctx->gather;
+    const int64_t np = (S + GatherPool::kPiece - 1) / GatherPool::kPiece;
+    uint64_t gen;
+    {
+      std::lock_guard<std::mutex> lk(g.mu);
+      if (g.ready_cap < np) {
+        g.ready.reset(new std::atomic<uint64_t>[np]);
+        for (int64_t p = 0; p < np; ++p) g.ready[p].store(0);
+        g.ready_cap = np;
+      }
+      g.in = in;
+      g.h = h;
+      g.S = S;
+      g.stride = elem_stride;
+      g.npieces = np;
+      g.next.store(0);
+      gen = ++g.gen;
+    }
+    g.cv.notify_all();
+    constexpr int64_t per_copy = GatherPool::kCopy / GatherPool::kPiece;
+    for (int64_t p = 0; p < np; ++p) {
+      while (g.ready[p].load(std::memory_order_acquire) != gen) {
+        const int64_t q = g.next.fetch_add(1);  // help while waiting
+        if (q < np) {
+          g.gather(q);
+          g.ready[q].store(gen, std::memory_order_release);
+        } else {
+          std::this_thread::yield();
+        }
+      }
+      if ((p + 1) % per_copy != 0 && p + 1 != np) continue;
+      const int64_t i0 = (p / per_copy) * GatherPool::kCopy, n = std::min(S - i0, GatherPool::kCopy);
+      hipError_t e = hipMemcpyAsync(d_span + i0, h + i0, (size_t)n * 4, hipMemcpyHostToDevice,
+                                    ctx->stream);
+      if (e != hipSuccess) return hip_err(ctx, e, "hipMemcpyAsync(span)");
+    }
+    ctx->h_stage_busy = true;
+    ctx->span_samples = S;
+    return LDPC_OK;
+  }
   // in pieces: each piece's copy to the device runs while the next is gathered
-  const int64_t piece = S >= ((int64_t)1 << 17) ? ((int64_t)1 << 15) : S;
+  const int64_t piece = S;
   for (int64_t i0 = 0; i0 < S; i0 += piece) {
     const int64_t i1 = std::min(S, i0 + piece);
     if (elem_stride == 1)
@@ -1632,8 +1748,10 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
     ctx->srv_rounds += 1;
     const uint32_t tag = ctx->srv_epoch & 0x7FFFFFu;
     const auto t0 = std::chrono::steady_clock::now();
+    auto t_first = t0;
     int relaunches = 0;
     for (int b = 0; b < n; ++b) {
+      if (b == 1 && ctx->srv_debug) t_first = std::chrono::steady_clock::now();
       uint64_t g;
       for (uint32_t spins = 1;; ++spins) {
         g = __atomic_load_n(res + b, __ATOMIC_ACQUIRE);
@@ -1687,15 +1805,21 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
     if (getenv("LDPC_SERVE_DEBUG")) {  // device-side split of the round (100 MHz ticks)
       const double host_us =
           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6;
-      uint64_t c[8] = {0};
+      const double first_us = std::chrono::duration<double>(t_first - t0).count() * 1e6;
+      uint64_t c[9] = {0};
       uint64_t *dg = ctx->d_srv_ctl + 16 * (ldpc::kServeCopies + 1);
       (void)hipMemcpy(c, dg, sizeof c, hipMemcpyDeviceToHost);
       const uint64_t zero[2] = {0, 0};
       (void)hipMemcpy(dg + 6, zero, sizeof zero, hipMemcpyHostToDevice);
-      ctx->dbg[0] += 1;
-      ctx->dbg[1] += host_us;
-      ctx->dbg[2] += 1e-2 * (double)c[6];
-      ctx->dbg[3] += 1e-2 * (double)c[7];
+      // (only the one-wave form of big rounds does not time its decoders)
+      if (c[6] >= c[5] && c[7] >= c[5] && c[5] >= c[8]) {
+        ctx->dbg[0] += 1;
+        ctx->dbg[1] += host_us;
+        ctx->dbg[2] += 1e-2 * (double)(c[5] - c[8]);
+        ctx->dbg[3] += 1e-2 * (double)(c[6] - c[5]);
+        ctx->dbg[4] += 1e-2 * (double)(c[7] - c[5]);
+        ctx->dbg[5] += n > 1 ? first_us : host_us;
+      }
     }
   }
   return LDPC_OK;
@@ -1736,10 +1860,11 @@ int ldpc_serve_end(ldpc_ctx *ctx) {
   if (!ctx) return LDPC_EINVAL;
   if (getenv("LDPC_SERVE_DEBUG") && ctx->dbg[0] > 0) {
     fprintf(stderr,
-            "ldpc_serve: %.0f rounds: host %.1f us per round; from the poller's publication: "
-            "last key read %.1f us, last result stored %.1f us (mean over rounds)\n",
+            "ldpc_serve: %.0f rounds: host %.1f us per round; poller: sight to publication %.1f "
+            "us; from the publication: last key read %.1f us, last result stored %.1f us; host: "
+            "first result seen %.1f us after the post (mean over rounds)\n",
             ctx->dbg[0], ctx->dbg[1] / ctx->dbg[0], ctx->dbg[2] / ctx->dbg[0],
-            ctx->dbg[3] / ctx->dbg[0]);
+            ctx->dbg[3] / ctx->dbg[0], ctx->dbg[4] / ctx->dbg[0], ctx->dbg[5] / ctx->dbg[0]);
     for (double &d : ctx->dbg) d = 0;
   }
   if (ctx->serving) {  // the launch finishes on its own; the stream orders what follows

@@ -65,11 +65,26 @@ __device__ __forceinline__ uint64_t ctl_word(uint32_t ep, uint32_t live, uint32_
   return ((uint64_t)ep << 40) | ((uint64_t)(live & 0xFFFFFu) << 20) | (B & 0xFFFFFu);
 }
 __device__ __forceinline__ uint64_t *ctl_copy(uint64_t *ctl, int i) { return ctl + 16 * i; }
+// Where window b's key is published: keys of the first kInlineKeys windows
+// ride in the round copies' lines (word 1 + b / 32 of copy b % 32, the line
+// decoder b polls, so its poll fetches its key too), the others in dkeys.
+// Keys keep the host's epoch tag (bits 40..63): a reader that finds an older
+// tag reads again, so no key store has to be ordered before the round word.
+constexpr int64_t kInlineKeys = 15 * kServeCopies;
+__device__ __forceinline__ uint64_t *key_slot(const ServeArgs &s, int64_t b) {
+  return b < kInlineKeys ? s.ctl + 16 * (b % kServeCopies) + 1 + b / kServeCopies
+                         : (uint64_t *)s.dkeys + b;
+}
 __device__ __forceinline__ uint32_t *census_word(uint64_t *ctl) {
   return reinterpret_cast<uint32_t *>(ctl + 16 * kServeCopies);
 }
 __device__ __forceinline__ uint64_t *diag(uint64_t *ctl, int j) { return ctl + 16 * (kServeCopies + 1) + j; }
-enum { kDiagExit, kDiagExitRound, kDiagStarts, kDiagG0, kDiagResults, kDiagPub, kDiagKey, kDiagDone };
+// LDPC_SERVE_DEBUG counters; the times are absolute 100 MHz ticks: the
+// poller's sight of the round and its publication, the last decoder's key
+// read and result store (the host reads them after the round and zeroes the
+// last two)
+enum { kDiagExit, kDiagExitRound, kDiagStarts, kDiagG0, kDiagResults, kDiagPub, kDiagKey, kDiagDone,
+       kDiagSeen };
 __device__ __forceinline__ uint32_t census_load(uint64_t *ctl) {
   return __hip_atomic_load((const __attribute__((address_space(1))) uint32_t *)census_word(ctl),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -98,20 +113,21 @@ __device__ __forceinline__ uint64_t wave_uniform(uint64_t v) {
 // The poller (wave 0 of workgroup 0): lane 0 reads the round word, lanes
 // 1..63 the first 63 key slots in the same instruction (host memory, one PCIe
 // round trip); a new round's keys -- each tagged with its epoch by the host,
-// so a slot read before the host rewrote it is read again -- go to device
-// memory (dkeys, agent-scope stores), then, behind the wave's vmcnt(0), the
-// round word to the ctl copies.
+// so a slot read before the host rewrote it is read again -- go to their
+// key_slot (agent-scope stores, tags kept), and the round word to the ctl
+// copies right behind them.
 constexpr int kKeyLoads = 8;
 __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
   uint32_t last = s.start_epoch;
   const uint64_t t_start = ticks();
   uint64_t t_last = t_start;
-  const uint64_t kKeyMask = (1ull << 40) - 1;
+  uint32_t live = 0;  // decoders counted by the census
   for (;;) {
     const uint64_t v = sys_load(lane == 0 ? s.round : (const uint64_t *)s.keys + (lane - 1));
     const uint64_t r = lane_bcast(v, 0);
     const uint32_t ep = (uint32_t)(r >> 32);
     if (ep != last) {
+      const uint64_t t_seen = ticks();
       // a round of a later launch (this launch's quit round was overwritten
       // before it was seen) ends this launch too
       const bool quit = ((uint32_t)r & kServeB) == kServeB ||
@@ -139,30 +155,33 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
             if (in[j] && (k[j] >> 40) != tag) k[j] = sys_load((const uint64_t *)s.keys + b);
             if (ticks() - t_keys > s.deadline) lost = true;
           }
-          if (in[j]) agent_store((uint64_t *)s.dkeys + b, k[j] & kKeyMask);
+          if (in[j]) agent_store(key_slot(s, b), k[j]);
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lost) {
         if (lane < kServeCopies) agent_store(ctl_copy(s.ctl, lane), kQuitRound);
         if (lane == 0) agent_store(diag(s.ctl, kDiagExit), 3);
         return;
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // the decoders that have started by now share the round: all of them
       // (every workgroup is resident) or, if some never start while this
       // launch runs, those counted 20 us after the launch began -- at least
-      // one
-      uint32_t live = census_load(s.ctl);
-      while (!quit && live < gridDim.x - 1 && (live == 0 || ticks() - t_start < 2000)) {
-        __builtin_amdgcn_s_sleep(2);
+      // one.  Once all have started the count is not read again.
+      if (live < gridDim.x - 1) {
         live = census_load(s.ctl);
-        if (ticks() - t_start > s.deadline) break;  // (no decoder at all: give up below)
+        while (!quit && live < gridDim.x - 1 && (live == 0 || ticks() - t_start < 2000)) {
+          __builtin_amdgcn_s_sleep(2);
+          live = census_load(s.ctl);
+          if (ticks() - t_start > s.deadline) break;  // (no decoder at all: give up below)
+        }
+        live = (uint32_t)__builtin_amdgcn_readfirstlane((int)live);
       }
-      live = (uint32_t)__builtin_amdgcn_readfirstlane((int)live);
       const uint64_t w = quit ? kQuitRound : ctl_word(ep, live, (uint32_t)B);
       if (lane < kServeCopies) agent_store(ctl_copy(s.ctl, lane), w);
-      if (s.debug && lane == 0) agent_store(diag(s.ctl, kDiagPub), ticks());
+      if (s.debug && lane == 0) {
+        agent_store(diag(s.ctl, kDiagSeen), t_seen);
+        agent_store(diag(s.ctl, kDiagPub), ticks());
+      }
       last = ep;
       t_last = ticks();
       if (quit) {  // diagnostics: why, and the round word seen
@@ -196,6 +215,7 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
 // (profiles/round5/serve_latency.txt).  Big rounds go to launches instead
 // (the block's hybrid, ldpc_decoder_cb_impl.h).
 constexpr int kServeWavesPerSimd = 3;
+constexpr int64_t kFastPollers = 256;
 // bytes of the two forms' overlaid frame regions
 template <typename Real, int METHOD, int S, int NW, int DVN>
 __host__ __device__ size_t serve_lds_main() {
@@ -233,20 +253,42 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
   __syncthreads();
   const int64_t g = sslot[1];  // this decoder's place among those that started
   const uint64_t *poll = ctl_copy(s.ctl, (int)(g % kServeCopies));
+  const uint64_t *my_key = key_slot(s, g);
   // epochs only grow (ctl is zeroed before the launch, below start_epoch)
   uint32_t last = s.start_epoch;
   uint64_t idle = ticks();
   for (;;) {
-    if (tid == 0) {  // the next round
-      uint64_t r;
+    if (tid == 0) {  // the next round, and this decoder's key with it
+      uint64_t r, k = 0;
       for (int spins = 0;; ++spins) {
         r = agent_load(poll);
+        k = agent_load(my_key);
         if ((uint32_t)(r >> 40) > last) break;
         if ((spins & 15) == 15 && ticks() - idle > s.deadline) {
           r = kQuitRound;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        // Decoders past the first kFastPollers poll ~30x less often: a
+        // thousand decoders polling the round copies back to back delayed
+        // the round's sight by ~10 us; rounds that need them are big
+        // anyway.
+        if (g < kFastPollers)
+          __builtin_amdgcn_s_sleep(6);
+        else
+          __builtin_amdgcn_s_sleep(120);
+      }
+      // the workgroup form's key: tagged with the round's epoch (see key_slot)
+      if (r != kQuitRound && g < (int64_t)(r & 0xFFFFFu) && (int64_t)(r & 0xFFFFFu) <= (int64_t)((r >> 20) & 0xFFFFFu)) {
+        const uint64_t ktag = (r >> 40) & 0xFFFFFFu;
+        const uint64_t t_k = ticks();
+        while ((k >> 40) != ktag) {
+          if (ticks() - t_k > s.deadline) {  // the host is gone
+            r = kQuitRound;
+            break;
+          }
+          k = agent_load(my_key);
+        }
+        sslot[1] = (int64_t)(k & ((1ull << 40) - 1));
       }
       sslot[0] = (int64_t)r;
     }
@@ -256,7 +298,7 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
     const uint32_t ep = (uint32_t)(r >> 40), B = (uint32_t)r & 0xFFFFFu;
     const int64_t G = (int64_t)((r >> 20) & 0xFFFFFu);
     const uint64_t tag = (uint64_t)((ep & 0x7FFFFFu) << 9) << 32;
-    if (s.debug && tid == 0) {  // diagnostics: rounds seen by decoders
+    if (s.debug && tid == 0 && (g & 63) == 0) {  // diagnostics: rounds seen (sampled decoders)
       dbg_add(diag(s.ctl, kDiagStarts));
       if (g == 0) agent_store(diag(s.ctl, kDiagG0), r);
     }
@@ -264,9 +306,10 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
       // one window per workgroup
       if (g < (int64_t)B) {
         if (tid == 0) {
-          sslot[1] = (int64_t)agent_load((const uint64_t *)s.dkeys + g);
           mtb[kDummy] = METHOD == 1 ? Real(1) : Math<PREC>::max_();  // (the LDS is shared)
-          if (s.debug) dbg_max(diag(s.ctl, kDiagKey), ticks() - agent_load(diag(s.ctl, kDiagPub)));
+          // (sampled: one decoder in 64, so the counters' atomics do not
+          // queue behind each other and time themselves)
+          if (s.debug && (g & 63) == 0) dbg_max(diag(s.ctl, kDiagKey), ticks());
         }
         __syncthreads();  // (mw_frame's first barrier orders the key's readers)
         const int64_t key = sslot[1];
@@ -286,9 +329,9 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
             pk |= ((uint32_t)__builtin_amdgcn_readlane((int)o, j) & 255u) << (8 * j);
           if (lane == 0) {
             sys_store(s.res + g, tag | ((uint64_t)(uint32_t)weight << 32) | pk);
-            if (s.debug) {
+            if (s.debug && (g & 63) == 0) {
               dbg_add(diag(s.ctl, kDiagResults));
-              dbg_max(diag(s.ctl, kDiagDone), ticks() - agent_load(diag(s.ctl, kDiagPub)));
+              dbg_max(diag(s.ctl, kDiagDone), ticks());
             }
           }
         }
@@ -298,7 +341,13 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
       // one window per wave
       const int64_t W = G * S;
       for (int64_t b = g * S + wave; b < (int64_t)B && g < G; b += W) {
-        const int64_t key = (int64_t)wave_uniform(agent_load((const uint64_t *)s.dkeys + b));
+        // the key, once it carries this round's tag (bounded: a host that is
+        // gone leaves a stale key, decoded into a result nobody reads)
+        uint64_t kk = wave_uniform(agent_load(key_slot(s, b)));
+        const uint64_t t_k = ticks();
+        while ((kk >> 40) != (ep & 0xFFFFFFu) && ticks() - t_k < s.deadline)
+          kk = wave_uniform(agent_load(key_slot(s, b)));
+        const int64_t key = (int64_t)(kk & ((1ull << 40) - 1));
         const float *src = a.in + (key >> 1);
         const float sgn = (key & 1) ? -1.0f : 1.0f;
         float xin[NW];
