@@ -1933,6 +1933,39 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
   // the set is complete (so the next candidate lands elsewhere), then freed.
   std::vector<hipStream_t> spare;
   int rc = LDPC_OK;
+  auto concurrent = [&](hipStream_t a, hipStream_t c, bool &ok) {
+    uint32_t seen = 0;
+    if ((e = hipMemset(ctx->d_probe, 0, 8)) != hipSuccess ||
+        ldpc::launch_probe_pair(ctx->d_probe, 200000 /* 2 ms */, a, c) != 0 ||
+        (e = hipStreamSynchronize(a)) != hipSuccess || (e = hipStreamSynchronize(c)) != hipSuccess ||
+        (e = hipMemcpy(&seen, ctx->d_probe + 1, 4, hipMemcpyDeviceToHost)) != hipSuccess)
+      return hip_err(ctx, e, "stream probe");
+    ok = seen == 1u;
+    return LDPC_OK;
+  };
+  // First the plain way: n streams made back to back (measured the fastest
+  // set, profiles/round5/stream_sets.txt), kept if every pair runs at once.
+  if (ctx->tp_streams.empty()) {
+    std::vector<hipStream_t> batch;
+    bool all = true;
+    for (int i = 0; i < n && rc == LDPC_OK; ++i) {
+      hipStream_t c = nullptr;
+      if ((e = hipStreamCreateWithFlags(&c, hipStreamNonBlocking)) != hipSuccess) {
+        rc = hip_err(ctx, e, "hipStreamCreate");
+        break;
+      }
+      batch.push_back(c);
+    }
+    for (size_t i = 0; i < batch.size() && all && rc == LDPC_OK; ++i)
+      for (size_t j = i + 1; j < batch.size() && all && rc == LDPC_OK; ++j)
+        rc = concurrent(batch[i], batch[j], all);
+    if (rc == LDPC_OK && all && (int)batch.size() == n)
+      ctx->tp_streams = batch;
+    else
+      for (hipStream_t t : batch) (void)hipStreamDestroy(t);
+    if (rc != LDPC_OK) return rc;
+  }
+  // Otherwise one candidate at a time.
   // (more streams than the process has hardware queues cannot all be
   // concurrent: after a few candidates the set's streams are handed out again)
   for (int tries = 0; (int)ctx->tp_streams.size() < n && tries < 3 * n; ++tries) {
@@ -1943,16 +1976,8 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
     }
     bool ok = true;
     for (hipStream_t a : ctx->tp_streams) {
-      uint32_t seen = 0;
-      if ((e = hipMemset(ctx->d_probe, 0, 8)) != hipSuccess ||
-          ldpc::launch_probe_pair(ctx->d_probe, 200000 /* 2 ms */, a, c) != 0 ||
-          (e = hipStreamSynchronize(a)) != hipSuccess || (e = hipStreamSynchronize(c)) != hipSuccess ||
-          (e = hipMemcpy(&seen, ctx->d_probe + 1, 4, hipMemcpyDeviceToHost)) != hipSuccess) {
-        rc = hip_err(ctx, e, "stream probe");
-        ok = false;
-        break;
-      }
-      if (seen != 1u) {
+      rc = concurrent(a, c, ok);
+      if (rc != LDPC_OK || !ok) {
         ok = false;
         break;
       }

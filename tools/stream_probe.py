@@ -5,6 +5,8 @@ several ways of making its four streams, in one process.
   python tools/stream_probe.py [--steps K] [--patterns torch:0,torch:3,hip:0,...]
 
 torch:k  k throw-away torch.cuda.Stream() objects, then the four streams
+prioP:k  k throw-away raw streams, then four made with hipStreamCreateWithPriority(P)
+         (P: 0, 1, m1 for -1)
 hip:k    k throw-away hipStreamCreateWithFlags streams, then four raw HIP
          streams (wrapped as torch.cuda.ExternalStream for the events)
 ctx:k    k throw-away torch streams, then a new decoder context's own in-flight
@@ -56,6 +58,26 @@ def main():
             streams = [torch.cuda.Stream(dev) for _ in range(4)]
         elif kind == "hip":
             keep += [raw_stream() for _ in range(k)]
+            streams = [torch.cuda.ExternalStream(raw_stream(), device=dev) for _ in range(4)]
+        elif kind.startswith("prio"):  # prioP:k raw streams made with hipStreamCreateWithPriority
+            prio = int(kind[4:].replace("m", "-"))
+
+            def prio_stream():
+                h = ctypes.c_void_p()
+                rc = hip.hipStreamCreateWithPriority(ctypes.byref(h), ctypes.c_uint(1), ctypes.c_int(prio))
+                assert rc == 0, rc
+                return h.value
+            keep += [prio_stream() for _ in range(k)]
+            streams = [torch.cuda.ExternalStream(prio_stream(), device=dev) for _ in range(4)]
+        elif kind == "own":  # the measuring context's own in-flight set
+            keep += [torch.cuda.Stream(dev) for _ in range(k)]
+            streams = [torch.cuda.ExternalStream(h, device=dev) for h in dec.streams(4)]
+        elif kind == "newhip":  # a new context, raw HIP streams
+            keep += [raw_stream() for _ in range(k)]
+            d2 = L.Decoder(device=0)
+            d2.set_launch_mode(1)
+            keep.append(d2)
+            dd = d2
             streams = [torch.cuda.ExternalStream(raw_stream(), device=dev) for _ in range(4)]
         elif kind == "ctx":
             keep += [torch.cuda.Stream(dev) for _ in range(k)]
