@@ -294,12 +294,20 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
              torch.empty(B, dtype=torch.int32, device=dev),
              torch.empty(B, dtype=torch.int32, device=dev)) for _ in range(D)]
 
+    # at most two launches queued per stream: the host waits for step k - 2D
+    # before it enqueues step k (a pipeline's depth, not an unbounded backlog
+    # of hundreds of launches)
+    done_ev = [torch.cuda.Event() for _ in range(2 * D)]
+
     def step(k):
         d = k % D
+        if k >= 2 * D:
+            done_ev[k % (2 * D)].synchronize()
         pk, it, sy = outs[d]
         dec.decode_device(inputs[d % len(inputs)].data_ptr(), B, pk.data_ptr(), method=method,
                           max_iters=iters, et_period=et, precision=prec, d_iters=it.data_ptr(),
                           d_synd=sy.data_ptr(), stream=sps[d])
+        done_ev[k % (2 * D)].record(streams[d])
 
     e0 = torch.cuda.Event(enable_timing=True)
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(D)]
