@@ -110,8 +110,8 @@ __device__ __forceinline__ uint64_t wave_uniform(uint64_t v) {
          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
 }
 
-// The poller (wave 0 of workgroup 0): lane 0 reads the round word, lanes
-// 1..63 the first 63 key slots in the same instruction (host memory, one PCIe
+// The poller (wave 0 of workgroup 0): lane 0 reads the round word, the other
+// loads of the same poll the first 511 key slots (host memory, one PCIe
 // round trip); a new round's keys -- each tagged with its epoch by the host,
 // so a slot read before the host rewrote it is read again -- go to their
 // key_slot (agent-scope stores, tags kept), and the round word to the ctl
@@ -123,8 +123,15 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
   uint64_t t_last = t_start;
   uint32_t live = 0;  // decoders counted by the census
   for (;;) {
-    const uint64_t v = sys_load(lane == 0 ? s.round : (const uint64_t *)s.keys + (lane - 1));
-    const uint64_t r = lane_bcast(v, 0);
+    // every poll also reads the first 64 kKeyLoads - 1 key slots (the same
+    // PCIe round trip), so a round of up to 511 windows needs no second trip:
+    // -0.5..-1.3 us per round of 64..400 windows, +1..2 % on the block at
+    // 4 dB / 5 iterations (profiles/round5/serve_preload_ab.txt)
+    uint64_t v[kKeyLoads];
+#pragma unroll
+    for (int j = 0; j < kKeyLoads; ++j)
+      v[j] = sys_load(j == 0 && lane == 0 ? s.round : (const uint64_t *)s.keys + (64 * j + lane - 1));
+    const uint64_t r = lane_bcast(v[0], 0);
     const uint32_t ep = (uint32_t)(r >> 32);
     if (ep != last) {
       const uint64_t t_seen = ticks();
@@ -136,9 +143,8 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
       const uint64_t tag = (uint64_t)(ep & 0xFFFFFFu);
       const uint64_t t_keys = ticks();
       bool lost = false;  // a key slot that never showed this epoch (the host is gone)
-      // key slot c + 64 j + lane; kKeyLoads loads in flight per lane, so a
-      // round of up to 64 kKeyLoads keys costs one PCIe round trip (the
-      // first slot group, c = -1 and j = 0, is the read above)
+      // key slot c + 64 j + lane; kKeyLoads loads in flight per lane (the
+      // first group, c = -1, is the poll's own read)
       for (int64_t c = -1; c < B && !lost; c += 64 * kKeyLoads) {
         uint64_t k[kKeyLoads];
         bool in[kKeyLoads];
@@ -146,7 +152,7 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
         for (int j = 0; j < kKeyLoads; ++j) {
           const int64_t b = c + 64 * j + lane;
           in[j] = b >= 0 && b < B;
-          k[j] = (c < 0 && j == 0) ? v : (in[j] ? sys_load((const uint64_t *)s.keys + b) : 0);
+          k[j] = c < 0 ? v[j] : (in[j] ? sys_load((const uint64_t *)s.keys + b) : 0);
         }
 #pragma unroll
         for (int j = 0; j < kKeyLoads; ++j) {
