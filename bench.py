@@ -281,9 +281,9 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
     """Decode `steps` batches with `inflight` batches in flight: step k
     decodes inputs[k % D] on stream k % D into that stream's output buffers.
     Returns dict(wall, span_ms, per_launch_ms, iters, outs) where span_ms is
-    the device time from the first launch's start (a HIP event on stream 0,
-    which the other streams wait for) to the last launch's end (one event per
-    stream) and per_launch_ms = span_ms / steps.  outs[d] = (packed, iters,
+    the device time from the first launch's start (a HIP event on the first
+    timed step's stream, which each other stream waits for before its first
+    launch) to the last launch's end (one event per stream) and per_launch_ms = span_ms / steps.  outs[d] = (packed, iters,
     synd) of the last decode of batch d."""
     D = max(1, inflight)
     dev = inputs[0].device
@@ -299,10 +299,17 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
     # of hundreds of launches)
     done_ev = [torch.cuda.Event() for _ in range(2 * D)]
 
+    poll = os.environ.get("LDPC_BENCH_WAIT", "sync") == "poll"
+
     def step(k):
         d = k % D
         if k >= 2 * D:
-            done_ev[k % (2 * D)].synchronize()
+            ev = done_ev[k % (2 * D)]
+            if poll:
+                while not ev.query():
+                    pass
+            else:
+                ev.synchronize()
         pk, it, sy = outs[d]
         dec.decode_device(inputs[d % len(inputs)].data_ptr(), B, pk.data_ptr(), method=method,
                           max_iters=iters, et_period=et, precision=prec, d_iters=it.data_ptr(),
@@ -314,11 +321,20 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
     sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
     marks = {}
 
+    # every event exists before the timed region (a torch event is created at
+    # its first record): no event creation inside the timed steps
+    for ev in done_ev + [e0] + ends:
+        ev.record(streams[0])
+
     def timed_step(k):
-        if k == warmup:  # first timed step: start event, every stream waits on it
-            e0.record(streams[0])
-            for s in streams[1:]:
-                s.wait_event(e0)
+        # first timed step: the start event on its stream; each other stream
+        # waits on it right before its own first launch, so the first launch
+        # is not queued behind the other streams' waits on the host
+        d = k % D
+        if k == warmup:
+            e0.record(streams[d])
+        elif k < warmup + D:
+            streams[d].wait_event(e0)
         step(k)
         if k == warmup + steps - 1:
             for s, e in zip(streams, ends):
@@ -328,7 +344,8 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
     wall = timed_steps(timed_step, steps, warmup, sync, dist)
     span = max(e0.elapsed_time(e) for e in ends) if marks else 0.0
     return dict(wall=wall, span_ms=span, per_launch_ms=span / max(1, steps),
-                iters=outs[0][1].cpu().numpy(), outs=outs)
+                iters=outs[0][1].cpu().numpy(), outs=outs,
+                streams_distinct=len(set(s.cuda_stream for s in streams)))
 
 
 # --------------------------------------------------------------------------
@@ -820,6 +837,9 @@ def main():
         dec.set_launch_mode(1 if D > 1 else 0)
         if args.waves_per_cu:
             dec.set_waves_per_cu(args.waves_per_cu)
+    # the in-flight stream set, made now: before the variants' contexts make
+    # and free streams of their own
+    ctx_streams(torch, dec, dev, D)
     # The variants (other methods / precisions, latency, the block, config 4)
     # are measured first, on every rank, so the headline's K steps run on a
     # GPU that has been busy for a while (its clock ramps from ~2.0 to
@@ -942,8 +962,10 @@ def main():
         line["hbm_byte_model"] = hbm_model
     line["timing"] = {"device_span_ms_per_launch": round(r["per_launch_ms"], 5),
                       "wall_ms_per_step": round(per_launch_ms, 5),
-                      "note": "span = HIP events: start on stream 0 (other streams wait on it) "
-                              "to the last stream's end, / K",
+                      "note": "span = HIP events: start on the first timed step's stream "
+                              "(each other stream waits on it before its first launch) to the "
+                              "last stream's end, / K",
+                      "streams_distinct": r.get("streams_distinct"),
                       "order": "measured after the GPU variants below (same process), so the "
                                "K steps see the GPU's steady clock; --no-variants times a "
                                "cold GPU"}

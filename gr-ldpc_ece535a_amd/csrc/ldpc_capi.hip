@@ -1866,6 +1866,9 @@ int ldpc_serve_end(ldpc_ctx *ctx) {
             ctx->dbg[0], ctx->dbg[1] / ctx->dbg[0], ctx->dbg[2] / ctx->dbg[0],
             ctx->dbg[3] / ctx->dbg[0], ctx->dbg[4] / ctx->dbg[0], ctx->dbg[5] / ctx->dbg[0]);
     for (double &d : ctx->dbg) d = 0;
+    uint32_t census = 0;
+    (void)hipMemcpy(&census, ctx->d_srv_ctl + 16 * ldpc::kServeCopies, 4, hipMemcpyDeviceToHost);
+    fprintf(stderr, "ldpc_serve: %u of %d decoder workgroups started\n", census, ctx->srv_workgroups);
   }
   if (ctx->serving) {  // the launch finishes on its own; the stream orders what follows
     serve_post(ctx, ldpc::kServeB);
@@ -1933,6 +1936,11 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
   // the set is complete (so the next candidate lands elsewhere), then freed.
   std::vector<hipStream_t> spare;
   int rc = LDPC_OK;
+  // the probes must see only each other: work still running on some queue
+  // (another context's launches) would hold a probe kernel back past its
+  // timeout and reject a stream whose queue is in fact distinct
+  if (ctx->tp_streams.size() < (size_t)n && (e = hipDeviceSynchronize()) != hipSuccess)
+    return hip_err(ctx, e, "hipDeviceSynchronize");
   auto concurrent = [&](hipStream_t a, hipStream_t c, bool &ok) {
     uint32_t seen = 0;
     if ((e = hipMemset(ctx->d_probe, 0, 8)) != hipSuccess ||

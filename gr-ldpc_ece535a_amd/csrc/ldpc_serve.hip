@@ -172,8 +172,10 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
       // the decoders that have started by now share the round: all of them
       // (every workgroup is resident) or, if some never start while this
       // launch runs, those counted 20 us after the launch began -- at least
-      // one.  Once all have started the count is not read again.
-      if (live < gridDim.x - 1) {
+      // one.  Once all have started the count is not read again, and after
+      // the first 20 us only for a round that wants more decoders than were
+      // counted (a census load is a trip to memory on the round's path).
+      if (live < gridDim.x - 1 && (live == 0 || B > (int64_t)live || ticks() - t_start < 2000)) {
         live = census_load(s.ctl);
         while (!quit && live < gridDim.x - 1 && (live == 0 || ticks() - t_start < 2000)) {
           __builtin_amdgcn_s_sleep(2);
