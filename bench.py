@@ -143,6 +143,17 @@ def ctx_streams(torch, dec, dev, n):
     return [torch.cuda.ExternalStream(h, device=dev) for h in dec.streams(n)]
 
 
+def stream_probe_matrix(torch, dec, dev, D):
+    """Diagnostics (LDPC_BENCH_PROBE=1, tools/probe_lib.cpp): for each ordered
+    pair of the in-flight streams, 1 if a launch on the second ran while one
+    on the first waited for it."""
+    if os.environ.get("LDPC_BENCH_PROBE") != "1":
+        return None
+    pl = ctypes.CDLL(os.path.join(REPO, "tools", "_probe_lib.so"))
+    hs = [ctypes.c_void_p(s.cuda_stream) for s in ctx_streams(torch, dec, dev, D)]
+    return "".join(str(pl.probe_pair(hs[i], hs[j], 0)) for i in range(D) for j in range(D) if i != j)
+
+
 def synth_device(L, torch, dec, B, ebn0, seed, dev, check_frames=64):
     """Frames made on the GPU: Philox bits -> ldpc_encode_device -> BPSK +
     AWGN.  ebn0 may be a scalar or a per-frame array (config 5).  Returns
@@ -299,17 +310,10 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
     # of hundreds of launches)
     done_ev = [torch.cuda.Event() for _ in range(2 * D)]
 
-    poll = os.environ.get("LDPC_BENCH_WAIT", "sync") == "poll"
-
     def step(k):
         d = k % D
         if k >= 2 * D:
-            ev = done_ev[k % (2 * D)]
-            if poll:
-                while not ev.query():
-                    pass
-            else:
-                ev.synchronize()
+            done_ev[k % (2 * D)].synchronize()
         pk, it, sy = outs[d]
         dec.decode_device(inputs[d % len(inputs)].data_ptr(), B, pk.data_ptr(), method=method,
                           max_iters=iters, et_period=et, precision=prec, d_iters=it.data_ptr(),
@@ -840,6 +844,7 @@ def main():
     # the in-flight stream set, made now: before the variants' contexts make
     # and free streams of their own
     ctx_streams(torch, dec, dev, D)
+    probe0 = stream_probe_matrix(torch, dec, dev, D)
     # The variants (other methods / precisions, latency, the block, config 4)
     # are measured first, on every rank, so the headline's K steps run on a
     # GPU that has been busy for a while (its clock ramps from ~2.0 to
@@ -847,6 +852,9 @@ def main():
     # warmup_clock.txt) and every rank arrives in the same state.  Their CPU
     # checks run after the headline.
     pre = gpu_variants(L, torch, dec, args, dev, inputs, B, D, prec, dvb, world, rank)
+    probe = stream_probe_matrix(torch, dec, dev, D)
+    if probe is not None:
+        probe = {"after_creation": probe0, "before_headline": probe}
     r = time_decoder(dec, torch, inputs, B, args.method, args.iters, args.et_period, prec,
                      args.steps, args.warmup, dist, inflight=D)
     wall = r["wall"]
@@ -966,6 +974,7 @@ def main():
                               "(each other stream waits on it before its first launch) to the "
                               "last stream's end, / K",
                       "streams_distinct": r.get("streams_distinct"),
+                      "probe": probe,
                       "order": "measured after the GPU variants below (same process), so the "
                                "K steps see the GPU's steady clock; --no-variants times a "
                                "cold GPU"}

@@ -294,6 +294,11 @@ __global__ void __launch_bounds__(64) k_probe_set(uint32_t *flag) {
 }
 }  // namespace
 
+int launch_probe_touch(uint32_t *flag, void *stream) {
+  hipLaunchKernelGGL(k_probe_set, dim3(1), dim3(64), 0, (hipStream_t)stream, flag);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 int launch_probe_pair(uint32_t *flag, uint64_t deadline, void *wait_stream, void *set_stream) {
   hipLaunchKernelGGL(k_probe_wait, dim3(1), dim3(64), 0, (hipStream_t)wait_stream, flag, deadline);
   if (hipGetLastError() != hipSuccess) return -3;

@@ -32,5 +32,7 @@ int launch_longest_first(const float *in, int64_t cw_stride, int elem_stride, in
 // flag[0] = 0 and flag[1] = 0 beforehand; afterwards flag[1] == 1 iff the two
 // streams ran the pair concurrently (ldpc_aux.hip)
 int launch_probe_pair(uint32_t *flag, uint64_t deadline, void *wait_stream, void *set_stream);
+// one k_probe_set on `stream` (a stream's first launch: see ldpc_ctx_streams)
+int launch_probe_touch(uint32_t *flag, void *stream);
 
 }  // namespace ldpc

@@ -1932,72 +1932,83 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
   // Which hardware queue a stream lands on (GPU_MAX_HW_QUEUES of them) depends
   // on every stream the process made before it; two streams on one queue run
   // their launches one after the other.  A candidate joins the set only if a
-  // probe pair runs concurrently with every member; the others are kept until
-  // the set is complete (so the next candidate lands elsewhere), then freed.
-  std::vector<hipStream_t> spare;
+  // probe pair runs concurrently with every member (both ways round); the
+  // others are kept until the set is complete (so the next candidate lands
+  // elsewhere), then freed, and the finished set is probed once more.
+  // Measured (profiles/round5/inflight_bimodal.txt): a stream's FIRST launch
+  // can run beside a launch on a stream that shares its queue, so a probe
+  // that is a candidate's first use passed sets whose streams then ran one
+  // after the other -- one process in four at 0.72x the in-flight rate.  Every
+  // candidate now makes a launch of its own before it is probed, and a probe
+  // waits up to 20 ms: a queue the process has just made can take
+  // milliseconds before its first launch starts, which a 2 ms probe read as
+  // a shared queue.
   int rc = LDPC_OK;
-  // the probes must see only each other: work still running on some queue
-  // (another context's launches) would hold a probe kernel back past its
-  // timeout and reject a stream whose queue is in fact distinct
-  if (ctx->tp_streams.size() < (size_t)n && (e = hipDeviceSynchronize()) != hipSuccess)
-    return hip_err(ctx, e, "hipDeviceSynchronize");
-  auto concurrent = [&](hipStream_t a, hipStream_t c, bool &ok) {
-    uint32_t seen = 0;
-    if ((e = hipMemset(ctx->d_probe, 0, 8)) != hipSuccess ||
-        ldpc::launch_probe_pair(ctx->d_probe, 200000 /* 2 ms */, a, c) != 0 ||
-        (e = hipStreamSynchronize(a)) != hipSuccess || (e = hipStreamSynchronize(c)) != hipSuccess ||
-        (e = hipMemcpy(&seen, ctx->d_probe + 1, 4, hipMemcpyDeviceToHost)) != hipSuccess)
-      return hip_err(ctx, e, "stream probe");
-    ok = seen == 1u;
-    return LDPC_OK;
-  };
-  // First the plain way: n streams made back to back (measured the fastest
-  // set, profiles/round5/stream_sets.txt), kept if every pair runs at once.
-  if (ctx->tp_streams.empty()) {
-    std::vector<hipStream_t> batch;
-    bool all = true;
-    for (int i = 0; i < n && rc == LDPC_OK; ++i) {
-      hipStream_t c = nullptr;
-      if ((e = hipStreamCreateWithFlags(&c, hipStreamNonBlocking)) != hipSuccess) {
-        rc = hip_err(ctx, e, "hipStreamCreate");
-        break;
+  if (ctx->tp_streams.size() < (size_t)n) {
+    // the probes must see only each other: work still running on some queue
+    // would hold a probe kernel back past its timeout
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize");
+    auto concurrent = [&](hipStream_t a, hipStream_t c, bool &ok) {
+      uint32_t seen = 0;
+      if ((e = hipMemset(ctx->d_probe, 0, 8)) != hipSuccess ||
+          ldpc::launch_probe_pair(ctx->d_probe, 2000000 /* 20 ms */, a, c) != 0 ||
+          (e = hipStreamSynchronize(a)) != hipSuccess || (e = hipStreamSynchronize(c)) != hipSuccess ||
+          (e = hipMemcpy(&seen, ctx->d_probe + 1, 4, hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_err(ctx, e, "stream probe");
+      ok = seen == 1u;
+      return LDPC_OK;
+    };
+    auto both_ways = [&](hipStream_t a, hipStream_t c, bool &ok) {
+      int r = concurrent(a, c, ok);
+      if (r == LDPC_OK && ok) r = concurrent(c, a, ok);
+      return r;
+    };
+    auto fresh = [&](hipStream_t &c) {
+      c = nullptr;
+      if ((e = hipStreamCreateWithFlags(&c, hipStreamNonBlocking)) != hipSuccess)
+        return hip_err(ctx, e, "hipStreamCreate");
+      if (ldpc::launch_probe_touch(ctx->d_probe + 8, c) != 0 ||
+          (e = hipStreamSynchronize(c)) != hipSuccess) {
+        (void)hipStreamDestroy(c);
+        c = nullptr;
+        return hip_err(ctx, e, "stream probe");
       }
-      batch.push_back(c);
+      return LDPC_OK;
+    };
+    // members handed out by an earlier call stay (their callers hold them)
+    const size_t held = ctx->tp_streams.size();
+    for (int attempt = 0; attempt < 3 && rc == LDPC_OK; ++attempt) {
+      std::vector<hipStream_t> spare;
+      // (more streams than the process has hardware queues cannot all be
+      // concurrent: after a few candidates the set's streams are handed out
+      // again)
+      for (int tries = 0; (int)ctx->tp_streams.size() < n && tries < 3 * n; ++tries) {
+        hipStream_t c = nullptr;
+        if ((rc = fresh(c)) != LDPC_OK) break;
+        bool ok = true;
+        for (hipStream_t a : ctx->tp_streams) {
+          rc = both_ways(a, c, ok);
+          if (rc != LDPC_OK || !ok) break;
+        }
+        if (rc != LDPC_OK) {
+          (void)hipStreamDestroy(c);
+          break;
+        }
+        (ok ? ctx->tp_streams : spare).push_back(c);
+      }
+      for (hipStream_t t : spare) (void)hipStreamDestroy(t);
+      if (rc != LDPC_OK) break;
+      // the finished set, once more: a set that fails is made again
+      bool all = true;
+      for (size_t i = 0; i < ctx->tp_streams.size() && all && rc == LDPC_OK; ++i)
+        for (size_t j = i + 1; j < ctx->tp_streams.size() && all && rc == LDPC_OK; ++j)
+          rc = both_ways(ctx->tp_streams[i], ctx->tp_streams[j], all);
+      if (rc != LDPC_OK || all) break;
+      for (size_t i = held; i < ctx->tp_streams.size(); ++i) (void)hipStreamDestroy(ctx->tp_streams[i]);
+      ctx->tp_streams.resize(held);
     }
-    for (size_t i = 0; i < batch.size() && all && rc == LDPC_OK; ++i)
-      for (size_t j = i + 1; j < batch.size() && all && rc == LDPC_OK; ++j)
-        rc = concurrent(batch[i], batch[j], all);
-    if (rc == LDPC_OK && all && (int)batch.size() == n)
-      ctx->tp_streams = batch;
-    else
-      for (hipStream_t t : batch) (void)hipStreamDestroy(t);
     if (rc != LDPC_OK) return rc;
   }
-  // Otherwise one candidate at a time.
-  // (more streams than the process has hardware queues cannot all be
-  // concurrent: after a few candidates the set's streams are handed out again)
-  for (int tries = 0; (int)ctx->tp_streams.size() < n && tries < 3 * n; ++tries) {
-    hipStream_t c = nullptr;
-    if ((e = hipStreamCreateWithFlags(&c, hipStreamNonBlocking)) != hipSuccess) {
-      rc = hip_err(ctx, e, "hipStreamCreate");
-      break;
-    }
-    bool ok = true;
-    for (hipStream_t a : ctx->tp_streams) {
-      rc = concurrent(a, c, ok);
-      if (rc != LDPC_OK || !ok) {
-        ok = false;
-        break;
-      }
-    }
-    if (rc != LDPC_OK) {
-      (void)hipStreamDestroy(c);
-      break;
-    }
-    (ok ? ctx->tp_streams : spare).push_back(c);
-  }
-  for (hipStream_t t : spare) (void)hipStreamDestroy(t);
-  if (rc != LDPC_OK) return rc;
   if (ctx->tp_streams.empty()) return set_err(ctx, LDPC_EDEVICE, "no stream");
   const size_t m = ctx->tp_streams.size();
   for (int i = 0; i < n; ++i) streams_out[i] = (void *)ctx->tp_streams[(size_t)i % m];
