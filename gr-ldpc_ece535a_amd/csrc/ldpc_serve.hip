@@ -223,7 +223,6 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
 // (profiles/round5/serve_latency.txt).  Big rounds go to launches instead
 // (the block's hybrid, ldpc_decoder_cb_impl.h).
 constexpr int kServeWavesPerSimd = 3;
-constexpr int64_t kFastPollers = 256;
 // bytes of the two forms' overlaid frame regions
 template <typename Real, int METHOD, int S, int NW, int DVN>
 __host__ __device__ size_t serve_lds_main() {
@@ -276,14 +275,12 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
           r = kQuitRound;
           break;
         }
-        // Decoders past the first kFastPollers poll ~30x less often: a
-        // thousand decoders polling the round copies back to back delayed
-        // the round's sight by ~10 us; rounds that need them are big
-        // anyway.
-        if (g < kFastPollers)
-          __builtin_amdgcn_s_sleep(6);
-        else
-          __builtin_amdgcn_s_sleep(120);
+        // every decoder polls every ~0.16 us: with the keys riding in the
+        // round lines, a thousand pollers cost the round's sight nothing
+        // measurable, and decoders past the first 256 polling 30x less often
+        // made rounds of more windows 0.5-1 us slower and the block 2 %
+        // slower (profiles/round5/serve_pollers_ab.txt)
+        __builtin_amdgcn_s_sleep(6);
       }
       // the workgroup form's key: tagged with the round's epoch (see key_slot)
       if (r != kQuitRound && g < (int64_t)(r & 0xFFFFFu) && (int64_t)(r & 0xFFFFFu) <= (int64_t)((r >> 20) & 0xFFFFFu)) {
