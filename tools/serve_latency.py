@@ -23,11 +23,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=200)
     ap.add_argument("--iters", default="5,50")
     ap.add_argument("--ebn0", type=float, default=4.0)
+    ap.add_argument("--mode", type=int, default=0, help="ldpc_set_launch_mode for the launch path")
+    ap.add_argument("--no-serve", action="store_true")
     a = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime: torch's)
     import bench
     import ldpc_ece535a as L
     dec = L.Decoder()
+    dec.set_launch_mode(a.mode)
     y, _ = bench.synth(dec.H, 4096, a.ebn0, 3)
     s = y.ravel()
     rng = np.random.default_rng(1)
@@ -43,6 +46,10 @@ def main():
                 dec.decode_windows(s, wins[r % 8], method=1, max_iters=it, reuse_span=True)
                 t.append(time.perf_counter() - t0)
             launch_us = 1e6 * np.median(t[a.rounds // 4:])
+            if a.no_serve:
+                print("iters %2d B %5d: launch %8.1f us per round (mode %d)" % (it, B, launch_us, a.mode),
+                      flush=True)
+                continue
             dec.stage_span(s, max_windows=max(B, 4096))
             dec.serve_begin(method=1, max_iters=it, max_windows=max(B, 4096))
             t = []
