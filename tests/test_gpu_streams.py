@@ -81,3 +81,57 @@ def test_many_streams_reuse_counters():
             assert (pk.cpu().numpy() == ref["packed"]).all(), k
             assert (it.cpu().numpy() == ref["iters"]).all(), k
     dec.close()
+
+
+@pytest.mark.parametrize("extra", [0, 1, 3])
+def test_ctx_streams_run_concurrently(extra):
+    """ldpc_ctx_streams' set runs its launches side by side whatever streams
+    the process made before (profiles/round5/inflight_bimodal.txt: a set with
+    two streams on one hardware queue measured 0.72x).  In the throughput
+    launch mode a launch holds one wave per SIMD, so two launches on two
+    streams of a good set take about as long as one; on a shared queue they
+    take twice as long.  Every pair of the set is timed that way, and the
+    in-flight outputs equal the one-stream run's."""
+    import time
+    import torch
+    import ldpc_ece535a as L
+    keep = [torch.cuda.Stream() for _ in range(extra)]  # queue history
+    for st in keep:
+        with torch.cuda.stream(st):
+            torch.ones(16, device="cuda").sum()
+    torch.cuda.synchronize()
+    dec = L.Decoder()
+    dec.set_launch_mode(1)
+    hs = dec.streams(4)
+    assert len(set(hs)) == 4
+    B = 4096
+    ys = [torch.from_numpy(_frames(dec.H, B, 2.0, 40 + j)).cuda() for j in range(4)]
+    outs = [torch.empty((B, dec.KB), dtype=torch.uint8, device="cuda") for _ in range(4)]
+    its = [torch.empty(B, dtype=torch.int32, device="cuda") for _ in range(4)]
+
+    def run(streams, reps=3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for d, st in enumerate(streams):
+                dec.decode_device(ys[d].data_ptr(), B, outs[d].data_ptr(), method=1,
+                                  max_iters=50, d_iters=its[d].data_ptr(), stream=st)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    run(hs)  # warm-up (clocks)
+    run([hs[0]] * 4, 1)  # the four batches one after another on one stream
+    one = [(outs[d].cpu().numpy().copy(), its[d].cpu().numpy().copy()) for d in range(4)]
+    # the measure tells the two cases apart: both launches on one stream
+    t1 = run([hs[0]])
+    assert run([hs[0], hs[0]]) / t1 >= 1.6
+    for i in range(4):
+        for j in range(i + 1, 4):
+            t1 = min(run([hs[i]]), run([hs[j]]))
+            t2 = run([hs[i], hs[j]])
+            assert t2 / t1 < 1.6, "streams %d and %d: two launches %.2fx one" % (i, j, t2 / t1)
+    run(hs)
+    for d in range(4):
+        assert (outs[d].cpu().numpy() == one[d][0]).all()
+        assert (its[d].cpu().numpy() == one[d][1]).all()
+    dec.close()
