@@ -1939,10 +1939,12 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
   // can run beside a launch on a stream that shares its queue, so a probe
   // that is a candidate's first use passed sets whose streams then ran one
   // after the other -- one process in four at 0.72x the in-flight rate.  Every
-  // candidate now makes a launch of its own before it is probed, and a probe
-  // waits up to 20 ms: a queue the process has just made can take
-  // milliseconds before its first launch starts, which a 2 ms probe read as
-  // a shared queue.
+  // candidate now makes a launch of its own (and waits for it) before it is
+  // probed, and a probe waits up to 5 ms.  A new stream lands on the queue
+  // fewest streams use, so when the process's streams sit unevenly on its
+  // queues (a test process that made dozens) the missing queue is reached
+  // only after the others have taken the rejected candidates: up to 16 per
+  // wanted stream are tried.
   int rc = LDPC_OK;
   if (ctx->tp_streams.size() < (size_t)n) {
     // the probes must see only each other: work still running on some queue
@@ -1951,7 +1953,7 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
     auto concurrent = [&](hipStream_t a, hipStream_t c, bool &ok) {
       uint32_t seen = 0;
       if ((e = hipMemset(ctx->d_probe, 0, 8)) != hipSuccess ||
-          ldpc::launch_probe_pair(ctx->d_probe, 2000000 /* 20 ms */, a, c) != 0 ||
+          ldpc::launch_probe_pair(ctx->d_probe, 500000 /* 5 ms */, a, c) != 0 ||
           (e = hipStreamSynchronize(a)) != hipSuccess || (e = hipStreamSynchronize(c)) != hipSuccess ||
           (e = hipMemcpy(&seen, ctx->d_probe + 1, 4, hipMemcpyDeviceToHost)) != hipSuccess)
         return hip_err(ctx, e, "stream probe");
@@ -1982,7 +1984,7 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
       // (more streams than the process has hardware queues cannot all be
       // concurrent: after a few candidates the set's streams are handed out
       // again)
-      for (int tries = 0; (int)ctx->tp_streams.size() < n && tries < 3 * n; ++tries) {
+      for (int tries = 0; (int)ctx->tp_streams.size() < n && tries < 16 * n; ++tries) {
         hipStream_t c = nullptr;
         if ((rc = fresh(c)) != LDPC_OK) break;
         bool ok = true;
