@@ -297,7 +297,7 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
  * (1..16) streams that run concurrently -- each on its own hardware queue,
  * checked by probe launch pairs (both ways round, after each candidate's own
  * first launch, and the finished set once more) when the set is first made,
- * a few ms -- owned by the
+ * a few ms, up to ~0.3 s in a process with dozens of streams -- owned by the
  * context (destroyed by ldpc_destroy); with fewer hardware queues than n
  * (GPU_MAX_HW_QUEUES), the concurrent ones are handed out again in turn.  A
  * caller's own streams may share a
