@@ -12,8 +12,10 @@
 // windows' 5 iterations.
 //
 // Here ONE launch serves every round of a general_work call:
-//   * workgroup 0 (one lane) is the poller: it watches the round word in
-//     host-mapped memory, {epoch, B}, and republishes it in device memory;
+//   * wave 0 of workgroup 0 is the poller: each poll reads the round word in
+//     host-mapped memory, {epoch, B}, and the first 511 window keys in one
+//     PCIe round trip, and a new round is republished in device memory (the
+//     keys of its first 480 windows inside the lines the decoders poll);
 //   * every other workgroup is a decoder: tables and the log table are loaded
 //     into LDS once, then it waits for a new epoch, decodes windows g, g + G,
 //     ... of the round's list (the batch kernels' workgroup-per-frame
@@ -27,7 +29,8 @@
 //     clock), after which the host relaunches the server if it still wants a
 //     round.
 // Visibility: the device reads host memory with system-scope loads (the
-// round word, then the keys, which the host wrote before it), writes results
+// round word and the keys, each key tagged with its round's epoch, so a key
+// read before the host wrote it is read again), writes results
 // with one system-scope 8-byte store per window, and hands the round word to
 // the decoders as one agent-scope (sc1) granule polled with sc1 loads
 // (MI355X_MICROARCH.md, inter-workgroup visibility, R2).
