@@ -1992,20 +1992,23 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
           rc = both_ways(a, c, ok);
           if (rc != LDPC_OK || !ok) break;
         }
-        if (rc != LDPC_OK) {
-          (void)hipStreamDestroy(c);
-          break;
-        }
-        (ok ? ctx->tp_streams : spare).push_back(c);
+        (ok && rc == LDPC_OK ? ctx->tp_streams : spare).push_back(c);
+        if (rc != LDPC_OK) break;
       }
       for (hipStream_t t : spare) (void)hipStreamDestroy(t);
       if (rc != LDPC_OK) break;
-      // the finished set, once more: a set that fails is made again
+      // freeing a stream can release its hardware queue, and for a few ms
+      // after that probes read concurrent pairs as shared: let it settle
+      if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize");
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      // the finished set, once more; one that fails is made again, and after
+      // three tries the last one stays (a set, even a slower one, rather than
+      // an error)
       bool all = true;
       for (size_t i = 0; i < ctx->tp_streams.size() && all && rc == LDPC_OK; ++i)
         for (size_t j = i + 1; j < ctx->tp_streams.size() && all && rc == LDPC_OK; ++j)
           rc = both_ways(ctx->tp_streams[i], ctx->tp_streams[j], all);
-      if (rc != LDPC_OK || all) break;
+      if (rc != LDPC_OK || all || attempt == 2) break;
       for (size_t i = held; i < ctx->tp_streams.size(); ++i) (void)hipStreamDestroy(ctx->tp_streams[i]);
       ctx->tp_streams.resize(held);
     }
