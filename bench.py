@@ -217,19 +217,15 @@ def bytes_per_iter(E, N, prec):
 # --------------------------------------------------------------------------
 # timing (shared with tests/test_bench_dist.py, which runs it on the CPU)
 # --------------------------------------------------------------------------
-def timed_steps(step, steps, warmup, sync, dist=None, before=None):
+def timed_steps(step, steps, warmup, sync, dist=None):
     """W untimed steps, then exactly K timed steps bracketed by a barrier
-    and a device synchronize on both sides.  `before` (bookkeeping such as
-    the start event, no GPU work) runs between the synchronize and the
-    clock's start.  Returns the wall time (s)."""
+    and a device synchronize on both sides.  Returns the wall time (s)."""
     for k in range(warmup):
         step(k)
     sync()
     if dist is not None:
         dist.barrier()
     sync()
-    if before is not None:
-        before()
     t0 = time.perf_counter()
     for k in range(steps):
         step(warmup + k)
@@ -314,21 +310,14 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
     # of hundreds of launches)
     done_ev = [torch.cuda.Event() for _ in range(2 * D)]
 
-    # each stream's launch, its arguments converted once (ldpc_decode_device,
-    # the C ABI dec.decode_device wraps)
-    from ldpc_ece535a import _capi
-    fn = _capi.lib().ldpc_decode_device
-    vp = ctypes.c_void_p
-    args = [(dec._ctx, int(method), int(iters), int(et), int(prec),
-             vp(inputs[d % len(inputs)].data_ptr()), int(dec.N), 1, 1.0, int(B),
-             vp(outs[d][0].data_ptr()), None, vp(outs[d][1].data_ptr()),
-             vp(outs[d][2].data_ptr()), None, sps[d]) for d in range(D)]
-
     def step(k):
         d = k % D
         if k >= 2 * D:
             done_ev[k % (2 * D)].synchronize()
-        _capi._check(fn(*args[d]), dec._ctx)
+        pk, it, sy = outs[d]
+        dec.decode_device(inputs[d % len(inputs)].data_ptr(), B, pk.data_ptr(), method=method,
+                          max_iters=iters, et_period=et, precision=prec, d_iters=it.data_ptr(),
+                          d_synd=sy.data_ptr(), stream=sps[d])
         done_ev[k % (2 * D)].record(streams[d])
 
     e0 = torch.cuda.Event(enable_timing=True)
@@ -341,23 +330,22 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
     for ev in done_ev + [e0] + ends:
         ev.record(streams[0])
 
-    def start():
-        # the start event on the first timed step's stream, every other stream
-        # waiting on it: recorded before the clock starts (no GPU work; the
-        # device is idle after the synchronize)
-        e0.record(streams[warmup % D])
-        for d in range(D):
-            if d != warmup % D:
-                streams[d].wait_event(e0)
-
     def timed_step(k):
+        # first timed step: the start event on its stream; each other stream
+        # waits on it right before its own first launch, so the first launch
+        # is not queued behind the other streams' waits on the host
+        d = k % D
+        if k == warmup:
+            e0.record(streams[d])
+        elif k < warmup + D:
+            streams[d].wait_event(e0)
         step(k)
         if k == warmup + steps - 1:
             for s, e in zip(streams, ends):
                 e.record(s)
             marks["done"] = True
 
-    wall = timed_steps(timed_step, steps, warmup, sync, dist, before=start)
+    wall = timed_steps(timed_step, steps, warmup, sync, dist)
     span = max(e0.elapsed_time(e) for e in ends) if marks else 0.0
     return dict(wall=wall, span_ms=span, per_launch_ms=span / max(1, steps),
                 iters=outs[0][1].cpu().numpy(), outs=outs,
