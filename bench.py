@@ -12,11 +12,15 @@ convention (sigma = sqrt(10^(-EbN0/10)), apps/ldpc_lapack.cpp:635-642).
 Data are made on the GPU before timing: Philox bits (ldpc_random_bits) ->
 systematic GF(2) encode (ldpc_encode_device) -> BPSK + AWGN
 (ldpc_bpsk_awgn); the first frames are cross-checked against the host
-encoder.  D distinct batches are made (D = --inflight, default 4): step k
-decodes batch k mod D on stream k mod D, so D batches are in flight -- the
-next batch's frames fill the SIMDs the previous batch's last long frames
-leave idle (a streaming receiver's steady state).  Every step decodes its
-whole batch; the single-batch latency (D = 1) is reported beside it.
+encoder.  D distinct batches are made (D = --inflight, default 4); step k
+posts batch k mod D to the decoder's frame ring (ldpc_ring_post,
+csrc/ldpc_ring.hip): ONE persistent launch per timed region decodes every
+posted batch, frames of all batches from one device queue, so the frames of
+the next batch fill the SIMDs the previous batch's last long frames leave
+idle (a streaming receiver's steady state) and only the region's end has a
+tail.  Every step decodes its whole batch into its own outputs; the
+single-batch latency (one launch per batch, one at a time) is reported
+beside it.
 
 N > 1 runs under torch.distributed.run, one rank per GPU.  Weak scaling
 (default): every rank decodes its own B frames.  --strong: one global batch
@@ -128,30 +132,19 @@ _STREAMS = {}
 
 def side_stream(torch, dev):
     """The one torch stream the bench makes its data on (every synth_device
-    call): the decode launches themselves run on the decoder context's own
-    in-flight streams (ldpc_ctx_streams, each on its own hardware queue), so
-    what the process made before does not decide which of them overlap."""
+    call)."""
     key = str(dev)
     if key not in _STREAMS:
         _STREAMS[key] = torch.cuda.Stream(dev)
     return _STREAMS[key]
 
 
-def ctx_streams(torch, dec, dev, n):
-    """The decoder context's n in-flight streams as torch streams (for the
-    HIP events that time them)."""
-    return [torch.cuda.ExternalStream(h, device=dev) for h in dec.streams(n)]
-
-
-def stream_probe_matrix(torch, dec, dev, D):
-    """Diagnostics (LDPC_BENCH_PROBE=1, tools/probe_lib.cpp): for each ordered
-    pair of the in-flight streams, 1 if a launch on the second ran while one
-    on the first waited for it."""
-    if os.environ.get("LDPC_BENCH_PROBE") != "1":
-        return None
-    pl = ctypes.CDLL(os.path.join(REPO, "tools", "_probe_lib.so"))
-    hs = [ctypes.c_void_p(s.cuda_stream) for s in ctx_streams(torch, dec, dev, D)]
-    return "".join(str(pl.probe_pair(hs[i], hs[j], 0)) for i in range(D) for j in range(D) if i != j)
+def ring_stream(torch, dev):
+    """The stream the frame ring's sessions follow and the timing events sit on."""
+    key = "ring" + str(dev)
+    if key not in _STREAMS:
+        _STREAMS[key] = torch.cuda.Stream(dev)
+    return _STREAMS[key]
 
 
 def synth_device(L, torch, dec, B, ebn0, seed, dev, check_frames=64):
@@ -287,6 +280,59 @@ def plan_batch(B, world, rank, strong):
     return lo, hi - lo
 
 
+def time_ring(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, dist=None,
+              inflight=None, streams=None):
+    """Decode `steps` batches through the frame ring (ldpc_ring_*): step k
+    posts inputs[k % D] with outputs of its own.  One ring session per region
+    (the warmup's, the timed steps'): ldpc_ring_begin at the region's first
+    step, ldpc_ring_end after its last, so the closing synchronize of the
+    region waits for the launch to end, i.e. for every batch of the region.
+    Returns dict(wall, span_ms, per_launch_ms, iters, outs) like
+    time_decoder: span_ms from a HIP event recorded on the session's stream
+    before the timed session begins to one recorded after it ends (the
+    launch follows the first and the second follows the launch),
+    per_launch_ms = span_ms / steps (per batch), outs[d] = (packed, iters,
+    synd) of the last timed batch of inputs[d]."""
+    D = len(inputs)
+    dev = inputs[0].device
+    # the session's stream (torch's default stream is the null stream, which
+    # the ring's non-blocking streams do not order against)
+    st = ring_stream(torch, dev)
+    sp = ctypes.c_void_p(st.cuda_stream)
+    # outputs of their own for every step of both regions: a timed batch's
+    # outputs can only come from the timed session
+    P = max(1, steps + warmup)
+    pool = [(torch.empty((B, dec.KB), dtype=torch.uint8, device=dev),
+             torch.empty(B, dtype=torch.int32, device=dev),
+             torch.empty(B, dtype=torch.int32, device=dev)) for _ in range(P)]
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    for ev in (e0, e1):  # created before the timed region
+        ev.record(st)
+    last = {}
+
+    def step(k):
+        if k == 0 or k == warmup:
+            if k == warmup:
+                e0.record(st)
+            dec.ring_begin(method=method, max_iters=iters, et_period=et, precision=prec, stream=sp)
+        pk, it, sy = pool[k]
+        dec.ring_post(inputs[k % D].data_ptr(), B, pk.data_ptr(), it.data_ptr(), sy.data_ptr())
+        if k >= warmup:
+            last[k % D] = k
+        if k == warmup - 1 or k == warmup + steps - 1:
+            dec.ring_end()
+            if k == warmup + steps - 1:
+                e1.record(st)
+
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    wall = timed_steps(step, steps, warmup, sync, dist)
+    span = e0.elapsed_time(e1) if steps else 0.0
+    outs = [pool[last[d]] if d in last else pool[0] for d in range(D)]
+    return dict(wall=wall, span_ms=span, per_launch_ms=span / max(1, steps),
+                iters=outs[0][1].cpu().numpy(), outs=outs, ring=dec.ring_info())
+
+
 def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, dist=None,
                  inflight=1, streams=None):
     """Decode `steps` batches with `inflight` batches in flight: step k
@@ -299,7 +345,7 @@ def time_decoder(dec, torch, inputs, B, method, iters, et, prec, steps, warmup, 
     D = max(1, inflight)
     dev = inputs[0].device
     if streams is None:
-        streams = ctx_streams(torch, dec, dev, D)
+        streams = [torch.cuda.Stream(dev) for _ in range(D)]
     sps = [ctypes.c_void_p(s.cuda_stream) for s in streams]
     outs = [(torch.empty((B, dec.KB), dtype=torch.uint8, device=dev),
              torch.empty(B, dtype=torch.int32, device=dev),
@@ -624,8 +670,8 @@ def config5_variant(L, torch, args, dev, sizes=(1, 16, 256, 4096, 65536), check_
                     "cap, one launch at a time (latency mode); latency = HIP-event span per "
                     "launch"}
     kept = {}
-    # one launch at a time: the context's first in-flight stream
-    c5_stream = ctx_streams(torch, dec, dev, 1)
+    # one launch at a time, on a stream of its own
+    c5_stream = [torch.cuda.Stream(dev)]
     for name, m in (("sum-product f64 (exact)", 1), ("min-sum f64", 0)):
         rows = {}
         for Bs in sizes:
@@ -702,7 +748,7 @@ def gpu_variants(L, torch, dec, args, dev, inputs, B, D, prec, dvb, world, rank)
                              "min-sum f64": (0, 0), "min-sum f32": (0, 1)}.items():
             if (m, p) == (args.method, prec):
                 continue
-            r2, st = time_variant(time_decoder, dec, torch, inputs, B, m, args.iters,
+            r2, st = time_variant(time_ring, dec, torch, inputs, B, m, args.iters,
                                   args.et_period, p, max(5, args.steps // 2), 4, D)
             it2 = r2["iters"]
             var[name] = {"Mbit/s": round(B * dec.K * st / r2["wall"] / 1e6, 2),
@@ -841,10 +887,6 @@ def main():
         dec.set_launch_mode(1 if D > 1 else 0)
         if args.waves_per_cu:
             dec.set_waves_per_cu(args.waves_per_cu)
-    # the in-flight stream set, made now: before the variants' contexts make
-    # and free streams of their own
-    ctx_streams(torch, dec, dev, D)
-    probe0 = stream_probe_matrix(torch, dec, dev, D)
     # The variants (other methods / precisions, latency, the block, config 4)
     # are measured first, on every rank, so the headline's K steps run on a
     # GPU that has been busy for a while (its clock ramps from ~2.0 to
@@ -852,11 +894,12 @@ def main():
     # warmup_clock.txt) and every rank arrives in the same state.  Their CPU
     # checks run after the headline.
     pre = gpu_variants(L, torch, dec, args, dev, inputs, B, D, prec, dvb, world, rank)
-    probe = stream_probe_matrix(torch, dec, dev, D)
-    if probe is not None:
-        probe = {"after_creation": probe0, "before_headline": probe}
-    r = time_decoder(dec, torch, inputs, B, args.method, args.iters, args.et_period, prec,
-                     args.steps, args.warmup, dist, inflight=D)
+    # small codes: the frame ring (one launch per timed region, frames of all
+    # batches from one queue); large codes (config 4's pipeline): a launch per
+    # batch
+    timer = time_decoder if dvb else time_ring
+    r = timer(dec, torch, inputs, B, args.method, args.iters, args.et_period, prec,
+              args.steps, args.warmup, dist, inflight=D)
     wall = r["wall"]
     iters_b = [o[1].cpu().numpy() for o in r["outs"]]
     synd_b = [o[2].cpu().numpy() for o in r["outs"]]
@@ -953,7 +996,9 @@ def main():
                                 "achieved_basis": "edge-message byte model (no PMC entry)",
                                 "model": hbm_model["model"]}
     elif pmc and "SQ_INSTS_VALU" in pmc:
-        line["roofline"] = valu_roofline(pmc, per_launch_ms,
+        # per batch: the PMC entry's counts per batch over the device span per
+        # batch (the ring launch's own time / K)
+        line["roofline"] = valu_roofline(pmc, r["per_launch_ms"] or per_launch_ms,
                                          (entry.get("isa_hot") or {}).get("other_weight"))
         line["roofline"]["traffic"] = traffic
         line["roofline"]["pmc_source"] = entry.get("source")
@@ -970,11 +1015,12 @@ def main():
         line["hbm_byte_model"] = hbm_model
     line["timing"] = {"device_span_ms_per_launch": round(r["per_launch_ms"], 5),
                       "wall_ms_per_step": round(per_launch_ms, 5),
-                      "note": "span = HIP events: start on the first timed step's stream "
-                              "(each other stream waits on it before its first launch) to the "
-                              "last stream's end, / K",
-                      "streams_distinct": r.get("streams_distinct"),
-                      "probe": probe,
+                      "note": ("span = HIP events on the ring session's stream: one before "
+                               "the timed session's launch (which waits on it), one after the "
+                               "session's end (which waits on the launch), / K batches; the "
+                               "roofline's per-batch time" if not dvb else
+                               "span = HIP events around the K launches, / K"),
+                      "frame_ring": r.get("ring"),
                       "order": "measured after the GPU variants below (same process), so the "
                                "K steps see the GPU's steady clock; --no-variants times a "
                                "cold GPU"}

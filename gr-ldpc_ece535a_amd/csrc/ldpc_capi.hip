@@ -141,7 +141,23 @@ struct ldpc_ctx {
   // LDPC_SERVE_DEBUG: rounds, host us, poller's sight -> publication, ->
   // last key read, -> last result stored (us)
   double dbg[6] = {0, 0, 0, 0, 0, 0};  // ... and the host's sight of the first result
-  bool srv_debug = getenv("LDPC_SERVE_DEBUG") != nullptr;
+  bool srv_debug = false;  // LDPC_SERVE_DEBUG, read when a launch starts
+  bool srv_test_skip_check = false;  // ldpc_test_hook(LDPC_TEST_SERVE_UNCHECKED)
+  // the frame ring (ldpc_ring_*, ldpc_ring.hip): mapped host memory
+  // [kRingSlots descriptors | kRingSlots completion words], device memory
+  // [per-slot frame counters | queue head], the launch's own stream and an
+  // event recorded behind the launch (complete = the launch has ended)
+  bool ring_on = false;  // a session is open (ldpc_ring_begin .. ldpc_ring_end)
+  int ring_method = 0, ring_iters = 0, ring_et = 1, ring_prec = 0;
+  uint8_t *h_ring = nullptr;
+  uint32_t *d_ring = nullptr;
+  hipStream_t ring_stream = nullptr;
+  hipEvent_t ring_ev = nullptr, ring_user_ev = nullptr;
+  void *ring_user_stream = nullptr;
+  uint64_t ring_next = 0;      // the next batch's sequence number
+  int64_t ring_frames = 0;     // tickets posted so far (the next batch's start)
+  int64_t ring_start[ldpc::kRingSlots] = {};  // start ticket of the batch in each slot
+  int ring_launches = 0, ring_workgroups = 0;
   // in-flight stream set for throughput callers (ldpc_ctx_streams): streams
   // verified to run concurrently, i.e. on distinct hardware queues
   std::vector<hipStream_t> tp_streams;
@@ -1020,6 +1036,15 @@ ldpc_ctx *ldpc_create_csr(int M, int N, const int32_t *row_ptr, const int32_t *c
 void ldpc_destroy(ldpc_ctx *ctx) {
   if (!ctx) return;
   serve_stop(ctx);
+  if (ctx->ring_on) (void)ldpc_ring_end(ctx);
+  if (ctx->ring_stream) {
+    (void)hipStreamSynchronize(ctx->ring_stream);
+    (void)hipStreamDestroy(ctx->ring_stream);
+  }
+  if (ctx->ring_ev) (void)hipEventDestroy(ctx->ring_ev);
+  if (ctx->ring_user_ev) (void)hipEventDestroy(ctx->ring_user_ev);
+  if (ctx->h_ring) (void)hipHostFree(ctx->h_ring);
+  if (ctx->d_ring) (void)hipFree(ctx->d_ring);
   if (ctx->win_profile && ctx->win_calls)
     fprintf(stderr,
             "ldpc_decode_windows profile: %lld calls, %lld windows; staging %.3f ms, window list + "
@@ -1635,10 +1660,15 @@ int decode_windows_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period,
 
 // Launches the window server for the context's parameters on its stream
 // (ctl zeroed first: it must read below every epoch the launch serves).
-int serve_launch(ldpc_ctx *ctx) {
+// repost_n >= 0 (a relaunch after the old launch's deadline): the round the
+// host is waiting on, repost_n windows, is posted again with the NEW session
+// before the launch, so the new poller never sees the old session's word for
+// it and quits (the host used to post after the launch).
+int serve_launch(ldpc_ctx *ctx, int repost_n = -1) {
   hipError_t e;
   if (!ctx->d_srv_ctl || !ctx->d_srv_keys || !ctx->h_srv)
     return set_err(ctx, LDPC_EINVAL, "window server buffers missing");
+  if ((e = hipSetDevice(ctx->device)) != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   if ((e = hipMemsetAsync(ctx->d_srv_ctl, 0, ldpc::kServeCtlBytes, ctx->stream)) != hipSuccess)
     return hip_err(ctx, e, "hipMemsetAsync(server ctl)");
   void *dh = nullptr;
@@ -1650,15 +1680,23 @@ int serve_launch(ldpc_ctx *ctx) {
   sa.res = (uint64_t *)((uint8_t *)dh + srv_res_off(ctx->srv_cap));
   sa.dkeys = ctx->d_srv_keys;
   sa.ctl = ctx->d_srv_ctl;
+  sa.span = ctx->span_samples;
   const char *dl = getenv("LDPC_SERVE_DEADLINE_MS");
   sa.deadline = (uint64_t)((dl ? atof(dl) : 200.0) * 1e5);  // 100 MHz ticks
-  sa.start_epoch = ctx->srv_epoch;
   ctx->srv_launches += 1;  // this launch's session: the rounds posted from now on
   sa.session = (uint32_t)ctx->srv_launches;
+  if (repost_n >= 0) {
+    ctx->srv_epoch -= 1;  // the launch serves epochs above start_epoch
+    sa.start_epoch = ctx->srv_epoch;
+    serve_post(ctx, (uint32_t)repost_n);  // the same round (epoch, key tags), the new session
+  } else {
+    sa.start_epoch = ctx->srv_epoch;
+  }
   // decoder workgroups per CU (capped by occupancy); 0 = as many as fit
   const char *pc = getenv("LDPC_SERVE_BLOCKS_PER_CU");
   sa.blocks_per_cu = pc ? atoi(pc) : 0;
-  sa.debug = getenv("LDPC_SERVE_DEBUG") ? 1 : 0;
+  ctx->srv_debug = getenv("LDPC_SERVE_DEBUG") != nullptr;  // (read per launch)
+  sa.debug = ctx->srv_debug ? 1 : 0;
   int wg = 0;
   ldpc::DecodeArgs a{};
   a.in = (const float *)ctx->d_wstage;
@@ -1668,10 +1706,23 @@ int serve_launch(ldpc_ctx *ctx) {
   a.max_iters = ctx->srv_iters;
   a.et_period = 1;
   const int rc = ldpc::launch_serve(code_view(ctx), a, sa, ctx->srv_method, ctx->srv_prec,
-                                    ctx->slots, ctx->nw, ctx->stream, &wg);
+                                    ctx->slots, ctx->nw, ctx->device, ctx->stream, &wg);
   ctx->srv_workgroups = wg;
   if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no window server for this code shape");
   if (rc != 0) return hip_err(ctx, hipGetLastError(), "window server launch");
+  return LDPC_OK;
+}
+
+// Starts the epochs over (a new session): the running launch, if any, has
+// finished; host keys and results and the device key copies are cleared, so
+// no slot carries a tag from before the restart.
+int serve_reset_epochs(ldpc_ctx *ctx) {
+  hipError_t e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize(server)");
+  memset(ctx->h_srv, 0, srv_bytes(ctx->srv_cap));
+  if ((e = hipMemsetAsync(ctx->d_srv_keys, 0, (size_t)ctx->srv_cap * 8, ctx->stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipMemsetAsync(server keys)");
+  ctx->srv_epoch = 0;
   return LDPC_OK;
 }
 
@@ -1696,7 +1747,7 @@ int serve_begin_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, in
     return hip_err(ctx, e, "hipMalloc(server ctl)");
   // a new buffer (or epochs near the end of their range) starts the epochs over:
   // the previous launch has finished first
-  if (ctx->srv_cap < max_windows || ctx->srv_epoch >= (1u << 23) - (1u << 16)) {
+  if (ctx->srv_cap < max_windows || ctx->srv_epoch >= ldpc::kServeEpochLimit) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->srv_cap < max_windows) {
       if (ctx->h_srv) (void)hipHostFree(ctx->h_srv);
@@ -1712,8 +1763,7 @@ int serve_begin_impl(ldpc_ctx *ctx, int method, int max_iters, int precision, in
         return hip_err(ctx, e, "hipMalloc(server keys)");
       ctx->srv_cap = cap;
     }
-    memset(ctx->h_srv, 0, srv_bytes(ctx->srv_cap));
-    ctx->srv_epoch = 0;
+    if ((rc = serve_reset_epochs(ctx)) != LDPC_OK) return rc;
   }
   ctx->srv_method = method;
   ctx->srv_iters = max_iters;
@@ -1732,14 +1782,31 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
   if (B == 0) return LDPC_OK;
   if (!win || !out_packed) return set_err(ctx, LDPC_EINVAL, "null buffer");
   const int N = ctx->N, KB = ctx->KB;
+  // (ldpc_test_hook 1 skips this check once, so that the device's own check
+  // of every key -- ldpc_serve.hip key_fault -- can be exercised)
+  const bool host_check = !ctx->srv_test_skip_check;
+  ctx->srv_test_skip_check = false;
   for (int b = 0; b < B; ++b)
-    if (win[b] < 0 || (win[b] >> 1) + N > ctx->span_samples || win[b] >= ((int64_t)1 << 40))
+    if (win[b] < 0 || win[b] >= ((int64_t)1 << 40) ||
+        (host_check && (win[b] >> 1) + N > ctx->span_samples))
       return set_err(ctx, LDPC_EINVAL, "window outside the staged span");
+  int device_fault = 0;  // a granule that carries no decode (kServeBadKey / kServeLostKey)
+  int64_t fault_key = 0;
   int64_t *keys = (int64_t *)(ctx->h_srv + srv_keys_off());
   const uint64_t *res = (const uint64_t *)(ctx->h_srv + srv_res_off(ctx->srv_cap));
   const double timeout_s = 10.0;
   for (int b0 = 0; b0 < B; b0 += (int)ctx->srv_cap) {
     const int n = (int)std::min<int64_t>(ctx->srv_cap, B - b0);
+    // epochs stay below kServeEpochLimit (result tags are epoch mod 2^23, and a
+    // tag that wrapped would match a stale slot): a session that reaches it is
+    // ended and started over before this round
+    if (ctx->srv_epoch + 2 >= ldpc::kServeEpochLimit) {
+      serve_stop(ctx);
+      int rc = serve_reset_epochs(ctx);
+      if (rc == LDPC_OK) rc = serve_launch(ctx);
+      if (rc != LDPC_OK) return rc;
+      ctx->serving = true;
+    }
     // each key carries the epoch it is posted with (mod 2^24), so the poller
     // can tell a slot it read before this round's write (ldpc_serve.hip)
     const uint64_t ktag = (uint64_t)((ctx->srv_epoch + 1) & 0xFFFFFFu) << 40;
@@ -1760,7 +1827,7 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
           // the launch ended (its deadline passed between rounds): start another
           const hipError_t q = hipStreamQuery(ctx->stream);
           if (q == hipSuccess) {
-            if (getenv("LDPC_SERVE_DEBUG")) {
+            if (ctx->srv_debug) {
               uint64_t c[8] = {0}, c0 = 0;
               uint32_t census = 0;
               (void)hipMemcpy(&c0, ctx->d_srv_ctl, 8, hipMemcpyDeviceToHost);
@@ -1781,13 +1848,11 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
               ctx->serving = false;
               return set_err(ctx, LDPC_ETIMEOUT, "the window server keeps ending before its round");
             }
-            ctx->srv_epoch -= 1;  // the launch serves epochs above start_epoch
-            const int rc = serve_launch(ctx);
+            const int rc = serve_launch(ctx, n);  // the same round, posted for the new session
             if (rc != LDPC_OK) {
               ctx->serving = false;
               return rc;
             }
-            serve_post(ctx, (uint32_t)n);  // the same round (epoch, tag), the new session's
           } else if (q != hipErrorNotReady) {
             ctx->serving = false;
             return hip_err(ctx, q, "window server");
@@ -1798,11 +1863,18 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
           }
         }
       }
-      const uint32_t pk = (uint32_t)g;
+      const uint32_t pk = (uint32_t)g, wt = (uint32_t)(g >> 32) & 511u;
+      if (wt == ldpc::kServeBadKey || wt == ldpc::kServeLostKey) {
+        if (!device_fault) {
+          device_fault = (int)wt;
+          fault_key = win[b0 + b];
+        }
+        continue;  // (the round's other results are still collected)
+      }
       for (int j = 0; j < KB; ++j) out_packed[(size_t)(b0 + b) * KB + j] = (uint8_t)(pk >> (8 * j));
-      if (syn_weight_opt) syn_weight_opt[b0 + b] = (int32_t)((g >> 32) & 511u);
+      if (syn_weight_opt) syn_weight_opt[b0 + b] = (int32_t)wt;
     }
-    if (getenv("LDPC_SERVE_DEBUG")) {  // device-side split of the round (100 MHz ticks)
+    if (ctx->srv_debug) {  // device-side split of the round (100 MHz ticks)
       const double host_us =
           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6;
       const double first_us = std::chrono::duration<double>(t_first - t0).count() * 1e6;
@@ -1822,7 +1894,141 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
       }
     }
   }
+  if (device_fault) {
+    char buf[200];
+    snprintf(buf, sizeof buf,
+             "window server: %s (window key %lld, span of %lld samples); the window was not "
+             "decoded",
+             device_fault == (int)ldpc::kServeBadKey
+                 ? "the device refused a window key outside the staged span"
+                 : "a window key never reached the device within the deadline",
+             (long long)fault_key, (long long)ctx->span_samples);
+    return set_err(ctx, LDPC_EDEVICE, buf);
+  }
   return LDPC_OK;
+}
+
+// ---- the frame ring (ldpc_ring_*) -------------------------------------------
+// Mapped host memory: kRingSlots 64-byte descriptors, then kRingSlots
+// completion words.  Device memory: kRingSlots frame counters, one 256-byte
+// line each, then the queue head on a line of its own.
+constexpr size_t kRingCompOff = sizeof(ldpc::RingDesc) * ldpc::kRingSlots;
+constexpr size_t kRingHostBytes = kRingCompOff + 8 * ldpc::kRingSlots;
+constexpr size_t kRingTicketOff = (size_t)ldpc::kRingSlots * ldpc::kRingDoneStride;  // in u32
+constexpr size_t kRingMirrorOff = 4 * (kRingTicketOff + 64);  // bytes: the descriptor mirror
+constexpr size_t kRingDevBytes = kRingMirrorOff + sizeof(ldpc::RingDesc) * ldpc::kRingSlots;
+constexpr uint64_t kRingDeadlineTicks = 5000000;  // 50 ms without a batch: a wave leaves
+constexpr double kRingTimeoutS = 10.0;
+
+bool ring_done(ldpc_ctx *ctx, uint64_t q) {
+  return __atomic_load_n(reinterpret_cast<uint64_t *>(ctx->h_ring + kRingCompOff) +
+                             q % ldpc::kRingSlots,
+                         __ATOMIC_ACQUIRE) >= q + 1;
+}
+
+// Writes batch q's descriptor: words 1..7 tagged with (q + 1) mod 2^16 in bits
+// 48..63, then word 0 = q + 1 (x86 stores are ordered; the device accepts the
+// line only when all eight agree, ldpc_ring.hip locate).
+void ring_write_desc(ldpc_ctx *ctx, uint64_t q, int64_t start, const void *in, int64_t cw,
+                     void *packed, void *iters, void *synd, int B, int quit) {
+  uint64_t *w = reinterpret_cast<uint64_t *>(ctx->h_ring) + 8 * (q % ldpc::kRingSlots);
+  const uint64_t tag = ((q + 1) & 0xFFFFu) << 48, pay = (1ull << 48) - 1;
+  const uint64_t v[7] = {(uint64_t)start, (uint64_t)(uintptr_t)in, (uint64_t)cw,
+                         (uint64_t)(uintptr_t)packed, (uint64_t)(uintptr_t)iters,
+                         (uint64_t)(uintptr_t)synd,
+                         (uint64_t)(uint32_t)B | ((uint64_t)(quit ? 1 : 0) << 32)};
+  for (int j = 0; j < 7; ++j) __atomic_store_n(w + 1 + j, (v[j] & pay) | tag, __ATOMIC_RELAXED);
+  __atomic_store_n(w, q + 1, __ATOMIC_RELEASE);
+}
+
+// Launches the ring from batch `cursor` (every earlier batch complete), its
+// first ticket `ticket0`: counters and queue head zeroed first, on the ring's
+// stream, and the event recorded behind the launch.
+int ring_launch(ldpc_ctx *ctx, uint64_t cursor, int64_t ticket0) {
+  hipError_t e;
+  if ((e = hipSetDevice(ctx->device)) != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  if ((e = hipMemsetAsync(ctx->d_ring, 0, kRingDevBytes, ctx->ring_stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipMemsetAsync(ring)");
+  void *dh = nullptr;
+  if ((e = hipHostGetDevicePointer(&dh, ctx->h_ring, 0)) != hipSuccess)
+    return hip_err(ctx, e, "hipHostGetDevicePointer(ring)");
+  ldpc::RingArgs r{};
+  r.desc = reinterpret_cast<const ldpc::RingDesc *>(dh);
+  r.comp = reinterpret_cast<uint64_t *>((uint8_t *)dh + kRingCompOff);
+  r.done = ctx->d_ring;
+  r.ticket = ctx->d_ring + kRingTicketOff;
+  r.mirror = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(ctx->d_ring) + kRingMirrorOff);
+  r.ticket0 = ticket0;
+  r.cursor0 = cursor;
+  r.deadline = kRingDeadlineTicks;
+  r.max_iters = ctx->ring_iters;
+  r.et_period = ctx->ring_et;
+  int wg = 0;
+  const int rc = ldpc::launch_ring(code_view(ctx), r, ctx->ring_method, ctx->ring_prec, ctx->slots,
+                                   ctx->nw, ctx->device, ctx->ring_stream, &wg);
+  if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no frame ring for this code shape");
+  if (rc != 0) return hip_err(ctx, hipGetLastError(), "frame ring launch");
+  ctx->ring_workgroups = wg;
+  ctx->ring_launches += 1;
+  if ((e = hipEventRecord(ctx->ring_ev, ctx->ring_stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipEventRecord(ring)");
+  return LDPC_OK;
+}
+
+// A launch whose waves all left on the deadline (no batch for 50 ms) has
+// ended: if posted batches are not complete, launch again from the first of
+// them.  Its frames are decoded again from frame 0 -- a wave may have left
+// holding a ticket of a batch it never saw -- and the frame counters start
+// at zero, so a batch completes exactly once.
+// `upto`: batches before it are the ones that must complete (a posted quit
+// descriptor is not one of them).
+int ring_revive(ldpc_ctx *ctx, uint64_t upto) {
+  const hipError_t q = hipEventQuery(ctx->ring_ev);
+  if (q == hipErrorNotReady) return LDPC_OK;
+  if (q != hipSuccess) return hip_err(ctx, q, "frame ring");
+  uint64_t first = upto;
+  const uint64_t lo = upto > (uint64_t)ldpc::kRingSlots ? upto - ldpc::kRingSlots : 0;
+  for (uint64_t b = lo; b < upto; ++b)
+    if (!ring_done(ctx, b)) {
+      first = b;
+      break;
+    }
+  if (first == upto) return LDPC_OK;  // nothing outstanding: relaunch on the next post
+  return ring_launch(ctx, first, ctx->ring_start[first % ldpc::kRingSlots]);
+}
+
+// Waits until batch q is complete (q < ring_next).
+int ring_wait_impl(ldpc_ctx *ctx, uint64_t q) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spins = 1; !ring_done(ctx, q); ++spins) {
+    if ((spins & 0x3FFu) == 0) {
+      const int rc = ring_revive(ctx, q + 1);
+      if (rc != LDPC_OK) return rc;
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
+          kRingTimeoutS)
+        return set_err(ctx, LDPC_ETIMEOUT, "a frame ring batch passed its timeout");
+    }
+  }
+  return LDPC_OK;
+}
+
+// Posts one descriptor (a batch, or quit): waits for its slot's previous
+// batch, writes the line, and relaunches a launch that has ended.
+int64_t ring_post_impl(ldpc_ctx *ctx, const float *d_in, int64_t cw, int B, uint8_t *packed,
+                       int32_t *iters, int32_t *synd, int quit) {
+  const uint64_t q = ctx->ring_next;
+  if (q >= (uint64_t)ldpc::kRingSlots) {
+    const int rc = ring_wait_impl(ctx, q - ldpc::kRingSlots);
+    if (rc != LDPC_OK) return rc;
+  }
+  ctx->ring_start[q % ldpc::kRingSlots] = ctx->ring_frames;
+  ring_write_desc(ctx, q, ctx->ring_frames, d_in, cw, packed, iters, synd, B, quit);
+  ctx->ring_next = q + 1;
+  ctx->ring_frames += B;
+  // a launch that has ended meanwhile would never see it
+  // (a quit descriptor alone needs no launch: nothing would be decoded)
+  const int rc = ring_revive(ctx, quit ? q : q + 1);
+  return rc != LDPC_OK ? rc : (int64_t)q;
 }
 }  // namespace
 
@@ -1858,7 +2064,7 @@ int ldpc_serve_windows(ldpc_ctx *ctx, const int64_t *windows, int B, uint8_t *ou
 
 int ldpc_serve_end(ldpc_ctx *ctx) {
   if (!ctx) return LDPC_EINVAL;
-  if (getenv("LDPC_SERVE_DEBUG") && ctx->dbg[0] > 0) {
+  if (ctx->srv_debug && ctx->dbg[0] > 0) {
     fprintf(stderr,
             "ldpc_serve: %.0f rounds: host %.1f us per round; poller: sight to publication %.1f "
             "us; from the publication: last key read %.1f us, last result stored %.1f us; host: "
@@ -1875,6 +2081,114 @@ int ldpc_serve_end(ldpc_ctx *ctx) {
     ctx->serving = false;
   }
   return LDPC_OK;
+}
+
+int ldpc_ring_begin(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+                    void *hip_stream) {
+  if (!ctx) return LDPC_EINVAL;
+  int rc = check_decode_args(ctx, method, max_iters, et_period, precision, 1, 1, ctx->N);
+  if (rc != LDPC_OK) return rc;
+  if (ctx->ring_on) return set_err(ctx, LDPC_EINVAL, "a frame ring session is open (ldpc_ring_end)");
+  if (ctx->graph || (method != 0 && method != 1))
+    return set_err(ctx, LDPC_EUNSUPPORTED,
+                   "the frame ring takes min-sum / sum-product on small codes");
+  serve_stop(ctx);
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  if (!ctx->h_ring &&
+      (e = hipHostMalloc((void **)&ctx->h_ring, kRingHostBytes,
+                         hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+    return hip_err(ctx, e, "hipHostMalloc(ring)");
+  if (!ctx->d_ring && (e = hipMalloc((void **)&ctx->d_ring, kRingDevBytes)) != hipSuccess)
+    return hip_err(ctx, e, "hipMalloc(ring)");
+  if (!ctx->ring_stream &&
+      (e = hipStreamCreateWithFlags(&ctx->ring_stream, hipStreamNonBlocking)) != hipSuccess)
+    return hip_err(ctx, e, "hipStreamCreate(ring)");
+  if (!ctx->ring_ev && (e = hipEventCreateWithFlags(&ctx->ring_ev, hipEventDisableTiming)) != hipSuccess)
+    return hip_err(ctx, e, "hipEventCreate(ring)");
+  if (!ctx->ring_user_ev &&
+      (e = hipEventCreateWithFlags(&ctx->ring_user_ev, hipEventDisableTiming)) != hipSuccess)
+    return hip_err(ctx, e, "hipEventCreate(ring)");
+  // the previous session's launch has ended before the slots are cleared
+  if ((e = hipStreamSynchronize(ctx->ring_stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipStreamSynchronize(ring)");
+  memset(ctx->h_ring, 0, kRingHostBytes);
+  ctx->ring_method = method;
+  ctx->ring_iters = max_iters;
+  ctx->ring_et = et_period;
+  ctx->ring_prec = precision;
+  ctx->ring_next = 0;
+  ctx->ring_frames = 0;
+  // the launch follows the work enqueued on the caller's stream so far
+  ctx->ring_user_stream = hip_stream ? hip_stream : (void *)ctx->stream;
+  if ((e = hipEventRecord(ctx->ring_user_ev, (hipStream_t)ctx->ring_user_stream)) != hipSuccess ||
+      (e = hipStreamWaitEvent(ctx->ring_stream, ctx->ring_user_ev, 0)) != hipSuccess)
+    return hip_err(ctx, e, "frame ring: stream order");
+  rc = ring_launch(ctx, 0, 0);
+  if (rc != LDPC_OK) return rc;
+  ctx->ring_on = true;
+  return LDPC_OK;
+}
+
+int64_t ldpc_ring_post(ldpc_ctx *ctx, const float *d_in, int64_t cw_stride, int B,
+                       uint8_t *d_out_packed, int32_t *d_iters_used_opt,
+                       int32_t *d_syn_weight_opt) {
+  if (!ctx) return LDPC_EINVAL;
+  if (!ctx->ring_on) return set_err(ctx, LDPC_EINVAL, "no frame ring session (ldpc_ring_begin)");
+  if (B < 1) return set_err(ctx, LDPC_EINVAL, "B must be >= 1");
+  if (!d_in || !d_out_packed) return set_err(ctx, LDPC_EINVAL, "null buffer");
+  if (cw_stride < ctx->N || cw_stride >= ((int64_t)1 << 40))
+    return set_err(ctx, LDPC_EINVAL, "cw_stride must be in [N, 2^40)");
+  for (const void *p : {(const void *)d_in, (const void *)d_out_packed, (const void *)d_iters_used_opt,
+                        (const void *)d_syn_weight_opt})
+    if ((uintptr_t)p >> 48) return set_err(ctx, LDPC_EINVAL, "pointer above 2^48");
+  if (ctx->ring_frames + B >= ((int64_t)1 << 31))
+    return set_err(ctx, LDPC_EINVAL, "a frame ring session takes < 2^31 frames: end it and begin anew");
+  return ring_post_impl(ctx, d_in, cw_stride, B, d_out_packed, d_iters_used_opt, d_syn_weight_opt, 0);
+}
+
+int ldpc_ring_wait(ldpc_ctx *ctx, int64_t batch) {
+  if (!ctx) return LDPC_EINVAL;
+  if (batch < 0 || (uint64_t)batch >= ctx->ring_next)
+    return set_err(ctx, LDPC_EINVAL, "no such batch in this session");
+  return ring_wait_impl(ctx, (uint64_t)batch);
+}
+
+int ldpc_ring_end(ldpc_ctx *ctx) {
+  if (!ctx) return LDPC_EINVAL;
+  if (!ctx->ring_on) return LDPC_OK;
+  ctx->ring_on = false;
+  const int64_t q = ring_post_impl(ctx, nullptr, 0, 0, nullptr, nullptr, nullptr, 1);
+  if (q < 0) return (int)q;
+  // work the caller enqueues on its stream from now on follows the launch
+  const hipError_t e = hipStreamWaitEvent((hipStream_t)ctx->ring_user_stream, ctx->ring_ev, 0);
+  return e == hipSuccess ? LDPC_OK : hip_err(ctx, e, "frame ring: stream order");
+}
+
+int ldpc_ring_info(const ldpc_ctx *ctx, int *launches_out, int *workgroups_out) {
+  if (!ctx) return LDPC_EINVAL;
+  if (launches_out) *launches_out = ctx->ring_launches;
+  if (workgroups_out) *workgroups_out = ctx->ring_workgroups;
+  return LDPC_OK;
+}
+
+int ldpc_test_hook(ldpc_ctx *ctx, int op, int64_t arg) {
+  if (!ctx) return LDPC_EINVAL;
+  switch (op) {
+    case LDPC_TEST_SERVE_UNCHECKED:
+      ctx->srv_test_skip_check = true;
+      return LDPC_OK;
+    case LDPC_TEST_SERVE_EPOCH:
+      // epochs only grow within a session (a launch serves epochs above its start)
+      if (arg < (int64_t)ctx->srv_epoch || arg >= (int64_t)ldpc::kServeEpochLimit)
+        return set_err(ctx, LDPC_EINVAL, "epoch must be in [current, kServeEpochLimit)");
+      ctx->srv_epoch = (uint32_t)arg;
+      return LDPC_OK;
+    case LDPC_TEST_SERVE_EPOCH_NOW:
+      return (int)ctx->srv_epoch;
+    default:
+      return set_err(ctx, LDPC_EINVAL, "unknown test hook");
+  }
 }
 
 int ldpc_decode_windows(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,

@@ -155,6 +155,7 @@ struct WaveTables {
 struct FrameResult {
   int weight;
   uint32_t byte;
+  int used;  // iterations executed
 };
 // FAIR = false: a build that never manages issue priority (the throughput
 // build: fair_cycles is 0 there), so the clock reads and the state they need
@@ -734,7 +735,7 @@ __device__ __forceinline__ FrameResult decode_frame(const CodeView &code, const 
   }
   // the next frame's rb writes must not overtake this frame's LDS reads
   wave_lds_sync();
-  return FrameResult{weight, o};
+  return FrameResult{weight, o, used};
 }
 
 // Frame b's first sample and polarity (DecodeArgs::pm_half: the second half

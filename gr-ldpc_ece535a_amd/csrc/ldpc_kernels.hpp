@@ -135,10 +135,60 @@ struct alignas(16) ServeArgs {
   uint32_t session;       // this launch's session id (the host's count of launches)
   int blocks_per_cu;      // decoder workgroups per CU (capped by occupancy; 0: occupancy)
   int debug;              // LDPC_SERVE_DEBUG: counters in ctl words 24..28
+  // samples of the staged span (DecodeArgs::in): every key is checked on the
+  // device, (key >> 1) + N <= span, before its window is gathered
+  int64_t span;
 };
+// Result granules that carry no decode: the syndrome-weight field (9 bits,
+// a real weight is <= M <= 256) says why.  The host turns either into an
+// error of the round.
+constexpr uint32_t kServeBadKey = 511;   // the key's window is outside the staged span
+constexpr uint32_t kServeLostKey = 510;  // the key never showed the round's tag (deadline)
+// Epochs stay below this (the host restarts a session before it); a round's
+// result tag is epoch mod 2^23.
+constexpr uint32_t kServeEpochLimit = (1u << 23) - (1u << 16);
 // *workgroups_out: the launch's decoder workgroups
 int launch_serve(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, int method,
-                 int prec, int slots, int nw, void *stream, int *workgroups_out);
+                 int prec, int slots, int nw, int device, void *stream, int *workgroups_out);
+
+// ---------------------------------------------------------------------------
+// The frame ring (ldpc_ring.hip, ldpc_ring_*): ONE persistent launch decodes
+// every batch posted to it.  Frames of all posted batches form one queue
+// (global tickets: batch q's frame f is ticket start_q + f), so a wave that
+// ends a short frame takes the next one whatever batch it belongs to -- no
+// SIMD idles at a batch's end waiting for its longest frames.
+// The host writes batch q's descriptor into slot q % kRingSlots of mapped
+// host memory, `seq` (= q + 1) last; the launch's last wave to finish one of
+// the batch's frames writes comp[slot] = q + 1.  Outputs are stored
+// write-through (sc1), so a batch's outputs are in memory when its comp word
+// is.  A slot is reused only once its batch is complete.
+// ---------------------------------------------------------------------------
+constexpr int kRingSlots = 256;
+struct alignas(64) RingDesc {
+  uint64_t seq;          // q + 1 once posted (written last)
+  int64_t start;         // ticket of the batch's frame 0
+  const float *in;       // frame f at in + f * cw_stride (elem_stride 1, polarity +1)
+  int64_t cw_stride;
+  uint8_t *packed;       // B x KB
+  int32_t *iters;        // B (optional)
+  int32_t *synd;         // B (optional)
+  int32_t B;             // 0 with quit
+  int32_t quit;          // 1: the launch ends at this batch (every later ticket)
+};
+struct RingArgs {
+  const RingDesc *desc;  // host-mapped, kRingSlots
+  uint64_t *comp;        // host-mapped, kRingSlots completion words
+  uint32_t *done;        // device, frames finished per slot (one 256-byte line each)
+  uint32_t *ticket;      // device queue head (zeroed before the launch)
+  uint64_t *mirror;      // device copies of the descriptor lines (zeroed before the launch)
+  int64_t ticket0;       // ticket of the launch's first frame
+  uint64_t cursor0;      // the launch's first batch (seq - 1)
+  uint64_t deadline;     // 100 MHz ticks without a posted batch before a wave leaves
+  int max_iters, et_period;
+};
+constexpr int kRingDoneStride = 64;  // u32 words between two slots' done counters
+int launch_ring(const CodeView &code, const RingArgs &r, int method, int prec, int slots, int nw,
+                int device, void *stream, int *workgroups_out);
 
 // Launch one decode (host side, implemented in ldpc_kernels.hip).
 // method: 0 min-sum, 1 sum-product, 2 bit-flip, 3 hard; prec 0 f64, 1 f32;

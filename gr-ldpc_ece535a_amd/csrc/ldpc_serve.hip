@@ -34,6 +34,8 @@
 // with one system-scope 8-byte store per window, and hands the round word to
 // the decoders as one agent-scope (sc1) granule polled with sc1 loads
 // (MI355X_MICROARCH.md, inter-workgroup visibility, R2).
+#include <atomic>
+
 #include "ldpc_frame.hpp"
 
 namespace ldpc {
@@ -77,6 +79,14 @@ constexpr int64_t kInlineKeys = 15 * kServeCopies;
 __device__ __forceinline__ uint64_t *key_slot(const ServeArgs &s, int64_t b) {
   return b < kInlineKeys ? s.ctl + 16 * (b % kServeCopies) + 1 + b / kServeCopies
                          : (uint64_t *)s.dkeys + b;
+}
+// Why a window key must not be gathered (0: it may): no key of this round
+// (-1), or a window that reaches past the staged span.  Every decoder checks
+// before its gather, whatever the host checked: a persistent kernel that
+// polls host memory must not be able to fault on a bad or stale key.
+__device__ __forceinline__ uint32_t key_fault(int64_t key, int N, int64_t span) {
+  if (key < 0) return kServeLostKey;
+  return (key >> 1) + N > span ? kServeBadKey : 0u;
 }
 __device__ __forceinline__ uint32_t *census_word(uint64_t *ctl) {
   return reinterpret_cast<uint32_t *>(ctl + 16 * kServeCopies);
@@ -160,8 +170,10 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
 #pragma unroll
         for (int j = 0; j < kKeyLoads; ++j) {
           const int64_t b = c + 64 * j + lane;
-          while (!lost && __ballot(in[j] && (k[j] >> 40) != tag)) {
-            if (in[j] && (k[j] >> 40) != tag) k[j] = sys_load((const uint64_t *)s.keys + b);
+          // (an older tag is read again; a later round's -- the host gave this
+          // round up -- is passed on, and the decoders answer it as lost)
+          while (!lost && __ballot(in[j] && (k[j] >> 40) < tag)) {
+            if (in[j] && (k[j] >> 40) < tag) k[j] = sys_load((const uint64_t *)s.keys + b);
             if (ticks() - t_keys > s.deadline) lost = true;
           }
           if (in[j]) agent_store(key_slot(s, b), k[j]);
@@ -285,18 +297,15 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
         // slower (profiles/round5/serve_pollers_ab.txt)
         __builtin_amdgcn_s_sleep(6);
       }
-      // the workgroup form's key: tagged with the round's epoch (see key_slot)
+      // the workgroup form's key: tagged with the round's epoch (see key_slot).
+      // A slot that still holds an older tag is read again; one that never
+      // shows this round's tag within the deadline, or already shows a later
+      // round's, yields no key (-1: a kServeLostKey granule, no gather).
       if (r != kQuitRound && g < (int64_t)(r & 0xFFFFFu) && (int64_t)(r & 0xFFFFFu) <= (int64_t)((r >> 20) & 0xFFFFFu)) {
         const uint64_t ktag = (r >> 40) & 0xFFFFFFu;
         const uint64_t t_k = ticks();
-        while ((k >> 40) != ktag) {
-          if (ticks() - t_k > s.deadline) {  // the host is gone
-            r = kQuitRound;
-            break;
-          }
-          k = agent_load(my_key);
-        }
-        sslot[1] = (int64_t)(k & ((1ull << 40) - 1));
+        while ((k >> 40) < ktag && ticks() - t_k <= s.deadline) k = agent_load(my_key);
+        sslot[1] = (k >> 40) == ktag ? (int64_t)(k & ((1ull << 40) - 1)) : -1;
       }
       sslot[0] = (int64_t)r;
     }
@@ -320,42 +329,55 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
           if (s.debug && (g & 63) == 0) dbg_max(diag(s.ctl, kDiagKey), ticks());
         }
         __syncthreads();  // (mw_frame's first barrier orders the key's readers)
-        const int64_t key = sslot[1];
-        uint64_t hard[NW];
-        Real post[NW];
-        int used = 0;
-        const int weight = mw_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a.max_iters, 1, mt, mtb, meb, mrb,
-                                                         msb, logtab, a.in + (key >> 1),
-                                                         (key & 1) ? -1.0f : 1.0f, 1, hard, post,
-                                                         used);
-        (void)post;
-        if (wave == 0) {  // packed bytes M.. (:207-219), then the granule
-          const uint32_t o = mw_packed_byte<NW>(code, hard, lane);
-          uint32_t pk = 0;
+        const int64_t key = sslot[1];  // (workgroup-uniform)
+        const uint32_t why = key_fault(key, code.N, s.span);
+        if (why) {
+          if (tid == 0) sys_store(s.res + g, tag | ((uint64_t)why << 32));
+        } else {
+          uint64_t hard[NW];
+          Real post[NW];
+          int used = 0;
+          const int weight = mw_frame<PREC, METHOD, S, NW, DCN, DVN>(code, a.max_iters, 1, mt, mtb, meb, mrb,
+                                                           msb, logtab, a.in + (key >> 1),
+                                                           (key & 1) ? -1.0f : 1.0f, 1, hard, post,
+                                                           used);
+          (void)post;
+          if (wave == 0) {  // packed bytes M.. (:207-219), then the granule
+            const uint32_t o = mw_packed_byte<NW>(code, hard, lane);
+            uint32_t pk = 0;
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            pk |= ((uint32_t)__builtin_amdgcn_readlane((int)o, j) & 255u) << (8 * j);
-          if (lane == 0) {
-            sys_store(s.res + g, tag | ((uint64_t)(uint32_t)weight << 32) | pk);
-            if (s.debug && (g & 63) == 0) {
-              dbg_add(diag(s.ctl, kDiagResults));
-              dbg_max(diag(s.ctl, kDiagDone), ticks());
+            for (int j = 0; j < 4; ++j)
+              pk |= ((uint32_t)__builtin_amdgcn_readlane((int)o, j) & 255u) << (8 * j);
+            if (lane == 0) {
+              sys_store(s.res + g, tag | ((uint64_t)(uint32_t)weight << 32) | pk);
+              if (s.debug && (g & 63) == 0) {
+                dbg_add(diag(s.ctl, kDiagResults));
+                dbg_max(diag(s.ctl, kDiagDone), ticks());
+              }
             }
           }
+          wave_lds_sync();
         }
-        wave_lds_sync();
       }
     } else {
       // one window per wave
       const int64_t W = G * S;
       for (int64_t b = g * S + wave; b < (int64_t)B && g < G; b += W) {
-        // the key, once it carries this round's tag (bounded: a host that is
-        // gone leaves a stale key, decoded into a result nobody reads)
+        // the key, once it carries this round's tag: an older tag is read
+        // again (bounded); a key that never shows this round's tag is not
+        // decoded (a kServeLostKey granule), nor is one outside the span
+        // (kServeBadKey) -- no gather ever uses a key the checks did not pass
+        const uint64_t ktag = ep & 0xFFFFFFu;
         uint64_t kk = wave_uniform(agent_load(key_slot(s, b)));
         const uint64_t t_k = ticks();
-        while ((kk >> 40) != (ep & 0xFFFFFFu) && ticks() - t_k < s.deadline)
+        while ((kk >> 40) < ktag && ticks() - t_k <= s.deadline)
           kk = wave_uniform(agent_load(key_slot(s, b)));
-        const int64_t key = (int64_t)(kk & ((1ull << 40) - 1));
+        const int64_t key = (kk >> 40) == ktag ? (int64_t)(kk & ((1ull << 40) - 1)) : -1;
+        const uint32_t why = key_fault(key, code.N, s.span);
+        if (why) {
+          if (lane == 0) sys_store(s.res + b, tag | ((uint64_t)why << 32));
+          continue;
+        }
         const float *src = a.in + (key >> 1);
         const float sgn = (key & 1) ? -1.0f : 1.0f;
         float xin[NW];
@@ -389,24 +411,31 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
   }
 }
 
-int cus_of_device() {
-  static int cus_of[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cus_of[dev] &&
-      hipDeviceGetAttribute(&cus_of[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus_of[dev] = 256;
-  return cus_of[dev];
+// CUs of the context's device (not the calling thread's current one: the
+// block relaunches a server from its own thread)
+int cus_of_device(int dev) {
+  static std::atomic<int> cus_of[64];
+  if (dev < 0 || dev >= 64) return 256;
+  int n = cus_of[dev].load(std::memory_order_relaxed);
+  if (!n) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+    cus_of[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
 }
 
 template <int PREC, int METHOD, int S, int NW, int DCN, int DVN>
-int launch_s(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, hipStream_t st,
-             int *wg) {
+int launch_s(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, int device,
+             hipStream_t st, int *wg) {
   typedef typename Math<PREC>::Real Real;
   // the two forms' LDS, overlaid
   const size_t lds = serve_lds_main<Real, METHOD, S, NW, DVN>();
   const void *fn = (const void *)serve_kernel<PREC, METHOD, S, NW, DCN, DVN>;
-  static int per_cu = 0;  // resident decoder workgroups per CU
+  // resident decoder workgroups per CU (the same on every MI355X of a box;
+  // computed once, racing threads compute the same value)
+  static std::atomic<int> per_cu_once{0};
+  int per_cu = per_cu_once.load(std::memory_order_relaxed);
   if (!per_cu) {
     if (lds > 65536 &&
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
@@ -419,9 +448,10 @@ int launch_s(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, hipS
     // only start once the launch ends, and rounds go to the decoders that
     // started (the census), so this is a speed matter only
     per_cu = std::min(n, 4 * kServeWavesPerSimd / S);
+    per_cu_once.store(per_cu, std::memory_order_relaxed);
   }
   const int blocks = (s.blocks_per_cu > 0 ? std::min(per_cu, s.blocks_per_cu) : per_cu) *
-                     cus_of_device();
+                     cus_of_device(device);
   *wg = blocks - 1;
   hipLaunchKernelGGL((serve_kernel<PREC, METHOD, S, NW, DCN, DVN>), dim3((unsigned)blocks),
                      dim3(64 * S), lds, st, code, a, s);
@@ -430,51 +460,51 @@ int launch_s(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, hipS
 
 template <int PREC, int METHOD, int NW>
 int serve_slots(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, int slots,
-                hipStream_t st, int *wg) {
+                int dev, hipStream_t st, int *wg) {
   // low-degree codes (the reference's H) get loops sized to their degrees, as
   // the batch kernels (ldpc_kernels.hip launch_slots)
   if constexpr (NW == 1) {
     if (code.dc_max <= 6 && code.dv_max <= 3) switch (slots) {
-        case 1: return launch_s<PREC, METHOD, 1, NW, 5, 3>(code, a, s, st, wg);
-        case 2: return launch_s<PREC, METHOD, 2, NW, 5, 3>(code, a, s, st, wg);
-        case 3: return launch_s<PREC, METHOD, 3, NW, 5, 3>(code, a, s, st, wg);
-        case 4: return launch_s<PREC, METHOD, 4, NW, 5, 3>(code, a, s, st, wg);
+        case 1: return launch_s<PREC, METHOD, 1, NW, 5, 3>(code, a, s, dev, st, wg);
+        case 2: return launch_s<PREC, METHOD, 2, NW, 5, 3>(code, a, s, dev, st, wg);
+        case 3: return launch_s<PREC, METHOD, 3, NW, 5, 3>(code, a, s, dev, st, wg);
+        case 4: return launch_s<PREC, METHOD, 4, NW, 5, 3>(code, a, s, dev, st, wg);
         default: break;
       }
   }
   constexpr int D = kDcMax - 1, V = kDvMax;
   switch (slots) {
-    case 1: return launch_s<PREC, METHOD, 1, NW, D, V>(code, a, s, st, wg);
-    case 2: return launch_s<PREC, METHOD, 2, NW, D, V>(code, a, s, st, wg);
-    case 3: return launch_s<PREC, METHOD, 3, NW, D, V>(code, a, s, st, wg);
-    case 4: return launch_s<PREC, METHOD, 4, NW, D, V>(code, a, s, st, wg);
+    case 1: return launch_s<PREC, METHOD, 1, NW, D, V>(code, a, s, dev, st, wg);
+    case 2: return launch_s<PREC, METHOD, 2, NW, D, V>(code, a, s, dev, st, wg);
+    case 3: return launch_s<PREC, METHOD, 3, NW, D, V>(code, a, s, dev, st, wg);
+    case 4: return launch_s<PREC, METHOD, 4, NW, D, V>(code, a, s, dev, st, wg);
     default: return -2;  // workgroups of more than 4 waves: launches
   }
 }
 
 template <int NW>
 int serve_nw(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, int method, int prec,
-             int slots, hipStream_t st, int *wg) {
+             int slots, int dev, hipStream_t st, int *wg) {
   if (method == 1) {
-    if (prec == 1) return serve_slots<1, 1, NW>(code, a, s, slots, st, wg);
-    if (prec == 2) return serve_slots<2, 1, NW>(code, a, s, slots, st, wg);
-    if (prec == 3) return serve_slots<3, 1, NW>(code, a, s, slots, st, wg);
-    return serve_slots<0, 1, NW>(code, a, s, slots, st, wg);
+    if (prec == 1) return serve_slots<1, 1, NW>(code, a, s, slots, dev, st, wg);
+    if (prec == 2) return serve_slots<2, 1, NW>(code, a, s, slots, dev, st, wg);
+    if (prec == 3) return serve_slots<3, 1, NW>(code, a, s, slots, dev, st, wg);
+    return serve_slots<0, 1, NW>(code, a, s, slots, dev, st, wg);
   }
   if (method == 0)  // min-sum: both f64 modes are the same arithmetic
-    return prec == 1 ? serve_slots<1, 0, NW>(code, a, s, slots, st, wg)
-                     : serve_slots<0, 0, NW>(code, a, s, slots, st, wg);
+    return prec == 1 ? serve_slots<1, 0, NW>(code, a, s, slots, dev, st, wg)
+                     : serve_slots<0, 0, NW>(code, a, s, slots, dev, st, wg);
   return -2;
 }
 
 }  // namespace
 
 int launch_serve(const CodeView &code, const DecodeArgs &a, const ServeArgs &s, int method,
-                 int prec, int slots, int nw, void *stream, int *workgroups_out) {
+                 int prec, int slots, int nw, int device, void *stream, int *workgroups_out) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (code.KB > 4 || s.start_epoch >= (1u << 23) - (1u << 16)) return -2;
-  if (nw == 1) return serve_nw<1>(code, a, s, method, prec, slots, st, workgroups_out);
-  if (nw == 4) return serve_nw<4>(code, a, s, method, prec, slots, st, workgroups_out);
+  if (code.KB > 4 || s.start_epoch >= kServeEpochLimit) return -2;
+  if (nw == 1) return serve_nw<1>(code, a, s, method, prec, slots, device, st, workgroups_out);
+  if (nw == 4) return serve_nw<4>(code, a, s, method, prec, slots, device, st, workgroups_out);
   return -2;
 }
 

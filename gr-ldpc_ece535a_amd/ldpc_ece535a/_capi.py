@@ -19,6 +19,8 @@ PREC_F64, PREC_F32, PREC_F64_LIBM, PREC_F64_FAST = 0, 1, 2, 3
 FLAG_NO_REORDER = 1
 FLAG_GRAPH = 2
 FLAG_PLAIN_LAYOUT = 4
+TEST_SERVE_UNCHECKED, TEST_SERVE_EPOCH, TEST_SERVE_EPOCH_NOW = 1, 2, 3
+SERVE_EPOCH_LIMIT = (1 << 23) - (1 << 16)
 PATH_SMALL, PATH_GRAPH = 0, 1
 MODE_LATENCY, MODE_THROUGHPUT = 0, 1
 ERRORS = {0: "LDPC_OK", -1: "LDPC_EINVAL", -2: "LDPC_EUNSUPPORTED", -3: "LDPC_EDEVICE",
@@ -76,6 +78,12 @@ SIGNATURES = {
     "ldpc_set_schedule": (_i, [_vp, _i]),
     "ldpc_set_frame_order": (_i, [_vp, _i]),
     "ldpc_synchronize": (_i, [_vp]),
+    "ldpc_test_hook": (_i, [_vp, _i, _i64]),
+    "ldpc_ring_begin": (_i, [_vp, _i, _i, _i, _i, _vp]),
+    "ldpc_ring_post": (_i64, [_vp, _vp, _i64, _i, _vp, _vp, _vp]),
+    "ldpc_ring_wait": (_i, [_vp, _i64]),
+    "ldpc_ring_end": (_i, [_vp]),
+    "ldpc_ring_info": (_i, [_vp, _i32p, _i32p]),
 }
 
 _lib = None
@@ -355,6 +363,42 @@ class Decoder:
         arr = (ctypes.c_void_p * int(n))()
         _check(lib().ldpc_ctx_streams(self._ctx, int(n), arr), self._ctx)
         return [int(x) for x in arr]
+
+    def ring_begin(self, method=METHOD_SUMPRODUCT, max_iters=50, et_period=1,
+                   precision=PREC_F64, stream=None):
+        """ldpc_ring_begin: open a frame-ring session (one persistent launch for
+        every batch posted until ring_end), after the work on `stream`."""
+        _check(lib().ldpc_ring_begin(self._ctx, int(method), int(max_iters), int(et_period),
+                                     int(precision), stream), self._ctx)
+
+    def ring_post(self, d_in, B, d_packed, d_iters=None, d_synd=None, cw_stride=None):
+        """ldpc_ring_post: post B device-resident frames (raw pointers); returns
+        the batch id."""
+        if cw_stride is None:
+            cw_stride = self.N
+        ptr = lambda x: None if x is None else int(x)  # noqa: E731
+        return _check(lib().ldpc_ring_post(self._ctx, ptr(d_in), int(cw_stride), int(B),
+                                           ptr(d_packed), ptr(d_iters), ptr(d_synd)), self._ctx)
+
+    def ring_wait(self, batch):
+        """ldpc_ring_wait: return once batch `batch` is complete."""
+        _check(lib().ldpc_ring_wait(self._ctx, int(batch)), self._ctx)
+
+    def ring_end(self):
+        """ldpc_ring_end: end the session (work enqueued on the session's
+        stream afterwards follows its last batch)."""
+        _check(lib().ldpc_ring_end(self._ctx), self._ctx)
+
+    def ring_info(self):
+        """ldpc_ring_info: {launches, workgroups} of this context's ring."""
+        a, b = ctypes.c_int32(0), ctypes.c_int32(0)
+        _check(lib().ldpc_ring_info(self._ctx, ctypes.byref(a), ctypes.byref(b)), self._ctx)
+        return {"launches": a.value, "workgroups": b.value}
+
+    def test_hook(self, op, arg=0):
+        """ldpc_test_hook (test seam): TEST_SERVE_UNCHECKED, TEST_SERVE_EPOCH,
+        TEST_SERVE_EPOCH_NOW."""
+        return _check(lib().ldpc_test_hook(self._ctx, int(op), int(arg)), self._ctx)
 
     def serve_end(self):
         _check(lib().ldpc_serve_end(self._ctx), self._ctx)

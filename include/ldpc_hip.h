@@ -276,6 +276,23 @@ int ldpc_serve_windows(ldpc_ctx *ctx, const int64_t *windows, int B, uint8_t *ou
                        int32_t *syn_weight_opt);
 int ldpc_serve_end(ldpc_ctx *ctx);
 
+/* Test seams (tests/test_gpu_serve.py; not for production callers).
+ *   LDPC_TEST_SERVE_UNCHECKED  the next ldpc_serve_windows call skips the host's
+ *                              check of its keys against the staged span, so the
+ *                              device's own check is what refuses a bad key: its
+ *                              window is not gathered, the call returns
+ *                              LDPC_EDEVICE and the server keeps serving
+ *   LDPC_TEST_SERVE_EPOCH      sets the server's round counter to arg (not below
+ *                              its current value, below 2^23 - 2^16), so that the
+ *                              restart of a session that reaches the limit can be
+ *                              tested without 8 million rounds
+ *   LDPC_TEST_SERVE_EPOCH_NOW  returns the round counter
+ * Returns LDPC_OK (or the counter) or a negative code. */
+#define LDPC_TEST_SERVE_UNCHECKED 1
+#define LDPC_TEST_SERVE_EPOCH 2
+#define LDPC_TEST_SERVE_EPOCH_NOW 3
+int ldpc_test_hook(ldpc_ctx *ctx, int op, int64_t arg);
+
 /* Device-resident buffers (already in HBM); enqueues on `hip_stream`
  * (hipStream_t, NULL = the context's own stream) and returns without
  * synchronising -- except min-sum on a large-code context, whose pass loop
@@ -291,6 +308,47 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
                        int B, uint8_t *d_out_packed, uint8_t *d_out_bits_opt,
                        int32_t *d_iters_used_opt, int32_t *d_syn_weight_opt,
                        float *d_llr_out_opt, void *hip_stream);
+
+/* The frame ring: ONE persistent launch decodes every batch posted to it
+ * (small codes; min-sum and sum-product, any precision).  The frames of all
+ * posted batches form one device queue, so a wave that finishes a frame of
+ * batch q takes the next frame whatever batch it belongs to: no SIMD waits at
+ * a batch's end for the batch's longest frames (reference: every decode is
+ * one frame's call, lib/ldpc_decoder_cb_impl.cc:155-164, with the per-frame
+ * early exit :535-537 / :406-408 that makes frames differ in length).
+ *   ldpc_ring_begin  opens a session for (method, max_iters, et_period,
+ *                    precision) and starts the launch on the context's ring
+ *                    stream, after the work enqueued on hip_stream so far
+ *                    (NULL: the context's stream).  One session per context.
+ *   ldpc_ring_post   posts a batch of B device-resident frames (frame b at
+ *                    d_in + b*cw_stride, elem_stride 1, polarity +1) with its
+ *                    device outputs as ldpc_decode_device; returns the batch's
+ *                    id (>= 0, consecutive from 0 per session) or a negative
+ *                    code.  The input must be in device memory when the call
+ *                    is made, and must stay unchanged until the batch is
+ *                    complete.  Returns at once, except when 256 batches are
+ *                    outstanding: it then waits for the oldest.
+ *   ldpc_ring_wait   returns when batch `batch` is complete: its outputs are
+ *                    in device memory (stored write-through), visible to
+ *                    copies and kernels started after the call.
+ *   ldpc_ring_end    ends the session without waiting: work enqueued on
+ *                    hip_stream of ldpc_ring_begin after this call runs after
+ *                    the last batch.
+ *   ldpc_ring_info   launches made by this context's ring (a launch whose
+ *                    waves found no batch for 50 ms ends; the next post or
+ *                    wait starts another from the first incomplete batch) and
+ *                    the last launch's workgroups.
+ * Results equal ldpc_decode_device's for the same frames (the same
+ * arithmetic).  Outputs iters/synd are optional (NULL).  LDPC_ETIMEOUT when a
+ * wait passes 10 s. */
+int ldpc_ring_begin(ldpc_ctx *ctx, int method, int max_iters, int et_period, int precision,
+                    void *hip_stream);
+int64_t ldpc_ring_post(ldpc_ctx *ctx, const float *d_in, int64_t cw_stride, int B,
+                       uint8_t *d_out_packed, int32_t *d_iters_used_opt,
+                       int32_t *d_syn_weight_opt);
+int ldpc_ring_wait(ldpc_ctx *ctx, int64_t batch);
+int ldpc_ring_end(ldpc_ctx *ctx);
+int ldpc_ring_info(const ldpc_ctx *ctx, int *launches_out, int *workgroups_out);
 
 /* The context's in-flight streams (hipStream_t) for callers that keep
  * several ldpc_decode_device calls in flight (LDPC_MODE_THROUGHPUT): n

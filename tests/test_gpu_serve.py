@@ -122,3 +122,58 @@ def test_serve_errors():
     with pytest.raises(L.LdpcError):  # bit-flip: launches only
         dec.serve_begin(method=2, max_iters=5, max_windows=16)
     dec.close()
+
+
+def test_serve_device_refuses_out_of_span_key():
+    """The device checks every key against the staged span before it gathers
+    (ldpc_serve.hip key_fault): a key past the span, let through the host's
+    own check by the test seam, comes back as an error of the round -- not an
+    illegal memory access -- in both the workgroup form (a round of a few
+    windows) and the one-wave form (a round of more windows than decoders),
+    and the server goes on serving correct rounds."""
+    from ldpc_ece535a._capi import TEST_SERVE_UNCHECKED
+    dec = L.Decoder()
+    Hr = dec.H
+    s = _span(Hr, 300, 31)
+    rng = np.random.default_rng(9)
+    dec.stage_span(s, max_windows=8192)
+    dec.serve_begin(method=1, max_iters=5, max_windows=8192)
+    far = (int(s.size) + (1 << 30)) << 1  # ~4 GB past the span's end
+    for n in (3, 6000):
+        w = _windows(rng, n, s.size, dec.N)
+        w[n // 2] = far
+        w[-1] = (s.size - dec.N + 1) << 1  # one sample past the end
+        dec.test_hook(TEST_SERVE_UNCHECKED)
+        with pytest.raises(L.LdpcError, match="LDPC_EDEVICE.*outside the staged span"):
+            dec.serve_windows(w)
+        good = _windows(rng, n, s.size, dec.N)
+        g = dec.serve_windows(good)
+        ref = _oracle(1, Hr, s, good, 5)
+        assert (g["packed"] == ref["packed"]).all() and (g["synd"] == ref["synd"]).all()
+    dec.serve_end()
+    dec.close()
+
+
+def test_serve_epoch_limit_restarts_the_session():
+    """Round epochs stay below 2^23 - 2^16 (result tags are epoch mod 2^23):
+    a session that reaches the limit is ended and started over before its
+    next round, and every round's results stay right across it."""
+    from ldpc_ece535a._capi import (SERVE_EPOCH_LIMIT, TEST_SERVE_EPOCH,
+                                    TEST_SERVE_EPOCH_NOW)
+    dec = L.Decoder()
+    Hr = dec.H
+    s = _span(Hr, 200, 41)
+    rng = np.random.default_rng(10)
+    dec.stage_span(s, max_windows=1024)
+    dec.serve_begin(method=0, max_iters=5, max_windows=1024)
+    dec.test_hook(TEST_SERVE_EPOCH, SERVE_EPOCH_LIMIT - 6)
+    seen = []
+    for n in (1, 700, 5, 64, 1, 300, 2, 9):
+        w = _windows(rng, n, s.size, dec.N)
+        g = dec.serve_windows(w)
+        seen.append(dec.test_hook(TEST_SERVE_EPOCH_NOW))
+        ref = _oracle(0, Hr, s, w, 5)
+        assert (g["packed"] == ref["packed"]).all() and (g["synd"] == ref["synd"]).all()
+    dec.serve_end()
+    dec.close()
+    assert max(seen) < SERVE_EPOCH_LIMIT and min(seen) < 16  # it restarted
