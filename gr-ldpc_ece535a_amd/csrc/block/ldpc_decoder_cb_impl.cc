@@ -220,15 +220,11 @@ ldpc_decoder_cb_impl::ldpc_decoder_cb_impl(int method, int iterations, ldpc_bloc
 }
 
 int ldpc_decoder_cb_impl::Stager::run() {
-  const int r = ldpc_stage_span(ctx, in, n, 2, max_windows);
-  serve_rc = LDPC_EUNSUPPORTED;
-  if (r == LDPC_OK && serve) serve_rc = ldpc_serve_begin(ctx, method, iterations, precision, max_windows);
-  return r;
+  return ldpc_stage_span(ctx, in, n, 2, max_windows);
 }
 
 void ldpc_decoder_cb_impl::stage_async(const float *in, int64_t n_floats, int max_windows) {
   Stager &sg = d_stager;
-  const bool serve = d_serve && d_serve_mode == 1 && (d_method == 0 || d_method == 1);
   if (!sg.th.joinable())
     sg.th = std::thread([&sg]() {
       std::unique_lock<std::mutex> lk(sg.mu);
@@ -248,10 +244,6 @@ void ldpc_decoder_cb_impl::stage_async(const float *in, int64_t n_floats, int ma
   sg.in = in;
   sg.n = n_floats;
   sg.max_windows = max_windows;
-  sg.serve = serve;
-  sg.method = d_method;
-  sg.iterations = (int)d_iterations;
-  sg.precision = d_precision;
   sg.busy = true;
   sg.cv.notify_all();
 }
@@ -261,11 +253,6 @@ int ldpc_decoder_cb_impl::stage_wait() {
   {
     std::unique_lock<std::mutex> lk(sg.mu);
     sg.cv.wait(lk, [&sg]() { return !sg.busy; });
-  }
-  if (sg.rc == LDPC_OK && sg.serve) {
-    d_serving = sg.serve_rc == LDPC_OK;
-    if (sg.serve_rc == LDPC_EUNSUPPORTED) d_serve = false;  // this code / method: launches
-    else if (sg.serve_rc < 0) return sg.serve_rc;
   }
   return sg.rc;
 }
@@ -325,7 +312,7 @@ void ldpc_decoder_cb_impl::decode_wanted(const float *in, int nin, bool first, b
       i = j;
     }
   } else {
-    const bool small = d_serve && (d_serve_mode == 1 || (int64_t)B * d_iterations <= kServeWork);
+    const bool small = d_serve && (int64_t)B * d_iterations <= kServeWork;
     if (small && !d_serving) serve_start();
     if (small && d_serving) {
       const int rc = ldpc_serve_windows(d_ctx, d_want.data(), B, packed, synd);

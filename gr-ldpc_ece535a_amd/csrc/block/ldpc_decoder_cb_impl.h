@@ -58,23 +58,18 @@ class ldpc_decoder_cb_impl : public ldpc_decoder_cb {
     const float *in = nullptr;
     int64_t n = 0;
     int max_windows = 0;
-    bool serve = false;          // start the window server after staging
-    int method = 0, iterations = 0, precision = 0;
-    int serve_rc = 0;            // ldpc_serve_begin's result
-    int run();                   // stage (+ serve); returns the staging result
+    int run();                   // stages the span; returns ldpc_stage_span's result
   } d_stager;
   // How a round of windows is decoded: through the window server
   // (ldpc_serve_*: one persistent launch serves the call's rounds) or by a
   // launch of its own (ldpc_decode_windows).  The server answers a small
   // round sooner; a big one (windows x iterations above kServeWork) runs
   // faster as a launch, with the batch kernels' full throughput
-  // (profiles/round5/serve_latency*.txt).  LDPC_BLOCK_SERVE=0: launches only,
-  // =1: the server for every round (A/B); default: by round size.  Codes or
+  // (profiles/round5/serve_latency*.txt).  LDPC_BLOCK_SERVE=0: launches only
+  // (the A/B of the server); default: by round size.  (The server for every
+  // round, =1 until round 6, was slower in every regime measured.)  Codes or
   // methods the server does not take: launches.
-  int d_serve_mode = !getenv("LDPC_BLOCK_SERVE")           ? 2
-                     : getenv("LDPC_BLOCK_SERVE")[0] == '0' ? 0
-                     : getenv("LDPC_BLOCK_SERVE")[0] == '1' ? 1
-                                                            : 2;
+  int d_serve_mode = getenv("LDPC_BLOCK_SERVE") && getenv("LDPC_BLOCK_SERVE")[0] == '0' ? 0 : 2;
   // windows x iterations of the biggest round the server takes: the
   // crossovers measured at ~700 windows of 5 iterations and ~150 of 50
   // (profiles/round5/serve_latency.txt)

@@ -216,62 +216,6 @@ int launch_gather_windows(const float *span, const int64_t *win, int B, int N, f
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// Longest-first order (ldpc_set_frame_order).  Frames are taken in groups of
-// kOrderGroup (one workgroup each, one thread per frame): a group sorts its
-// frames by (sum |y|, index) -- a bitonic sort in LDS -- and the order
-// interleaves the groups rank by rank: queue positions 0..G-1 hold every
-// group's least reliable frame, the next G their second, and so on (each
-// group is a sample of the batch, so this approximates a global sort at the
-// cost of one short launch).  sum |y| >= 0, so its float bits order as
-// integers (NaN last).  The order only changes when a frame is decoded: its
-// outputs are its own.
-namespace {
-constexpr int kOrderGroup = 256;
-__global__ void __launch_bounds__(kOrderGroup) k_longest_first(const float *in, int64_t cw_stride,
-                                                               int elem_stride, int N, int64_t B,
-                                                               int32_t *order) {
-  __shared__ uint64_t kv[kOrderGroup];
-  const int t = threadIdx.x;
-  const int64_t G = (B + kOrderGroup - 1) / kOrderGroup, g = blockIdx.x;
-  const int64_t f = g * kOrderGroup + t;
-  const int n = (int)min((int64_t)kOrderGroup, B - g * kOrderGroup);  // frames of this group
-  float sabs = 0.0f;
-  if (t < n) {
-    const float *x = in + f * cw_stride;
-    for (int k = 0; k < N; ++k) sabs += fabsf(x[(int64_t)k * elem_stride]);
-  }
-  kv[t] = t < n ? ((uint64_t)__float_as_uint(sabs) << 32) | (uint32_t)t : ~0ull;
-  __syncthreads();
-  for (int k = 2; k <= kOrderGroup; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int p = t ^ j;
-      if (p > t) {
-        const uint64_t x = kv[t], y = kv[p];
-        if ((x > y) == ((t & k) == 0)) {
-          kv[t] = y;
-          kv[p] = x;
-        }
-      }
-      __syncthreads();
-    }
-  if (t >= n) return;
-  // rank t of group g: every group has ranks < nl (nl: the last group's
-  // size), only the G - 1 full groups the ranks past it
-  const int64_t nl = B - (G - 1) * kOrderGroup;
-  const int64_t pos = t < nl ? (int64_t)t * G + g : nl * G + (int64_t)(t - nl) * (G - 1) + g;
-  order[pos] = (int32_t)(g * kOrderGroup + (int64_t)(uint32_t)kv[t]);
-}
-}  // namespace
-
-int launch_longest_first(const float *in, int64_t cw_stride, int elem_stride, int N, int64_t B,
-                         int32_t *order, void *stream) {
-  if (B <= 0) return 0;
-  hipLaunchKernelGGL(k_longest_first, dim3((unsigned)((B + kOrderGroup - 1) / kOrderGroup)),
-                     dim3(kOrderGroup), 0, (hipStream_t)stream, in, cw_stride, elem_stride, N, B,
-                     order);
-  return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
 // Stream concurrency probe (ldpc_ctx_streams): k_probe_wait spins on a flag
 // for at most `deadline` ticks of the 100 MHz clock and records what it saw;
 // k_probe_set raises the flag.  Enqueued on two streams, the wait sees the
@@ -296,6 +240,26 @@ __global__ void __launch_bounds__(64) k_probe_set(uint32_t *flag) {
 
 int launch_probe_touch(uint32_t *flag, void *stream) {
   hipLaunchKernelGGL(k_probe_set, dim3(1), dim3(64), 0, (hipStream_t)stream, flag);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// Device timestamps of one spin (tests): out[0] = the 100 MHz clock when the
+// kernel starts, out[1] when it has spun `ticks` and ends.  Two of them on
+// two streams overlap in time iff the streams run side by side.
+namespace {
+__global__ void __launch_bounds__(64) k_stamp(uint64_t *out, uint64_t ticks) {
+  if (threadIdx.x != 0) return;
+  typedef __attribute__((address_space(1))) uint64_t gu64;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  __hip_atomic_store((gu64 *)out, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu64 *)(out + 1), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace
+
+int launch_stamp(uint64_t *out, uint64_t ticks, void *stream) {
+  hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, (hipStream_t)stream, out, ticks);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -22,17 +22,12 @@ int launch_encode_ira(const int32_t *rp, const int32_t *ci, int M, int K, const 
 int launch_gather_windows(const float *span, const int64_t *win, int B, int N, float *out,
                           void *stream);
 
-// Longest-first frame order of B frames (in + b cw_stride, N samples at
-// elem_stride): groups of 256 frames sorted by ascending sum |y| -- the least
-// reliable first, which tend to need the most iterations -- interleaved rank
-// by rank (ldpc_aux.hip).
-int launch_longest_first(const float *in, int64_t cw_stride, int elem_stride, int N, int64_t B,
-                         int32_t *order, void *stream);
-
 // flag[0] = 0 and flag[1] = 0 beforehand; afterwards flag[1] == 1 iff the two
 // streams ran the pair concurrently (ldpc_aux.hip)
 int launch_probe_pair(uint32_t *flag, uint64_t deadline, void *wait_stream, void *set_stream);
 // one k_probe_set on `stream` (a stream's first launch: see ldpc_ctx_streams)
 int launch_probe_touch(uint32_t *flag, void *stream);
+// out[0..1] = device clock (100 MHz) at the start and end of a `ticks` spin
+int launch_stamp(uint64_t *out, uint64_t ticks, void *stream);
 
 }  // namespace ldpc

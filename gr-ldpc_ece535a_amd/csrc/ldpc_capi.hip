@@ -93,10 +93,11 @@ struct GatherPool {
 };
 
 struct ldpc_ctx {
-  // LDPC_WIN_PROFILE=1: host time split of ldpc_decode_windows, printed by
-  // ldpc_destroy (span staging, window list + launch, wait, result copy)
-  bool win_profile = getenv("LDPC_WIN_PROFILE") != nullptr;
-  bool win_trace = getenv("LDPC_WIN_PROFILE") && getenv("LDPC_WIN_PROFILE")[0] == '2';  // a line per call
+  // LDPC_BLOCK_PROFILE=1: also the host time split of ldpc_decode_windows,
+  // printed by ldpc_destroy (span staging, window list + launch, wait, result
+  // copy); =2 also a line per call
+  bool win_profile = getenv("LDPC_BLOCK_PROFILE") != nullptr;
+  bool win_trace = win_profile && getenv("LDPC_BLOCK_PROFILE")[0] == '2';  // a line per call
   double win_prof[5] = {0, 0, 0, 0, 0};
   long long win_calls = 0, win_windows = 0;
   int M = 0, N = 0, E = 0, K = 0, KB = 0, dc_max = 0, dv_max = 0, dc_min = 0;
@@ -154,8 +155,10 @@ struct ldpc_ctx {
   hipStream_t ring_stream = nullptr;
   hipEvent_t ring_ev = nullptr, ring_user_ev = nullptr;
   void *ring_user_stream = nullptr;
-  uint64_t ring_next = 0;      // the next batch's sequence number
+  uint64_t ring_next = 0;      // the next batch's sequence number (grows across sessions)
   int64_t ring_frames = 0;     // tickets posted so far (the next batch's start)
+  uint64_t ring_first = 0;     // the session's first batch
+  int64_t ring_first_frame = 0;
   int64_t ring_start[ldpc::kRingSlots] = {};  // start ticket of the batch in each slot
   int ring_launches = 0, ring_workgroups = 0;
   // in-flight stream set for throughput callers (ldpc_ctx_streams): streams
@@ -173,11 +176,8 @@ struct ldpc_ctx {
   struct Queue {
     void *stream;
     uint32_t base;  // counter value at the start of the next launch
-    int32_t *order = nullptr;  // longest-first order of the stream's launches (ldpc_set_frame_order)
-    int64_t order_cap = 0;
   };
   std::vector<Queue> queues;
-  int frame_order = 0;  // ldpc_set_frame_order
   // large-code path: the workspace is shared, so launches on a different
   // stream than the previous one first wait for it (graph_done)
   void *graph_stream = nullptr;
@@ -1072,8 +1072,6 @@ void ldpc_destroy(ldpc_ctx *ctx) {
   if (ctx->d_srv_ctl) (void)hipFree(ctx->d_srv_ctl);
   if (ctx->d_srv_keys) (void)hipFree(ctx->d_srv_keys);
   if (ctx->d_tickets) (void)hipFree(ctx->d_tickets);
-  for (auto &qq : ctx->queues)
-    if (qq.order) (void)hipFree(qq.order);
   for (int32_t *p : {ctx->d_rp, ctx->d_ci, ctx->d_cp, ctx->d_ce, ctx->d_cr})
     if (p) (void)hipFree(p);
   for (int32_t *p : ctx->d_msn)
@@ -1323,32 +1321,11 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
               hipSuccess ||
           (e = hipDeviceSynchronize()) != hipSuccess)
         return hip_err(ctx, e, "ticket reset");
-      for (auto &qq : ctx->queues)
-        if (qq.order) (void)hipFree(qq.order);
       ctx->queues.clear();
       q = 0;
     }
     // slots are handed out in order from zeroed memory (creation, reset)
-    ctx->queues.push_back({st, 0u, nullptr, 0});
-  }
-  a.order = nullptr;
-  if (ctx->frame_order == 1 && !d_win && pm_half == 0 && B > 1 && (method == 0 || method == 1)) {
-    ldpc_ctx::Queue &qq = ctx->queues[q];
-    if (qq.order_cap < B) {
-      // grown on the stream's own schedule: earlier launches of this stream
-      // may still read the old buffer
-      if (qq.order && (e = hipStreamSynchronize((hipStream_t)st)) != hipSuccess)
-        return hip_err(ctx, e, "hipStreamSynchronize");
-      if (qq.order) (void)hipFree(qq.order);
-      qq.order = nullptr;
-      qq.order_cap = 0;
-      if ((e = hipMalloc((void **)&qq.order, (size_t)B * sizeof(int32_t))) != hipSuccess)
-        return hip_err(ctx, e, "hipMalloc(frame order)");
-      qq.order_cap = B;
-    }
-    if (ldpc::launch_longest_first(d_in, cw_stride, elem_stride, ctx->N, B, qq.order, st) != 0)
-      return set_err(ctx, LDPC_EDEVICE, "frame order launch failed");
-    a.order = qq.order;
+    ctx->queues.push_back({st, 0u});
   }
   a.ticket = ctx->d_tickets + q * LDPC_TICKET_STRIDE;
   a.ticket_base = ctx->queues[q].base;
@@ -1916,7 +1893,9 @@ constexpr size_t kRingCompOff = sizeof(ldpc::RingDesc) * ldpc::kRingSlots;
 constexpr size_t kRingHostBytes = kRingCompOff + 8 * ldpc::kRingSlots;
 constexpr size_t kRingTicketOff = (size_t)ldpc::kRingSlots * ldpc::kRingDoneStride;  // in u32
 constexpr size_t kRingMirrorOff = 4 * (kRingTicketOff + 64);  // bytes: the descriptor mirror
-constexpr size_t kRingDevBytes = kRingMirrorOff + sizeof(ldpc::RingDesc) * ldpc::kRingSlots;
+constexpr size_t kRingLockOff =
+    kRingMirrorOff + sizeof(ldpc::RingDesc) * ldpc::kRingSlots * ldpc::kRingXcds;
+constexpr size_t kRingDevBytes = kRingLockOff + 8 * ldpc::kRingSlots * ldpc::kRingXcds;
 constexpr uint64_t kRingDeadlineTicks = 5000000;  // 50 ms without a batch: a wave leaves
 constexpr double kRingTimeoutS = 10.0;
 
@@ -1958,6 +1937,7 @@ int ring_launch(ldpc_ctx *ctx, uint64_t cursor, int64_t ticket0) {
   r.done = ctx->d_ring;
   r.ticket = ctx->d_ring + kRingTicketOff;
   r.mirror = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(ctx->d_ring) + kRingMirrorOff);
+  r.lock = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(ctx->d_ring) + kRingLockOff);
   r.ticket0 = ticket0;
   r.cursor0 = cursor;
   r.deadline = kRingDeadlineTicks;
@@ -1987,7 +1967,8 @@ int ring_revive(ldpc_ctx *ctx, uint64_t upto) {
   if (q == hipErrorNotReady) return LDPC_OK;
   if (q != hipSuccess) return hip_err(ctx, q, "frame ring");
   uint64_t first = upto;
-  const uint64_t lo = upto > (uint64_t)ldpc::kRingSlots ? upto - ldpc::kRingSlots : 0;
+  const uint64_t lo = std::max<uint64_t>(
+      ctx->ring_first, upto > (uint64_t)ldpc::kRingSlots ? upto - ldpc::kRingSlots : 0);
   for (uint64_t b = lo; b < upto; ++b)
     if (!ring_done(ctx, b)) {
       first = b;
@@ -2017,7 +1998,7 @@ int ring_wait_impl(ldpc_ctx *ctx, uint64_t q) {
 int64_t ring_post_impl(ldpc_ctx *ctx, const float *d_in, int64_t cw, int B, uint8_t *packed,
                        int32_t *iters, int32_t *synd, int quit) {
   const uint64_t q = ctx->ring_next;
-  if (q >= (uint64_t)ldpc::kRingSlots) {
+  if (q >= ctx->ring_first + ldpc::kRingSlots) {
     const int rc = ring_wait_impl(ctx, q - ldpc::kRingSlots);
     if (rc != LDPC_OK) return rc;
   }
@@ -2112,19 +2093,22 @@ int ldpc_ring_begin(ldpc_ctx *ctx, int method, int max_iters, int et_period, int
   // the previous session's launch has ended before the slots are cleared
   if ((e = hipStreamSynchronize(ctx->ring_stream)) != hipSuccess)
     return hip_err(ctx, e, "hipStreamSynchronize(ring)");
+  // sequence numbers and tickets keep growing across the context's sessions,
+  // so no line a previous session left anywhere (host slots, the device
+  // mirror, a cache) can read as one of this session's batches
   memset(ctx->h_ring, 0, kRingHostBytes);
   ctx->ring_method = method;
   ctx->ring_iters = max_iters;
   ctx->ring_et = et_period;
   ctx->ring_prec = precision;
-  ctx->ring_next = 0;
-  ctx->ring_frames = 0;
+  ctx->ring_first = ctx->ring_next;
+  ctx->ring_first_frame = ctx->ring_frames;
   // the launch follows the work enqueued on the caller's stream so far
   ctx->ring_user_stream = hip_stream ? hip_stream : (void *)ctx->stream;
   if ((e = hipEventRecord(ctx->ring_user_ev, (hipStream_t)ctx->ring_user_stream)) != hipSuccess ||
       (e = hipStreamWaitEvent(ctx->ring_stream, ctx->ring_user_ev, 0)) != hipSuccess)
     return hip_err(ctx, e, "frame ring: stream order");
-  rc = ring_launch(ctx, 0, 0);
+  rc = ring_launch(ctx, ctx->ring_next, ctx->ring_frames);
   if (rc != LDPC_OK) return rc;
   ctx->ring_on = true;
   return LDPC_OK;
@@ -2142,14 +2126,15 @@ int64_t ldpc_ring_post(ldpc_ctx *ctx, const float *d_in, int64_t cw_stride, int 
   for (const void *p : {(const void *)d_in, (const void *)d_out_packed, (const void *)d_iters_used_opt,
                         (const void *)d_syn_weight_opt})
     if ((uintptr_t)p >> 48) return set_err(ctx, LDPC_EINVAL, "pointer above 2^48");
-  if (ctx->ring_frames + B >= ((int64_t)1 << 31))
+  if (ctx->ring_frames - ctx->ring_first_frame + B >= ((int64_t)1 << 31) ||
+      ctx->ring_frames + B >= ((int64_t)1 << 47))
     return set_err(ctx, LDPC_EINVAL, "a frame ring session takes < 2^31 frames: end it and begin anew");
   return ring_post_impl(ctx, d_in, cw_stride, B, d_out_packed, d_iters_used_opt, d_syn_weight_opt, 0);
 }
 
 int ldpc_ring_wait(ldpc_ctx *ctx, int64_t batch) {
   if (!ctx) return LDPC_EINVAL;
-  if (batch < 0 || (uint64_t)batch >= ctx->ring_next)
+  if (batch < (int64_t)ctx->ring_first || (uint64_t)batch >= ctx->ring_next)
     return set_err(ctx, LDPC_EINVAL, "no such batch in this session");
   return ring_wait_impl(ctx, (uint64_t)batch);
 }
@@ -2186,6 +2171,24 @@ int ldpc_test_hook(ldpc_ctx *ctx, int op, int64_t arg) {
       return LDPC_OK;
     case LDPC_TEST_SERVE_EPOCH_NOW:
       return (int)ctx->srv_epoch;
+    case LDPC_TEST_STREAM_OVERLAP: {
+      // streams i = arg >> 8 and j = arg & 255 of the in-flight set: a 0.2 ms
+      // spin on each, 1 if the two spins' device-clock intervals intersect
+      const size_t i = (size_t)(arg >> 8) & 255u, j = (size_t)arg & 255u;
+      if (i >= ctx->tp_streams.size() || j >= ctx->tp_streams.size())
+        return set_err(ctx, LDPC_EINVAL, "no such stream in the set");
+      hipError_t e;
+      if (!ctx->d_probe && (e = hipMalloc((void **)&ctx->d_probe, 256)) != hipSuccess)
+        return hip_err(ctx, e, "hipMalloc(probe)");
+      uint64_t *st = reinterpret_cast<uint64_t *>(ctx->d_probe) + 8, h[4] = {0, 0, 0, 0};
+      if (ldpc::launch_stamp(st, 20000, ctx->tp_streams[i]) != 0 ||
+          ldpc::launch_stamp(st + 2, 20000, ctx->tp_streams[j]) != 0 ||
+          (e = hipStreamSynchronize(ctx->tp_streams[i])) != hipSuccess ||
+          (e = hipStreamSynchronize(ctx->tp_streams[j])) != hipSuccess ||
+          (e = hipMemcpy(h, st, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess)
+        return set_err(ctx, LDPC_EDEVICE, "stream overlap probe");
+      return h[2] < h[1] && h[0] < h[3] ? 1 : 0;
+    }
     default:
       return set_err(ctx, LDPC_EINVAL, "unknown test hook");
   }
@@ -2261,9 +2264,25 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
   // wanted stream are tried.
   int rc = LDPC_OK;
   if (ctx->tp_streams.size() < (size_t)n) {
-    // the probes must see only each other: work still running on some queue
-    // would hold a probe kernel back past its timeout
-    if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize");
+    // the probes should see only each other: the context's own work is waited
+    // for (its stream, the frame ring's, the set so far; a window server is
+    // ended first) -- not the device: other contexts of the process (other
+    // blocks of a flowgraph) keep running.  Their work can hold a probe back
+    // past its timeout; the candidate is then rejected and another tried.
+    serve_stop(ctx);
+    auto own_idle = [&]() {
+      hipError_t r = hipStreamSynchronize(ctx->stream);
+      if (r == hipSuccess && ctx->ring_stream) r = hipStreamSynchronize(ctx->ring_stream);
+      for (hipStream_t t : ctx->tp_streams)
+        if (r == hipSuccess) r = hipStreamSynchronize(t);
+      return r;
+    };
+    if ((e = own_idle()) != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize");
+    // total probing is bounded: ~0.5 s, after which the set is what it is
+    const auto t_start = std::chrono::steady_clock::now();
+    auto over = [&]() {
+      return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > 0.5;
+    };
     auto concurrent = [&](hipStream_t a, hipStream_t c, bool &ok) {
       uint32_t seen = 0;
       if ((e = hipMemset(ctx->d_probe, 0, 8)) != hipSuccess ||
@@ -2298,7 +2317,9 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
       // (more streams than the process has hardware queues cannot all be
       // concurrent: after a few candidates the set's streams are handed out
       // again)
-      for (int tries = 0; (int)ctx->tp_streams.size() < n && tries < 16 * n; ++tries) {
+      for (int tries = 0; (int)ctx->tp_streams.size() < n && tries < 16 * n &&
+                          (ctx->tp_streams.empty() || !over());
+           ++tries) {
         hipStream_t c = nullptr;
         if ((rc = fresh(c)) != LDPC_OK) break;
         bool ok = true;
@@ -2313,7 +2334,7 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
       if (rc != LDPC_OK) break;
       // freeing a stream can release its hardware queue, and for a few ms
       // after that probes read concurrent pairs as shared: let it settle
-      if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize");
+      if ((e = own_idle()) != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize");
       std::this_thread::sleep_for(std::chrono::milliseconds(10));
       // the finished set, once more; one that fails is made again, and after
       // three tries the last one stays (a set, even a slower one, rather than
@@ -2322,7 +2343,7 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
       for (size_t i = 0; i < ctx->tp_streams.size() && all && rc == LDPC_OK; ++i)
         for (size_t j = i + 1; j < ctx->tp_streams.size() && all && rc == LDPC_OK; ++j)
           rc = both_ways(ctx->tp_streams[i], ctx->tp_streams[j], all);
-      if (rc != LDPC_OK || all || attempt == 2) break;
+      if (rc != LDPC_OK || all || attempt == 2 || over()) break;
       for (size_t i = held; i < ctx->tp_streams.size(); ++i) (void)hipStreamDestroy(ctx->tp_streams[i]);
       ctx->tp_streams.resize(held);
     }
@@ -2331,7 +2352,8 @@ int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out) {
   if (ctx->tp_streams.empty()) return set_err(ctx, LDPC_EDEVICE, "no stream");
   const size_t m = ctx->tp_streams.size();
   for (int i = 0; i < n; ++i) streams_out[i] = (void *)ctx->tp_streams[(size_t)i % m];
-  return LDPC_OK;
+  // the distinct streams handed out (the set's concurrent ones, at most n)
+  return (int)std::min<size_t>(m, (size_t)n);
 }
 
 int ldpc_set_waves_per_cu(ldpc_ctx *ctx, int waves_per_cu) {
@@ -2351,13 +2373,6 @@ int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode) {
   // priority games
   ctx->waves_per_cu = mode == LDPC_MODE_THROUGHPUT ? 4 : 0;
   ctx->fair_cycles = mode == LDPC_MODE_THROUGHPUT ? 0 : 1800;
-  return LDPC_OK;
-}
-
-int ldpc_set_frame_order(ldpc_ctx *ctx, int order) {
-  if (!ctx || order < 0 || order > 1)
-    return set_err(ctx, LDPC_EINVAL, "order must be 0 (queue order) or 1 (longest first)");
-  ctx->frame_order = order;
   return LDPC_OK;
 }
 

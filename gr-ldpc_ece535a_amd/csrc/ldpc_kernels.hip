@@ -144,7 +144,6 @@ __global__ void __launch_bounds__(kThreads, MINB)
   {
     int64_t pb = (int64_t)a.waves + b;
     pb = pb < a.B ? pb : b;
-    if (a.order) pb = a.order[pb];
     float ppol;
     const float *ps = frame_src(a, pb, ppol);
     (void)ppol;  // the prefetch only pulls the samples into L2
@@ -158,8 +157,7 @@ __global__ void __launch_bounds__(kThreads, MINB)
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     const uint64_t c_start = __builtin_amdgcn_s_memtime();
 #endif
-    // the frame at queue position b (a.order: longest-first order)
-    const int64_t f = a.order ? (int64_t)a.order[b] : b;
+    const int64_t f = b;
     // the frame's channel samples, one load per lane and column position
     // (a permutation of the frame's N samples); positions past N are 0
     float xin[NW], pol;

@@ -107,9 +107,6 @@ struct DecodeArgs {
   // issue-priority threshold in core clocks for waves whose last iteration
   // was slow (0: off); see decode_frame
   uint32_t fair_cycles;
-  // frame order (ldpc_set_frame_order): queue position b decodes frame
-  // order[b] (null: frame b).  Outputs go to the frame's own index.
-  const int32_t *order;
 };
 
 // ---------------------------------------------------------------------------
@@ -180,13 +177,15 @@ struct RingArgs {
   uint64_t *comp;        // host-mapped, kRingSlots completion words
   uint32_t *done;        // device, frames finished per slot (one 256-byte line each)
   uint32_t *ticket;      // device queue head (zeroed before the launch)
-  uint64_t *mirror;      // device copies of the descriptor lines (zeroed before the launch)
+  uint64_t *mirror;      // device copies of the descriptor lines, one set per XCD (zeroed)
+  uint64_t *lock;        // device, per XCD and slot: fetch lock {seq, time} (zeroed)
   int64_t ticket0;       // ticket of the launch's first frame
   uint64_t cursor0;      // the launch's first batch (seq - 1)
   uint64_t deadline;     // 100 MHz ticks without a posted batch before a wave leaves
   int max_iters, et_period;
 };
 constexpr int kRingDoneStride = 64;  // u32 words between two slots' done counters
+constexpr int kRingXcds = 8;         // mirror / lock copies: one per XCD (its own L2)
 int launch_ring(const CodeView &code, const RingArgs &r, int method, int prec, int slots, int nw,
                 int device, void *stream, int *workgroups_out);
 

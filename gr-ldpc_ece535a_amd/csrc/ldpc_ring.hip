@@ -88,8 +88,15 @@ struct Batch {
 
 constexpr uint64_t kPay = (1ull << 48) - 1;  // payload bits of a descriptor word
 
+#ifdef LDPC_TIMELINE
+// Diagnostic builds only (tools/ring_timeline.py): per ticket of the last
+// launch, 5 words (ldpc_debug_ring_timeline).
+constexpr int64_t kRingTimeline = 131072;
+__device__ uint64_t g_ring_timeline[5 * kRingTimeline];
+#endif
+
 // How a descriptor line (lane j < 8 holds word j) reads for batch q.
-enum LineState { kPosted, kNotYet, kReused, kTorn };
+enum LineState { kPosted, kNotYet, kReused, kTorn, kBusy };
 __device__ __forceinline__ LineState classify(uint64_t w, uint64_t q, int lane) {
   const uint64_t seq = readlane64(w, 0);
   if (seq < q + 1) return kNotYet;
@@ -104,18 +111,40 @@ __device__ __forceinline__ void ag_store64(uint64_t *p, uint64_t v) {
   __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Batch q's line as posted, or what the slot says instead.  The device
-// mirror (sc1 lines, one per slot) is read first; a wave that finds it stale
-// reads the host's line (eight 8-byte PCIe reads: with every wave reading
-// the host once per frame, those reads capped the ring at ~10 frames/us)
-// and, once it is posted, copies it into the mirror -- together with the
-// next slot's line when that one is posted too, so the waves that cross into
-// the next batch find it there.  Every word keeps its tag, so a mirror line
-// read while another wave writes it is recognised as torn.
-__device__ __forceinline__ LineState fetch(const RingArgs &r, uint64_t q, int lane, uint64_t &w) {
-  uint64_t *m = r.mirror + 8 * (q % kRingSlots);
+// mirror (sc1 lines, one per slot and XCD) is read first.  A wave that finds it stale
+// reads the host's line only if it takes the slot's fetch lock: every wave
+// reading the host -- eight 8-byte PCIe reads each -- capped the ring at ~10
+// frames/us, and at a launch's start 4 096 waves missing the empty mirror at
+// once cost ~0.6 ms.  The lock word is {(q + 1) mod 2^32, time taken};
+// it is taken (compare-and-swap, tried only after a plain load found it free)
+// when it names another batch, was released, or was taken more than ~20 us
+// ago (a mirror line a slower wave overwrote with an older one is fetched
+// again).  The holder copies a posted line into the mirror -- with the next
+// slot's line when that one is posted too, so the waves that cross into the
+// next batch find it there -- or releases the lock when the batch is not
+// posted yet, so the next poll can fetch again; the others answer kBusy and
+// read the mirror again.  Every word keeps its tag, so a mirror line read
+// while it is written is recognised as torn.
+constexpr uint32_t kLockHold = 125;  // ~20 us in the lock's 160 ns units
+__device__ __forceinline__ LineState fetch(const RingArgs &r, uint64_t q, int lane, uint64_t &w,
+                                           int xcd) {
+  uint64_t *m = r.mirror + 8 * (kRingSlots * xcd + q % kRingSlots);
   w = lane < 8 ? ag_load64(m + lane) : 0;
   LineState st = classify(w, q, lane);
   if (st == kPosted || st == kReused) return st;
+  uint64_t *lk = r.lock + kRingSlots * xcd + q % kRingSlots;
+  const uint32_t me = (uint32_t)(q + 1), now = (uint32_t)(ticks() >> 4);
+  bool mine = false;
+  if (lane == 0) {
+    uint64_t cur = ag_load64(lk);
+    const bool free_ = (uint32_t)(cur >> 32) != me || (uint32_t)cur == 0u ||
+                       now - (uint32_t)cur > kLockHold;
+    if (free_)
+      mine = __hip_atomic_compare_exchange_strong((gu64 *)lk, &cur, ((uint64_t)me << 32) | (now | 1u),
+                                                  __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (__ballot(mine) == 0) return kBusy;  // another wave is fetching it
   const uint64_t *h = reinterpret_cast<const uint64_t *>(r.desc + (q % kRingSlots));
   w = lane < 8 ? sys_load(h + lane) : 0;
   st = classify(w, q, lane);
@@ -124,7 +153,11 @@ __device__ __forceinline__ LineState fetch(const RingArgs &r, uint64_t q, int la
     const uint64_t q1 = q + 1;
     const uint64_t *h1 = reinterpret_cast<const uint64_t *>(r.desc + (q1 % kRingSlots));
     const uint64_t w1 = lane < 8 ? sys_load(h1 + lane) : 0;
-    if (classify(w1, q1, lane) == kPosted && lane < 8) ag_store64(r.mirror + 8 * (q1 % kRingSlots) + lane, w1);
+    if (classify(w1, q1, lane) == kPosted && lane < 8)
+      ag_store64(r.mirror + 8 * (kRingSlots * xcd + q1 % kRingSlots) + lane, w1);
+  } else if (lane == 0) {
+    // not posted (or torn, or reused): release, so the next poll fetches again
+    ag_store64(lk, (uint64_t)me << 32);
   }
   return st;
 }
@@ -133,14 +166,14 @@ __device__ __forceinline__ LineState fetch(const RingArgs &r, uint64_t q, int la
 // wave must leave: the quit descriptor was reached, or no batch was posted
 // for `deadline` ticks.  bt.q starts at the launch's cursor with end =
 // start = -1 ("not read yet").
-__device__ __forceinline__ bool locate(const RingArgs &r, int64_t t, Batch &bt, int lane) {
+__device__ __forceinline__ bool locate(const RingArgs &r, int64_t t, Batch &bt, int lane, int xcd) {
   bool first = bt.end < 0;  // bt.q itself has not been read yet
   uint64_t t_wait = 0;
   uint32_t nap = 0;
   while (first || t >= bt.end) {
     const uint64_t q = first ? bt.q : bt.q + 1;
     uint64_t w;
-    const LineState st = fetch(r, q, lane, w);
+    const LineState st = fetch(r, q, lane, w, xcd);
     if (st == kPosted) {
       bt.q = q;
       bt.start = (int64_t)(readlane64(w, 1) & kPay);
@@ -163,14 +196,19 @@ __device__ __forceinline__ bool locate(const RingArgs &r, int64_t t, Batch &bt, 
       bt.q = q;
       bt.start = bt.end = t;  // (t >= end: go on to q + 1)
       first = false;
-    } else if (st == kNotYet) {
-      // not posted yet: wait, backing off to ~54 us between polls (only
-      // while the ring has nothing to do)
+    } else if (st == kNotYet || st == kBusy) {
+      // not posted yet, or another wave is fetching the line: read the mirror
+      // again after ~0.5 us; once the wait passes ~20 us (the batch is not
+      // posted: the ring has nothing to do) back off to ~54 us between polls
       const uint64_t now = ticks();
       if (!t_wait) t_wait = now;
       if (now - t_wait > r.deadline) return false;
-      for (uint32_t k = 0; k <= nap; ++k) __builtin_amdgcn_s_sleep(127);  // ~3.4 us each
-      nap = nap < 15 ? nap + 1 : nap;
+      if (now - t_wait < 2000) {
+        __builtin_amdgcn_s_sleep(20);
+      } else {
+        for (uint32_t k = 0; k <= nap; ++k) __builtin_amdgcn_s_sleep(127);  // ~3.4 us each
+        nap = nap < 15 ? nap + 1 : nap;
+      }
     }  // (kTorn: read again)
   }
   return true;
@@ -196,18 +234,31 @@ __global__ void __launch_bounds__(kThreads, MINB) ring_kernel(CodeView code, Rin
   Batch bt{};
   bt.q = r.cursor0;
   bt.start = bt.end = -1;
-  uint32_t tk = 0;
-  if (lane == 0) tk = atomicAdd(r.ticket, 1u);
-  int64_t t = r.ticket0 + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
-  while (locate(r, t, bt, lane)) {
+  // wave w's first ticket is w; the queue hands out the ones after all the
+  // launch's waves (4 096 first claims on one counter at once took ~46 us:
+  // ~88 per us, MI355X_MICROARCH.md "dequeue")
+  const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+  int64_t t = r.ticket0 + (int64_t)blockIdx.x * kWavesPerBlock + wave;
+#ifdef LDPC_TIMELINE
+  const uint64_t t_wave0 = ticks();
+#endif
+  // this wave's XCD: its mirror and lock copies live in that XCD's L2 only
+  // (an sc1 load polling a line another XCD rewrote kept reading its own
+  // L2's copy: at a launch's start every wave off the fetching XCD waited
+  // out the ~20 us lock, tools/ring_timeline.py)
+  const int xcd = (int)(__builtin_amdgcn_s_getreg((31 << 11) | 20) & (kRingXcds - 1));  // XCC_ID
+  while (locate(r, t, bt, lane, xcd)) {
+#ifdef LDPC_TIMELINE
+    const uint64_t t_f0 = ticks();
+#endif
     const int64_t f = t - bt.start;
     const float *src = bt.in + f * bt.cw;
     float xin[NW];
 #pragma unroll
     for (int q = 0; q < NW; ++q) xin[q] = colq[q] >= 0 ? ag_load(src + colq[q]) : 0.0f;
-    // the next ticket, claimed now: its value is first needed after the decode
-    uint32_t nt = 0;
-    if (lane == 0) nt = atomicAdd(r.ticket, 1u);
+#ifdef LDPC_TIMELINE
+    const uint64_t t_f1 = ticks();  // (samples loaded and the claim issued)
+#endif
     FrameResult fr;
     if constexpr (METHOD == 1) {
       bool bad = false;
@@ -223,6 +274,14 @@ __global__ void __launch_bounds__(kThreads, MINB) ring_kernel(CodeView code, Rin
       fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, false, false>(
           code, a, f, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
     }
+    // the next ticket, claimed when this frame is done: a ticket claimed at
+    // the frame's start waited for the frame (up to 50 iterations), and at
+    // a session's end the last tickets sat with waves busy on long frames
+    // while the others had run out of work (tools/ring_timeline.py: the last
+    // frame started 90 us before the end, the queue emptied ~250 us before).
+    // The claim's round trip overlaps the output stores' drain below.
+    uint32_t nt = 0;
+    if (lane == 0) nt = atomicAdd(r.ticket, 1u);
     // outputs, write-through: packed bytes M.. (:207-219) as 32-bit words
     // where the layout allows, iterations, syndrome weight
     uint8_t *pk = bt.packed + f * KB;
@@ -250,7 +309,20 @@ __global__ void __launch_bounds__(kThreads, MINB) ring_kernel(CodeView code, Rin
         sys_store(r.comp + (bt.q % kRingSlots), bt.q + 1);
       }
     }
-    t = r.ticket0 + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)nt);
+#ifdef LDPC_TIMELINE
+    {  // per ticket: wave start, frame start, decode start, frame end, wave id | iterations
+      const int64_t rel = t - r.ticket0;
+      if (lane == 0 && rel >= 0 && rel < kRingTimeline) {
+        uint64_t *o = g_ring_timeline + 5 * rel;
+        o[0] = t_wave0;
+        o[1] = t_f0;
+        o[2] = t_f1;
+        o[3] = ticks();
+        o[4] = ((uint64_t)(blockIdx.x * kWavesPerBlock + wave) << 8) | (uint64_t)fr.used;
+      }
+    }
+#endif
+    t = r.ticket0 + nwaves + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)nt);
   }
 }
 
@@ -350,3 +422,13 @@ int launch_ring(const CodeView &code, const RingArgs &r, int method, int prec, i
 }
 
 }  // namespace ldpc
+
+#ifdef LDPC_TIMELINE
+extern "C" int ldpc_debug_ring_timeline(uint64_t *host, int tickets) {
+  if (tickets > ldpc::kRingTimeline) tickets = (int)ldpc::kRingTimeline;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ldpc::g_ring_timeline), sizeof(uint64_t) * 5 * tickets) ==
+                 hipSuccess
+             ? tickets
+             : -1;
+}
+#endif

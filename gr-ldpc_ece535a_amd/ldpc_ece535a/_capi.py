@@ -19,7 +19,7 @@ PREC_F64, PREC_F32, PREC_F64_LIBM, PREC_F64_FAST = 0, 1, 2, 3
 FLAG_NO_REORDER = 1
 FLAG_GRAPH = 2
 FLAG_PLAIN_LAYOUT = 4
-TEST_SERVE_UNCHECKED, TEST_SERVE_EPOCH, TEST_SERVE_EPOCH_NOW = 1, 2, 3
+TEST_SERVE_UNCHECKED, TEST_SERVE_EPOCH, TEST_SERVE_EPOCH_NOW, TEST_STREAM_OVERLAP = 1, 2, 3, 4
 SERVE_EPOCH_LIMIT = (1 << 23) - (1 << 16)
 PATH_SMALL, PATH_GRAPH = 0, 1
 MODE_LATENCY, MODE_THROUGHPUT = 0, 1
@@ -76,7 +76,6 @@ SIGNATURES = {
     "ldpc_set_waves_per_cu": (_i, [_vp, _i]),
     "ldpc_set_launch_mode": (_i, [_vp, _i]),
     "ldpc_set_schedule": (_i, [_vp, _i]),
-    "ldpc_set_frame_order": (_i, [_vp, _i]),
     "ldpc_synchronize": (_i, [_vp]),
     "ldpc_test_hook": (_i, [_vp, _i, _i64]),
     "ldpc_ring_begin": (_i, [_vp, _i, _i, _i, _i, _vp]),
@@ -359,9 +358,9 @@ class Decoder:
 
     def streams(self, n):
         """ldpc_ctx_streams: n hipStream_t handles (ints) of the context's
-        in-flight set, each on its own hardware queue."""
+        in-flight set (best effort: self.streams_distinct of them distinct)."""
         arr = (ctypes.c_void_p * int(n))()
-        _check(lib().ldpc_ctx_streams(self._ctx, int(n), arr), self._ctx)
+        self.streams_distinct = _check(lib().ldpc_ctx_streams(self._ctx, int(n), arr), self._ctx)
         return [int(x) for x in arr]
 
     def ring_begin(self, method=METHOD_SUMPRODUCT, max_iters=50, et_period=1,
@@ -436,10 +435,6 @@ class Decoder:
     def set_schedule(self, mode):
         """0 auto, 1 one wave per frame, 2 one workgroup per frame."""
         _check(lib().ldpc_set_schedule(self._ctx, int(mode)), self._ctx)
-
-    def set_frame_order(self, order):
-        """0 queue order, 1 longest first (ascending sum |y| per 4096 frames)."""
-        _check(lib().ldpc_set_frame_order(self._ctx, int(order)), self._ctx)
 
     def synchronize(self):
         _check(lib().ldpc_synchronize(self._ctx), self._ctx)

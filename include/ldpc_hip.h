@@ -291,6 +291,11 @@ int ldpc_serve_end(ldpc_ctx *ctx);
 #define LDPC_TEST_SERVE_UNCHECKED 1
 #define LDPC_TEST_SERVE_EPOCH 2
 #define LDPC_TEST_SERVE_EPOCH_NOW 3
+/*   LDPC_TEST_STREAM_OVERLAP   arg = (i << 8) | j: a 0.2 ms spin on streams i and j
+ *                              of the ldpc_ctx_streams set; returns 1 if their
+ *                              device-clock intervals intersect (the streams run
+ *                              side by side), else 0 */
+#define LDPC_TEST_STREAM_OVERLAP 4
 int ldpc_test_hook(ldpc_ctx *ctx, int op, int64_t arg);
 
 /* Device-resident buffers (already in HBM); enqueues on `hip_stream`
@@ -323,8 +328,8 @@ int ldpc_decode_device(ldpc_ctx *ctx, int method, int max_iters,
  *   ldpc_ring_post   posts a batch of B device-resident frames (frame b at
  *                    d_in + b*cw_stride, elem_stride 1, polarity +1) with its
  *                    device outputs as ldpc_decode_device; returns the batch's
- *                    id (>= 0, consecutive from 0 per session) or a negative
- *                    code.  The input must be in device memory when the call
+ *                    id (>= 0, consecutive; they keep growing across the
+ *                    context's sessions) or a negative code.  The input must be in device memory when the call
  *                    is made, and must stay unchanged until the batch is
  *                    complete.  Returns at once, except when 256 batches are
  *                    outstanding: it then waits for the oldest.
@@ -351,17 +356,21 @@ int ldpc_ring_end(ldpc_ctx *ctx);
 int ldpc_ring_info(const ldpc_ctx *ctx, int *launches_out, int *workgroups_out);
 
 /* The context's in-flight streams (hipStream_t) for callers that keep
- * several ldpc_decode_device calls in flight (LDPC_MODE_THROUGHPUT): n
- * (1..16) streams that run concurrently -- each on its own hardware queue,
- * checked by probe launch pairs (both ways round, after each candidate's own
- * first launch, and the finished set once more) when the set is first made,
- * a few ms, up to ~0.3 s in a process with dozens of streams -- owned by the
- * context (destroyed by ldpc_destroy); with fewer hardware queues than n
- * (GPU_MAX_HW_QUEUES), the concurrent ones are handed out again in turn.  A
- * caller's own streams may share a
- * hardware queue, depending on the streams the process made before them, and
- * then serialise their launches.  (Replaces nothing in the reference: its
- * decode runs on the calling thread, lib/ldpc_decoder_cb_impl.cc:155-164.) */
+ * several ldpc_decode_device calls in flight on their own (bench.py no longer
+ * does: it posts its batches to the frame ring, ldpc_ring_*, one launch on one
+ * stream).  n (1..16) streams meant to run concurrently, each on its own
+ * hardware queue: a candidate joins the set only if probe launch pairs run
+ * side by side with every member, both ways round, after the candidate's own
+ * first launch; the finished set is probed once more.  The context's own work
+ * is waited for first (its stream, its ring, its set; a window server is
+ * ended), never the whole device, and probing stops after ~0.5 s.  The set is
+ * best effort: in a process that holds many streams (or beside processes that
+ * do -- hardware queue slots are shared) fewer than n distinct concurrent
+ * streams may be found; the set's streams are then handed out again in turn.
+ * Returns the number of distinct streams handed out (1..n), or a negative
+ * code.  Streams are owned by the context (destroyed by ldpc_destroy).
+ * (Replaces nothing in the reference: its decode runs on the calling thread,
+ * lib/ldpc_decoder_cb_impl.cc:155-164.) */
 int ldpc_ctx_streams(ldpc_ctx *ctx, int n, void **streams_out);
 
 /* Tuning: persistent waves per CU for the decode kernel (0 = default).
@@ -387,17 +396,6 @@ int ldpc_set_launch_mode(ldpc_ctx *ctx, int mode);
  * where it has the lower latency on MI355X (one 50-iteration frame 61 vs
  * 89 us), else 1.  Results are identical across schedules. */
 int ldpc_set_schedule(ldpc_ctx *ctx, int schedule);
-
-/* Tuning: frame order of small-code min-sum / sum-product decodes of
- * device-resident frames (ldpc_decode_device, ldpc_decode).  0 (default):
- * frames start in index order.  1: longest first -- a short kernel ahead of
- * each launch sorts groups of 256 frames by ascending sum |y| and interleaves
- * them rank by rank (the least reliable frames, which tend to need the most
- * iterations, start first; DESIGN section 6 has the measured A/B).  Results
- * are identical. */
-#define LDPC_ORDER_QUEUE 0
-#define LDPC_ORDER_LONGEST_FIRST 1
-int ldpc_set_frame_order(ldpc_ctx *ctx, int order);
 
 /* Large-code path: device workspace cap in bytes (0 = default 8 GiB).  A
  * batch larger than the cap allows is decoded in consecutive groups. */

@@ -12,18 +12,18 @@ from ldpc_ece535a import flowgraph as fg
 pytestmark = pytest.mark.gpu
 
 
-PATHS = {"serve": {}, "launch": {"LDPC_BLOCK_SERVE": "0"}, "serve-all": {"LDPC_BLOCK_SERVE": "1"},
+PATHS = {"serve": {}, "launch": {"LDPC_BLOCK_SERVE": "0"},
          # the planner's A/B knobs: short dry runs, one search per round
          "plan": {"LDPC_BLOCK_MAXWANT": "64", "LDPC_BLOCK_SEARCHES": "1"},
          # every diagnostic knob on: stderr lines only, the same bytes
-         "diag": {"LDPC_BLOCK_DEBUG": "2", "LDPC_BLOCK_PROFILE": "2", "LDPC_WIN_PROFILE": "2",
+         "diag": {"LDPC_BLOCK_DEBUG": "2", "LDPC_BLOCK_PROFILE": "2",
                   "LDPC_SERVE_DEBUG": "1"}}
 
 
 def _block(method, path, **kw):
     """The block with its small rounds through the window server and big ones
-    by launch (default), a launch per round (LDPC_BLOCK_SERVE=0), the server
-    for every round (=1), another dry-run plan, or every diagnostic on."""
+    by launch (default), a launch per round (LDPC_BLOCK_SERVE=0), another
+    dry-run plan, or every diagnostic on."""
     import os
     env = PATHS[path]
     os.environ.update(env)

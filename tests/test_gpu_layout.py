@@ -102,28 +102,3 @@ def test_throughput_build_equals_latency_build(golden, method, prec):
     if prec != 1:
         ref = orc.decode_batch(method, dec.H, y, 50, nthreads=8)
         assert (b["packed"] == ref["packed"]).all() and (b["iters"] == ref["iters"]).all()
-
-
-@pytest.mark.parametrize("B", [2, 700, 4096, 9000])
-@pytest.mark.parametrize("method", [0, 1])
-def test_longest_first_order_same_outputs(method, B):
-    """ldpc_set_frame_order(1): a short kernel sorts groups of 256 frames by
-    ascending sum |y| and interleaves them rank by rank, and the kernel's
-    queue hands frames out in that order; every frame's outputs still go to
-    its own index -- equal to queue order and to the oracle, in both launch
-    modes, for one partial group, full groups and a partial last group."""
-    from oracle import oracle as orc
-    dec = L.Decoder()
-    y = frames(dec.H, B, 2.0, 7 + B)
-    base = dec.decode(y, method=method, max_iters=50, want_llr=True)
-    dec.set_frame_order(1)
-    for mode in (0, 1):
-        dec.set_launch_mode(mode)
-        got = dec.decode(y, method=method, max_iters=50, want_llr=True)
-        for k in ("packed", "bits", "iters", "synd"):
-            assert (got[k] == base[k]).all(), (k, mode)
-        assert np.array_equal(got["llr"], base["llr"], equal_nan=True)
-    ref = orc.decode_batch(method, dec.H, y[:512], 50, nthreads=8)
-    assert (base["packed"][:512] == ref["packed"]).all() and (base["iters"][:512] == ref["iters"]).all()
-    with pytest.raises(L.LdpcError):
-        dec.set_frame_order(2)

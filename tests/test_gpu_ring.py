@@ -77,7 +77,7 @@ def test_ring_batches_vs_oracle():
     info = dec.ring_info()
     dec.ring_end()
     torch.cuda.synchronize()
-    assert ids == list(range(len(sizes)))
+    assert ids == list(range(ids[0], ids[0] + len(sizes)))
     assert info["launches"] >= 2, info
     ref = oracle(1, Hr, y)
     pk, it, sy = (t.cpu().numpy() for t in o)
@@ -186,4 +186,26 @@ def test_ring_errors():
     dec.ring_end()
     dec.ring_end()  # (no session: a no-op)
     torch.cuda.synchronize()
+    dec.close()
+
+
+def test_ring_sessions_back_to_back():
+    """Consecutive sessions on one context (what bench.py does: a warmup
+    session, then the timed one), each batch into outputs of its own: no
+    descriptor a previous session left behind is taken for a new batch."""
+    dec = L.Decoder()
+    B = 1500
+    y = frames(dec.H, B, 2.0, 4242)
+    d_y = torch.from_numpy(y).cuda()
+    ref = oracle(1, dec.H, y)
+    for s in range(5):
+        o = [outs(dec, B) for _ in range(3)]
+        dec.ring_begin(method=1, max_iters=50)
+        for ok in o:
+            post(dec, d_y, ok)
+        dec.ring_end()
+        torch.cuda.synchronize()
+        for ok in o:
+            assert (ok[0].cpu().numpy() == ref["packed"]).all(), s
+            assert (ok[1].cpu().numpy() == ref["iters"]).all(), s
     dec.close()

@@ -86,15 +86,15 @@ def test_many_streams_reuse_counters():
 @pytest.mark.parametrize("extra", [0, 1, 3])
 def test_ctx_streams_run_concurrently(extra):
     """ldpc_ctx_streams' set runs its launches side by side whatever streams
-    the process made before (in the suite's own crowded process) (profiles/round5/inflight_bimodal.txt: a set with
-    two streams on one hardware queue measured 0.72x).  In the throughput
-    launch mode a launch holds one wave per SIMD, so two launches on two
-    streams of a good set take about as long as one; on a shared queue they
-    take twice as long.  Every pair of the set is timed that way, and the
-    in-flight outputs equal the one-stream run's."""
-    import time
+    the process made before (in the suite's own crowded process;
+    profiles/round5/inflight_bimodal.txt: a set with two streams on one
+    hardware queue measured 0.72x).  Checked with device clocks, not wall
+    time: a 0.2 ms spin on each of two streams, and the two spins' intervals
+    must intersect (LDPC_TEST_STREAM_OVERLAP); the same stream twice must
+    not.  The in-flight outputs equal the one-stream run's."""
     import torch
     import ldpc_ece535a as L
+    from ldpc_ece535a._capi import TEST_STREAM_OVERLAP
     keep = [torch.cuda.Stream() for _ in range(extra)]  # queue history
     for st in keep:
         with torch.cuda.stream(st):
@@ -107,35 +107,27 @@ def test_ctx_streams_run_concurrently(extra):
     # tests), and the GPU's hardware queue slots are shared by every queue of
     # every process: the set may hold fewer than four distinct streams, handed
     # out again in turn (include/ldpc_hip.h); those it holds must run side by
-    # side.  (A bench.py process gets four: profiles/round5/inflight_bimodal.txt.)
+    # side.
     u = sorted(set(hs), key=hs.index)
-    assert len(u) >= 2
+    assert dec.streams_distinct == len(u) >= 2
+    assert dec.test_hook(TEST_STREAM_OVERLAP, 0) == 0  # one stream: one after the other
+    for i in range(len(u)):
+        for j in range(len(u)):
+            if i != j:
+                assert dec.test_hook(TEST_STREAM_OVERLAP, (i << 8) | j) == 1, (i, j)
     B = 4096
     ys = [torch.from_numpy(_frames(dec.H, B, 2.0, 40 + j)).cuda() for j in range(4)]
     outs = [torch.empty((B, dec.KB), dtype=torch.uint8, device="cuda") for _ in range(4)]
     its = [torch.empty(B, dtype=torch.int32, device="cuda") for _ in range(4)]
 
-    def run(streams, reps=3):
+    def run(streams):
+        for d, st in enumerate(streams):
+            dec.decode_device(ys[d].data_ptr(), B, outs[d].data_ptr(), method=1,
+                              max_iters=50, d_iters=its[d].data_ptr(), stream=st)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            for d, st in enumerate(streams):
-                dec.decode_device(ys[d].data_ptr(), B, outs[d].data_ptr(), method=1,
-                                  max_iters=50, d_iters=its[d].data_ptr(), stream=st)
-        torch.cuda.synchronize()
-        return time.perf_counter() - t0
 
-    run(hs)  # warm-up (clocks)
-    run([hs[0]] * 4, 1)  # the four batches one after another on one stream
+    run([hs[0]] * 4)  # the four batches one after another on one stream
     one = [(outs[d].cpu().numpy().copy(), its[d].cpu().numpy().copy()) for d in range(4)]
-    # the measure tells the two cases apart: both launches on one stream
-    t1 = run([hs[0]])
-    assert run([hs[0], hs[0]]) / t1 >= 1.6
-    for i in range(len(u)):
-        for j in range(i + 1, len(u)):
-            t1 = min(run([u[i]]), run([u[j]]))
-            t2 = run([u[i], u[j]])
-            assert t2 / t1 < 1.6, "streams %d and %d: two launches %.2fx one" % (i, j, t2 / t1)
     run(hs)
     for d in range(4):
         assert (outs[d].cpu().numpy() == one[d][0]).all()

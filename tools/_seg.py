@@ -11,7 +11,7 @@ from oracle import oracle as orc
 st = np.load(os.path.join(REPO, "tests/golden/streams.npz"))
 paths = {"serve": {}, "launch": {"LDPC_BLOCK_SERVE": "0"},
          "plan": {"LDPC_BLOCK_MAXWANT": "64", "LDPC_BLOCK_SEARCHES": "1"},
-         "diag": {"LDPC_BLOCK_DEBUG": "2", "LDPC_BLOCK_PROFILE": "2", "LDPC_WIN_PROFILE": "2",
+         "diag": {"LDPC_BLOCK_DEBUG": "2", "LDPC_BLOCK_PROFILE": "2",
                   "LDPC_SERVE_DEBUG": "1"}}
 for path in sys.argv[1].split(","):
     for name in ["aligned", "offset"]:

@@ -10,7 +10,7 @@ mkdir -p "$out"
 cd "$R"
 ITERS=${ITERS:-5}
 DB=${DB:-4}
-LDPC_WIN_PROFILE=1 LDPC_BLOCK_PROFILE=1 timeout -k 10 180 python tools/block_bench.py --iters $ITERS --ebn0 $DB \
+LDPC_BLOCK_PROFILE=1 timeout -k 10 180 python tools/block_bench.py --iters $ITERS --ebn0 $DB \
   --reps 4 > "$out/split.txt" 2>&1
 export TMPDIR=/tmp
 LDPC_BLOCK_PROFILE=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o blk \

@@ -13,7 +13,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-sys.path.insert(0, os.path.join(REPO, "gr-ldpc_ece535a_amd"))
+sys.path.insert(0, os.environ.get("LDPC_PKG_DIR", os.path.join(REPO, "gr-ldpc_ece535a_amd")))
 import torch  # noqa: E402
 import bench  # noqa: E402
 import ldpc_ece535a as L  # noqa: E402
@@ -68,6 +68,18 @@ def main():
         return
     for _ in range(30):
         session(0)
+    if os.environ.get("VARIANTS"):  # LDPC_RING_PROBE experiment bits, alternated
+        vs = os.environ["VARIANTS"].split(",")
+        res = {v: [] for v in vs}
+        for rep in range(6):
+            for v in vs:
+                os.environ["LDPC_RING_PROBE"] = v
+                sp_ = sorted(session(0)[1] for _ in range(5))
+                res[v].append(sp_[2] * 1e3 / K)
+        for v in vs:
+            print("probe %-4s K=%d us/batch: median %.1f  all %s" % (
+                v, K, float(np.median(res[v])), " ".join("%.1f" % x for x in res[v])), flush=True)
+        return
     if os.environ.get("MODE") == "ring":
         for _ in range(10):
             session(0)
