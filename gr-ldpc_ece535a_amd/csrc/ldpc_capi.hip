@@ -161,6 +161,7 @@ struct ldpc_ctx {
   int64_t ring_first_frame = 0;
   int64_t ring_start[ldpc::kRingSlots] = {};  // start ticket of the batch in each slot
   int ring_launches = 0, ring_workgroups = 0;
+  bool ring_clean = false;  // d_ring zeroed for the next launch already
   // in-flight stream set for throughput callers (ldpc_ctx_streams): streams
   // verified to run concurrently, i.e. on distinct hardware queues
   std::vector<hipStream_t> tp_streams;
@@ -1926,8 +1927,12 @@ void ring_write_desc(ldpc_ctx *ctx, uint64_t q, int64_t start, const void *in, i
 int ring_launch(ldpc_ctx *ctx, uint64_t cursor, int64_t ticket0) {
   hipError_t e;
   if ((e = hipSetDevice(ctx->device)) != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  if ((e = hipMemsetAsync(ctx->d_ring, 0, kRingDevBytes, ctx->ring_stream)) != hipSuccess)
+  // (zeroed behind the previous session's launch by ldpc_ring_end, off the
+  // next session's critical path; a relaunch zeroes here)
+  if (!ctx->ring_clean &&
+      (e = hipMemsetAsync(ctx->d_ring, 0, kRingDevBytes, ctx->ring_stream)) != hipSuccess)
     return hip_err(ctx, e, "hipMemsetAsync(ring)");
+  ctx->ring_clean = false;
   void *dh = nullptr;
   if ((e = hipHostGetDevicePointer(&dh, ctx->h_ring, 0)) != hipSuccess)
     return hip_err(ctx, e, "hipHostGetDevicePointer(ring)");
@@ -2146,8 +2151,14 @@ int ldpc_ring_end(ldpc_ctx *ctx) {
   const int64_t q = ring_post_impl(ctx, nullptr, 0, 0, nullptr, nullptr, nullptr, 1);
   if (q < 0) return (int)q;
   // work the caller enqueues on its stream from now on follows the launch
-  const hipError_t e = hipStreamWaitEvent((hipStream_t)ctx->ring_user_stream, ctx->ring_ev, 0);
-  return e == hipSuccess ? LDPC_OK : hip_err(ctx, e, "frame ring: stream order");
+  hipError_t e = hipStreamWaitEvent((hipStream_t)ctx->ring_user_stream, ctx->ring_ev, 0);
+  if (e != hipSuccess) return hip_err(ctx, e, "frame ring: stream order");
+  // the next session's counters, zeroed on the ring's stream once this
+  // launch has ended (the caller's stream waits for the launch only)
+  if ((e = hipMemsetAsync(ctx->d_ring, 0, kRingDevBytes, ctx->ring_stream)) != hipSuccess)
+    return hip_err(ctx, e, "hipMemsetAsync(ring)");
+  ctx->ring_clean = true;
+  return LDPC_OK;
 }
 
 int ldpc_ring_info(const ldpc_ctx *ctx, int *launches_out, int *workgroups_out) {

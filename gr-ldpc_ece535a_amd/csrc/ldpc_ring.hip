@@ -92,7 +92,8 @@ constexpr uint64_t kPay = (1ull << 48) - 1;  // payload bits of a descriptor wor
 // Diagnostic builds only (tools/ring_timeline.py): per ticket of the last
 // launch, 5 words (ldpc_debug_ring_timeline).
 constexpr int64_t kRingTimeline = 131072;
-__device__ uint64_t g_ring_timeline[5 * kRingTimeline];
+constexpr int kTlWords = 6;
+__device__ uint64_t g_ring_timeline[kTlWords * kRingTimeline];
 #endif
 
 // How a descriptor line (lane j < 8 holds word j) reads for batch q.
@@ -249,7 +250,7 @@ __global__ void __launch_bounds__(kThreads, MINB) ring_kernel(CodeView code, Rin
   const int xcd = (int)(__builtin_amdgcn_s_getreg((31 << 11) | 20) & (kRingXcds - 1));  // XCC_ID
   while (locate(r, t, bt, lane, xcd)) {
 #ifdef LDPC_TIMELINE
-    const uint64_t t_f0 = ticks();
+    const uint64_t t_f0 = ticks(), c_f0 = __builtin_amdgcn_s_memtime();
 #endif
     const int64_t f = t - bt.start;
     const float *src = bt.in + f * bt.cw;
@@ -310,15 +311,17 @@ __global__ void __launch_bounds__(kThreads, MINB) ring_kernel(CodeView code, Rin
       }
     }
 #ifdef LDPC_TIMELINE
-    {  // per ticket: wave start, frame start, decode start, frame end, wave id | iterations
+    {  // per ticket: wave start, frame start, decode start, frame end, wave id |
+       // iterations, core clocks of the frame
       const int64_t rel = t - r.ticket0;
       if (lane == 0 && rel >= 0 && rel < kRingTimeline) {
-        uint64_t *o = g_ring_timeline + 5 * rel;
+        uint64_t *o = g_ring_timeline + kTlWords * rel;
         o[0] = t_wave0;
         o[1] = t_f0;
         o[2] = t_f1;
         o[3] = ticks();
         o[4] = ((uint64_t)(blockIdx.x * kWavesPerBlock + wave) << 8) | (uint64_t)fr.used;
+        o[5] = __builtin_amdgcn_s_memtime() - c_f0;  // core clocks of the frame
       }
     }
 #endif
@@ -426,7 +429,8 @@ int launch_ring(const CodeView &code, const RingArgs &r, int method, int prec, i
 #ifdef LDPC_TIMELINE
 extern "C" int ldpc_debug_ring_timeline(uint64_t *host, int tickets) {
   if (tickets > ldpc::kRingTimeline) tickets = (int)ldpc::kRingTimeline;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ldpc::g_ring_timeline), sizeof(uint64_t) * 5 * tickets) ==
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ldpc::g_ring_timeline),
+                             sizeof(uint64_t) * ldpc::kTlWords * tickets) ==
                  hipSuccess
              ? tickets
              : -1;

@@ -66,8 +66,11 @@ def hot_path(lines, full=False):
         m = re.match(r"s_cbranch_\w+\s+(\.LBB\d+_\d+)", l)
         if m:
             tgt = m.group(1) + ":"
+            # cold: the marker sits in the first basic block the branch skips
+            # (the compiler may schedule instructions of that block ahead of
+            # it, but not move it into another block)
             cold, j = False, i + 1
-            while j < len(lines) and not lines[j].startswith(tgt) and j < i + 14:
+            while j < len(lines) and not re.match(r"^\.LBB\d+_\d+:", lines[j]):
                 if "ldpc_cold" in lines[j]:
                     cold = True
                     break

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--steps", type=int, default=0, help="timed launches at the end of the run")
     ap.add_argument("--source", default=None, help="recorded in the json entry")
     ap.add_argument("--key", default=None)
+    ap.add_argument("--ring-batches", type=int, default=0,
+                    help="frame ring: the kernel's LAST dispatch (the timed session) decoded this "
+                         "many batches; its counters and duration are divided by it (per batch)")
     ap.add_argument("--per-decode", default=None,
                     help="large-code path: sum the traffic of every kernel whose name contains "
                          "this substring and divide by the number of decodes (g_reset dispatches)")
@@ -65,10 +68,28 @@ def main():
             print("stats:", {k: r[k] for k in r if k in ("Name", "Calls", "AverageNs", "TotalDurationNs",
                                                            "Percentage")})
     counters = collections.defaultdict(list)
+    if a.ring_batches:
+        last = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in kt
+                      if a.kernel in r["Kernel_Name"])[-1]
+        res["mean_ns"] = res["span_ns_per_launch"] = (last[1] - last[0]) / a.ring_batches
+        res["ring_session_ns"] = last[1] - last[0]
+        res["ring_batches"] = a.ring_batches
+        print("ring: last dispatch %.1f us, %d batches: %.1f ns per batch" % (
+            (last[1] - last[0]) / 1e3, a.ring_batches, res["mean_ns"]))
     for p in ("pmc1", "pmc2", "pmc3", "pmc4", "pmc5"):
-        for r in rows(os.path.join(a.dir, p, "**", "*counter_collection.csv")):
-            if a.kernel in r["Kernel_Name"]:
-                counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        prs = [r for r in rows(os.path.join(a.dir, p, "**", "*counter_collection.csv"))
+               if a.kernel in r["Kernel_Name"]]
+        if a.ring_batches and prs:
+            dmax = max(int(r["Dispatch_Id"]) for r in prs)
+            tot = collections.defaultdict(float)
+            for r in prs:
+                if int(r["Dispatch_Id"]) == dmax:
+                    tot[r["Counter_Name"]] += float(r["Counter_Value"])
+            for k, v in tot.items():
+                counters[k].append(v / a.ring_batches)
+            continue
+        for r in prs:
+            counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
     print("== counters (mean per dispatch of %s) ==" % a.kernel)
     pmc = {}
     for k, v in sorted(counters.items()):

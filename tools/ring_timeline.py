@@ -48,14 +48,37 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1)
 
-    for _ in range(40):
-        session()
-    span_ms = session()
+    if os.environ.get("PREROLL") == "serial":  # bench.py's order: 30 ms one batch at a time, 5-batch session
+        dec2 = L.Decoder()
+        dec2.set_launch_mode(0)
+        s1 = torch.cuda.Stream(dev)
+        import time
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < 0.03:
+                pk, it, sy = pool[0]
+                dec2.decode_device(ins[0].data_ptr(), B, pk.data_ptr(), method=1, max_iters=50,
+                                   d_iters=it.data_ptr(), d_synd=sy.data_ptr(), stream=s1.cuda_stream)
+                s1.synchronize()
+            dec.ring_begin(method=1, max_iters=50, stream=sp)
+            for k in range(5):
+                pk, it, sy = pool[k]
+                dec.ring_post(ins[k % 4].data_ptr(), B, pk.data_ptr(), it.data_ptr(), sy.data_ptr())
+            dec.ring_end()
+            torch.cuda.synchronize()
+            span_ms = session()
+            print("serial pre-roll: span %.1f us per batch" % (1e3 * span_ms / K))
+    else:
+        for _ in range(40):
+            session()
+        span_ms = session()
     n = K * B
-    buf = np.zeros(5 * n, np.uint64)
+    W = 6
+    buf = np.zeros(W * n, np.uint64)
     lib.ldpc_debug_ring_timeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
     got = lib.ldpc_debug_ring_timeline(buf.ctypes.data, n)
-    tl = buf[:5 * got].reshape(got, 5).astype(np.int64)
+    tl = buf[:W * got].reshape(got, W).astype(np.int64)
     wave0, f0, f1, f3 = tl[:, 0], tl[:, 1], tl[:, 2], tl[:, 3]
     wid, its = tl[:, 4] >> 8, tl[:, 4] & 255
     T0 = wave0.min()
@@ -78,6 +101,13 @@ def main():
               us(np.median(gaps)), us(np.percentile(gaps, 90)), us(np.percentile(gaps, 99)),
               us(gaps.sum()), 100.0 * gaps.sum() / ((f3 - f0).sum() + gaps.sum())))
     dur = f3 - f0
+    clk = tl[:, 5] / np.maximum(dur, 1) * 100.0  # MHz
+    mid = (f0 + f3) // 2
+    for lo_, hi_ in ((0.0, 0.1), (0.1, 0.5), (0.5, 0.9), (0.9, 1.0)):
+        a_, b_ = T0 + lo_ * (f3.max() - T0), T0 + hi_ * (f3.max() - T0)
+        sel_ = (mid >= a_) & (mid < b_)
+        print("core clock, frames centred in %3.0f-%3.0f%% of the span: %.0f MHz" % (
+            100 * lo_, 100 * hi_, np.median(clk[sel_])))
     print("frame time at full load: %.2f us per iteration (median of frame time / iterations)" % (
         us(np.median(dur / np.maximum(its, 1)))))
     # frames in flight over time
