@@ -157,7 +157,7 @@ __device__ __forceinline__ void log_ratio_n_packed(const double (&T)[n],
   double q[n];
   // wave-uniform at once (a per-lane flag held across the loop below costs a
   // VGPR and two conversions per call)
-  const bool any_special = __builtin_amdgcn_ballot_w64(ex::ratio_n<n>(T, q)) != 0;
+  const bool any_special = ex::ratio_n<n>(T, q);  // wave-uniform
   uint32_t pos[n];
   bool near[n];
   uint32_t base = 0;  // wave-uniform

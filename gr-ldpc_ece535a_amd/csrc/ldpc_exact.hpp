@@ -237,6 +237,7 @@ LDPC_HD void expm1_n(const double (&u)[n], const uint32_t (&hx)[n], double (&t)[
   constexpr double Q5 = -2.01099218183624371326e-07;
   double x[n], c[n], hxs[n], num[n], den[n], q[n];
   int k[n];
+  bool edge = false;
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     const uint32_t sgn = hiw(u[i]) & 0x80000000u;
@@ -245,8 +246,21 @@ LDPC_HD void expm1_n(const double (&u)[n], const uint32_t (&hx)[n], double (&t)[
     // 0x3FF0A2B2) instead of this rounding, but on that range (u < 0 here)
     // invln2 u - 0.5 lies in (-2, -1): the conversion gives -1 there too.
     // Only k = 0 needs its own select.
-    const int kc = (int)(invln2 * u[i] + from_hi(0x3fe00000u | sgn));
-    k[i] = hx[i] > 0x3fd62e42u ? kc : 0;
+    // Below the 0x3fd62e42 high word (|u| < 0.5 ln2 but for the top of that
+    // word) the rounding gives k = 0 as glibc's test does; only |u| in
+    // (0.5 ln2, 0x3fd62e42ffffffff] -- high word 0x3fd62e42, where glibc
+    // takes k = 0 and the rounding may give -1 -- needs the select, in a
+    // branch a wave takes only when one of its lanes has that high word.
+    k[i] = (int)(invln2 * u[i] + from_hi(0x3fe00000u | sgn));
+    edge |= hx[i] == 0x3fd62e42u;
+  }
+  if (LDPC_EX_ANY(edge)) {
+    LDPC_EX_COLD();
+#pragma unroll
+    for (int i = 0; i < n; ++i) k[i] = hx[i] > 0x3fd62e42u ? k[i] : 0;
+  }
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
     const RedEntry re = tab->red[k[i] - kTailLo];
     const double hi = u[i] - re.khi;
     const double lo = re.klo;
@@ -363,8 +377,13 @@ LDPC_HD void tanh_half_n(const double (&m)[n], double (&z)[n], const ExTab *tab)
   div_n<n>(num, den, q);
 #pragma unroll
   for (int i = 0; i < n; ++i) {
+    // glibc: 1 - q (|x| >= 1) or q, with x's sign.  |RN(q - 1)| = RN(1 - q)
+    // (rounding is odd-symmetric, 0 <= q <= 1) and RN(q + 0) = q (q > 0 here),
+    // so both are |q + w| with w = -1 or +0 -- one constant select (its low
+    // word is 0 either way) instead of a double one -- and the magnitude
+    // goes in with the sign transfer
     const bool big = (hm[i] & 0x7fffffffu) >= 0x40000000u;
-    const double r = big ? 1.0 - q[i] : q[i];  // >= 0: the sign is x's (m's)
+    const double r = q[i] + from_hi(big ? 0xbff00000u : 0u);
     const uint32_t zh = (hiw(r) & 0x7fffffffu) | (hm[i] & 0x80000000u);
     z[i] = dbl(((uint64_t)zh << 32) | (uint32_t)bits(r));
   }
@@ -493,22 +512,25 @@ inline double log_glibc(double x, const GlLogEntry *tab) {
 // every lane once T = 1 / NaN lanes divide by 1 and are selected away.
 // ---------------------------------------------------------------------------
 // the quotients (1 + T) / (1 - T) of log_ratio_n; returns whether a lane
-// holds a T of +-1 or NaN (its q is then a placeholder: see ratio_fix_n)
+// (device: any lane of the wave) holds a T of +-1 or NaN (its q is then a
+// placeholder: see ratio_fix_n)
 template <int n>
 LDPC_HD bool ratio_n(const double (&T)[n], double (&q)[n]) {
   static_assert(n <= 16, "the divisors (>= 2^-53 each) share one prefix product");
   double num[n], den[n];
-  bool special = false;
+  bool special = false;  // (device: any lane of the wave; host: this lane)
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     num[i] = 1.0 + T[i];
     den[i] = 1.0 - T[i];
-    special |= !(__builtin_fabs(T[i]) < 1.0);  // T = +-1 (2/0, 0/2) or NaN
+    // T = +-1 (2/0, 0/2) or NaN; one ballot per slot, OR-ed as scalar masks
+    // (a per-lane flag kept across the slots costs a select and a compare)
+    special |= LDPC_EX_ANY(!(__builtin_fabs(T[i]) < 1.0));
   }
   // 1 - T >= 2^-53 unless T = 1 or NaN: when some lane has one, every lane's
   // divisor is raised to >= 2^-60 (a finite quotient in the shared product;
   // the other lanes' divisors are unchanged) and ratio_fix_n replaces them
-  if (LDPC_EX_ANY(special)) {
+  if (special) {
     LDPC_EX_COLD();
 #pragma unroll
     for (int i = 0; i < n; ++i) den[i] = __builtin_fmax(den[i], 0x1p-60);
@@ -530,7 +552,7 @@ LDPC_HD void ratio_fix_n(const double (&T)[n], double (&E)[n]) {
 template <int n>
 LDPC_HD void log_ratio_n(const double (&T)[n], const ExTab *tab, double (&E)[n]) {
   double q[n];
-  const bool any_special = LDPC_EX_ANY(ratio_n<n>(T, q));
+  const bool any_special = ratio_n<n>(T, q);  // (wave-uniform on the device)
 #pragma unroll
   for (int i = 0; i < n; ++i) E[i] = log_q(q[i], tab->log);
   if (any_special) {

@@ -60,10 +60,18 @@ static_assert(kF == 2 || kF == 4, "frames per chunk: 2 or 4");
 // Workgroup b -> (chunk, block of the chunk).  With a multiple of 8 chunks,
 // chunk k's blocks run on XCD k mod 8 (the dispatcher deals workgroups to the
 // XCDs round robin), the XCD's chunks one after another.
-__device__ __forceinline__ void map_block(int b, int chunks, int nbpc, int &k, int &bi) {
+// rev: the XCD's chunks in the opposite order.  The variable pass runs them
+// backwards and the check pass forwards (a zigzag): each launch starts on the
+// chunks whose gathered table -- the row state the check pass just wrote, the
+// LQ the variable pass just wrote -- the previous launch wrote last, while it
+// is still in the XCD's L2.
+__device__ __forceinline__ void map_block(int b, int chunks, int nbpc, int &k, int &bi,
+                                          bool rev = false) {
   if ((chunks & 7) == 0) {
-    const int idx = b >> 3, c = idx / nbpc;
+    const int idx = b >> 3;
+    int c = idx / nbpc;
     bi = idx - c * nbpc;
+    if (rev) c = (chunks >> 3) - 1 - c;
     k = (b & 7) + 8 * c;
   } else {
     k = b / nbpc;
@@ -320,6 +328,9 @@ __device__ __forceinline__ void check_row(const MsnView &g, const MsnWork &w, in
 // per frame f, "a row of these blocks is unsatisfied" (bits 12(f+1)..), in
 // two levels (8 group words per chunk, then the chunk's word); no fence and
 // no waiting (a chunk that is not live decides in its block 0 alone).
+#ifndef LDPC_MSN_ZIGZAG
+#define LDPC_MSN_ZIGZAG 1  // the variable pass walks each XCD's chunks backwards
+#endif
 // occupancy hints (waves per SIMD; A/B knobs)
 #ifndef LDPC_MSN_CHECK_MINB
 #define LDPC_MSN_CHECK_MINB 1
@@ -611,7 +622,7 @@ __device__ void var_edges_rt(const MsnView &g, const MsnWork &w, int k, const in
 template <typename Real, int DV>
 __global__ void __launch_bounds__(256, LDPC_MSN_VAR_MINB) msn_var(MsnView g, MsnWork w, DecodeArgs a, int nb) {
   int k, bi;
-  map_block(blockIdx.x, w.chunks, w.nb_var, k, bi);
+  map_block(blockIdx.x, w.chunks, w.nb_var, k, bi, LDPC_MSN_ZIGZAG != 0);
   const int m = nb * w.chunks + k;  // the decision's mask buffer
   const uint32_t run = ld_uniform(&w.run[m]), fill = ld_uniform(&w.fill[m]),
                  stop = ld_uniform(&w.stop[m]);
