@@ -144,7 +144,6 @@ struct ldpc_ctx {
   double dbg[6] = {0, 0, 0, 0, 0, 0};  // ... and the host's sight of the first result
   bool srv_debug = false;  // LDPC_SERVE_DEBUG, read when a launch starts
   bool srv_test_skip_check = false;  // ldpc_test_hook(LDPC_TEST_SERVE_UNCHECKED)
-  long long srv_run_rounds = 0;  // rounds posted as run tables (LDPC_SERVE_DEBUG)
   // the frame ring (ldpc_ring_*, ldpc_ring.hip): mapped host memory
   // [kRingSlots descriptors | kRingSlots completion words], device memory
   // [per-slot frame counters | queue head], the launch's own stream and an
@@ -418,38 +417,6 @@ void serve_post(ldpc_ctx *ctx, uint32_t B) {
                    ((uint64_t)ctx->srv_epoch << 32) | ((uint64_t)(ctx->srv_launches & 0xFFF) << 20) |
                        (B & ldpc::kServeB),
                    __ATOMIC_RELEASE);
-}
-
-// The run table of a round (ldpc_kernels.hpp kServeRunFlag): greedy runs of
-// keys base + (i / pair) * stride + i % pair, pair 1 or 2, in list order.
-// Returns R (rt[1 + 2 r], rt[2 + 2 r]: run r's words, untagged), or 0 when
-// the round needs more than kServeMaxRuns runs (it then goes key by key).
-int serve_runs(const int64_t *w, int n, uint64_t *rt) {
-  int R = 0;
-  for (int i = 0; i < n;) {
-    if (R == ldpc::kServeMaxRuns) return 0;
-    // pair 1: w[i] + j * stride
-    int c1 = 1;
-    int64_t s1 = 0;
-    if (i + 1 < n && w[i + 1] > w[i] && w[i + 1] - w[i] < (1 << 19)) {
-      s1 = w[i + 1] - w[i];
-      while (i + c1 < n && c1 < (1 << 20) - 1 && w[i + c1] == w[i] + c1 * s1) ++c1;
-    }
-    // pair 2: (w[i], w[i] + 1), (w[i] + stride, w[i] + stride + 1), ...
-    int c2 = 0;
-    int64_t s2 = 0;
-    if (i + 2 < n && w[i + 1] == w[i] + 1 && w[i + 2] > w[i] + 1 && w[i + 2] - w[i] < (1 << 19)) {
-      s2 = w[i + 2] - w[i];
-      while (i + c2 < n && c2 < (1 << 20) - 1 && w[i + c2] == w[i] + (c2 / 2) * s2 + (c2 % 2)) ++c2;
-    }
-    const bool pair = c2 > c1;
-    const int c = pair ? c2 : c1;
-    rt[1 + 2 * R] = (uint64_t)w[i];
-    rt[2 + 2 * R] = ((uint64_t)c << 20) | ((uint64_t)(pair ? s2 : s1) << 1) | (pair ? 1u : 0u);
-    ++R;
-    i += c;
-  }
-  return R;
 }
 
 // Ends a running window server: posts its quit round and waits for the
@@ -1798,7 +1765,7 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
   const bool host_check = !ctx->srv_test_skip_check;
   ctx->srv_test_skip_check = false;
   for (int b = 0; b < B; ++b)
-    if (win[b] < 0 || win[b] >= ((int64_t)1 << 39) ||
+    if (win[b] < 0 || win[b] >= ((int64_t)1 << 40) ||
         (host_check && (win[b] >> 1) + N > ctx->span_samples))
       return set_err(ctx, LDPC_EINVAL, "window outside the staged span");
   int device_fault = 0;  // a granule that carries no decode (kServeBadKey / kServeLostKey)
@@ -1819,19 +1786,9 @@ int serve_windows_impl(ldpc_ctx *ctx, const int64_t *win, int B, uint8_t *out_pa
       ctx->serving = true;
     }
     // each key carries the epoch it is posted with (mod 2^24), so the poller
-    // can tell a slot it read before this round's write (ldpc_serve.hip).  A
-    // round that is at most kServeMaxRuns runs goes as its run table (the
-    // poller copies 1 + 2 R words instead of n keys, ldpc_kernels.hpp)
+    // can tell a slot it read before this round's write (ldpc_serve.hip)
     const uint64_t ktag = (uint64_t)((ctx->srv_epoch + 1) & 0xFFFFFFu) << 40;
-    uint64_t rt[1 + 2 * ldpc::kServeMaxRuns];
-    const int R = serve_runs(win + b0, n, rt);
-    if (R > 0) {
-      for (int t = 1; t <= 2 * R; ++t) keys[t] = (int64_t)(rt[t] | ktag);
-      keys[0] = (int64_t)(ldpc::kServeRunFlag | (uint64_t)R | ktag);
-      ctx->srv_run_rounds += 1;
-    } else {
-      for (int b = 0; b < n; ++b) keys[b] = (int64_t)((uint64_t)win[b0 + b] | ktag);
-    }
+    for (int b = 0; b < n; ++b) keys[b] = (int64_t)((uint64_t)win[b0 + b] | ktag);
     serve_post(ctx, (uint32_t)n);
     ctx->srv_rounds += 1;
     const uint32_t tag = ctx->srv_epoch & 0x7FFFFFu;
@@ -2100,7 +2057,6 @@ int ldpc_serve_end(ldpc_ctx *ctx) {
             "first result seen %.1f us after the post (mean over rounds)\n",
             ctx->dbg[0], ctx->dbg[1] / ctx->dbg[0], ctx->dbg[2] / ctx->dbg[0],
             ctx->dbg[3] / ctx->dbg[0], ctx->dbg[4] / ctx->dbg[0], ctx->dbg[5] / ctx->dbg[0]);
-    fprintf(stderr, "ldpc_serve: %lld rounds posted as run tables\n", ctx->srv_run_rounds);
     for (double &d : ctx->dbg) d = 0;
     uint32_t census = 0;
     (void)hipMemcpy(&census, ctx->d_srv_ctl + 16 * ldpc::kServeCopies, 4, hipMemcpyDeviceToHost);

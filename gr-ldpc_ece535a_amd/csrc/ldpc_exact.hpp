@@ -344,8 +344,14 @@ LDPC_HD void tanh_half_n(const double (&m)[n], double (&z)[n], const ExTab *tab)
     const uint32_t im = hm[i] & 0x7fffffffu;
     // u = |m| for |x| >= 1, else -|m|: the sign bit of im - bits(2.0)
     u[i] = dbl(((uint64_t)(im | ((im - 0x40000000u) & 0x80000000u)) << 32) | (uint32_t)bits(m[i]));
-    // outside [2^-54, 13.5): |x| < 2^-55, inf, NaN, or possibly k >= 20
-    special |= im - 0x3c900000u >= 0x402b0000u - 0x3c900000u;
+    // outside [2^-54, 13.5): |x| < 2^-55, inf, NaN, or possibly k >= 20 --
+    // but for m = +-0, which the general path below gets right (expm1's k = 0
+    // reduction of u = -0 gives t = +-0, q = +-0 / 2, and the sign is m's: the
+    // +-0 glibc returns for x (1 + x)).  The zeros are not rare: a column of
+    // degree 1 has no other edge, so its bit message is the empty sum +0.0
+    // every iteration (3 of the reference H's 64 columns), and with them in
+    // the special set every wave took the special branches every iteration
+    special |= im - 0x3c900000u >= 0x402b0000u - 0x3c900000u && m[i] != 0.0;
   }
   const bool any_special = LDPC_EX_ANY(special);
   if (any_special) {

@@ -32,6 +32,18 @@ __device__ __forceinline__ void wave_lds_sync() {
 #endif
 }
 
+#ifdef LDPC_PATH_STATS
+// Diagnostic builds only (tools/path_stats.py): per wave-iteration of the
+// column-centric sum-product loop, how often the exact arithmetic's rare
+// paths run and how often every lane's operands are saturated.
+//   [0] wave-iterations  [1] some T = +-1 / NaN  [2] every real T in {+-1, NaN, 0}
+//   [3] some nonzero |m| outside [2^-54, 13.5) or NaN  [4] every |m| >= 38.2 or NaN
+//   [7] some |m| >= 13.5 (expm1's k >= 20 formula)
+//   [5] every check message equal (bitwise) to the previous iteration's
+//   [6] [5] and every bit message too (an exact fixed point)
+__device__ unsigned long long g_path_stats[8];
+#endif
+
 #ifndef LDPC_TANH_SPLIT
 #define LDPC_TANH_SPLIT 16.0  // |m| below which the single-range tanh(m/2) is used
 #endif
@@ -258,6 +270,14 @@ __device__ __forceinline__ FrameResult decode_frame(const CodeView &code, const 
 #pragma unroll
       for (int k = 0; k < DVN; ++k) lds_st<Real>(ta[q][k], t0);
     }
+#ifdef LDPC_PATH_STATS
+    bool st_same = false;
+    double st_prev[NW][DVN];
+#pragma unroll
+    for (int q = 0; q < NW; ++q)
+#pragma unroll
+      for (int k = 0; k < DVN; ++k) st_prev[q][k] = __builtin_nan("");
+#endif
     const uint32_t fair = FAIR ? a.fair_cycles : 0u;  // 0: no issue-priority management
     uint64_t t_prev = fair ? __builtin_amdgcn_s_memtime() : 0;
     for (int h = 0; h < a.max_iters; ++h) {
@@ -295,6 +315,28 @@ __device__ __forceinline__ FrameResult decode_frame(const CodeView &code, const 
           log_ratio_n_packed<S>(Ts, logtab, Es, tb, lane);
         else
           Math<PREC>::template check_msg_n<S>(Ts, logtab, Es);
+#ifdef LDPC_PATH_STATS
+        if constexpr (PREC == 0) {
+          bool some = false, all = true, same = true;
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const double T = (double)Ts[s];
+            const bool sat = !(__builtin_fabs(T) < 1.0);
+            some |= sat;
+            all &= sat || T == 0.0;
+            same &= __builtin_bit_cast(uint64_t, (double)Es[s]) ==
+                    __builtin_bit_cast(uint64_t, (double)eb[lane + 64 * s]);
+          }
+          const bool s1 = __ballot(some) != 0, a1 = __ballot(!all) == 0, e1 = __ballot(!same) == 0;
+          st_same = e1;
+          if (lane == 0) {
+            atomicAdd(&g_path_stats[0], 1ull);
+            if (s1) atomicAdd(&g_path_stats[1], 1ull);
+            if (a1) atomicAdd(&g_path_stats[2], 1ull);
+            if (e1) atomicAdd(&g_path_stats[5], 1ull);
+          }
+        }
+#endif
 #pragma unroll
         for (int s = 0; s < S; ++s) eb[lane + 64 * s] = Es[s];
       } else if constexpr (FIN && LDPC_TANH_SPLIT > 0) {
@@ -392,6 +434,30 @@ __device__ __forceinline__ FrameResult decode_frame(const CodeView &code, const 
           }
           mv[q][k] = m;
         }
+#ifdef LDPC_PATH_STATS
+      if constexpr (PREC == 0) {
+        bool some = false, all = true, same = true, big = false;
+#pragma unroll
+        for (int q = 0; q < NW; ++q)
+#pragma unroll
+          for (int k = 0; k < DVN; ++k) {
+            const double m = (double)mv[q][k], am = __builtin_fabs(m);
+            some |= !(am >= 0x1p-54 && am < 13.5) && am != 0.0;
+            big |= am >= 13.5;
+            all &= !(am < 38.2);
+            same &= __builtin_bit_cast(uint64_t, m) == __builtin_bit_cast(uint64_t, st_prev[q][k]);
+            st_prev[q][k] = m;
+          }
+        const bool s1 = __ballot(some) != 0, a1 = __ballot(!all) == 0, e1 = __ballot(!same) == 0;
+        const bool b1 = __ballot(big) != 0;
+        if (lane == 0) {
+          if (s1) atomicAdd(&g_path_stats[3], 1ull);
+          if (b1) atomicAdd(&g_path_stats[7], 1ull);
+          if (a1) atomicAdd(&g_path_stats[4], 1ull);
+          if (e1 && st_same) atomicAdd(&g_path_stats[6], 1ull);
+        }
+      }
+#endif
       if constexpr (PREC != 3) {
         // tanh(m/2), :509: glibc's, bit for bit; mode 0 forms the column's
         // DVN quotients from one reciprocal

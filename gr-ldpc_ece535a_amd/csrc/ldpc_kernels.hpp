@@ -141,17 +141,6 @@ struct alignas(16) ServeArgs {
 // error of the round.
 constexpr uint32_t kServeBadKey = 511;   // the key's window is outside the staged span
 constexpr uint32_t kServeLostKey = 510;  // the key never showed the round's tag (deadline)
-// A round may come as runs instead of one key per window (the block's rounds
-// are mostly contiguous search positions at both polarities, or grid
-// positions at one stride): key slot 0 = tag | kServeRunFlag | R, then per
-// run w0 = tag | base key, w1 = tag | count << 20 | stride << 1 | (pair - 1);
-// window i of a run has key base + (i / pair) * stride + i % pair (pair 2:
-// both polarities of a position).  Window keys stay below 2^39.
-constexpr uint64_t kServeRunFlag = 1ull << 39;
-#ifndef LDPC_SERVE_MAX_RUNS
-#define LDPC_SERVE_MAX_RUNS 7  // (A/B: 0 posts every round key by key)
-#endif
-constexpr int kServeMaxRuns = LDPC_SERVE_MAX_RUNS;  // 1 + 2 R words fit a copy line beside the round word
 // Epochs stay below this (the host restarts a session before it); a round's
 // result tag is epoch mod 2^23.
 constexpr uint32_t kServeEpochLimit = (1u << 23) - (1u << 16);

@@ -56,10 +56,6 @@ __device__ __forceinline__ uint64_t sys_load(const uint64_t *p) {
 __device__ __forceinline__ void sys_store(uint64_t *p, uint64_t v) {
   __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int l) {
-  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
-         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-}
 
 // The round as the poller publishes it, one 8-byte granule: epoch (bits
 // 40..63), the decoders sharing it (20..39), B (0..19).  A decoder takes the
@@ -70,46 +66,8 @@ __device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int l) {
 // to kCopies lines of ctl, and decoder g polls copy g % kCopies: a thousand
 // decoders polling one line queue behind each other for microseconds.
 constexpr uint64_t kQuitRound = ~0ull;  // epoch all ones: every decoder leaves
-// bit 39 (the top bit of the decoder count, which stays below 2^19): the round
-// came as runs (kServeRunFlag), its table in words 1.. of every copy line
-__device__ __forceinline__ uint64_t ctl_word(uint32_t ep, uint32_t live, uint32_t B, bool runs) {
-  return ((uint64_t)ep << 40) | ((uint64_t)(live & 0x7FFFFu) << 20) | (runs ? 1ull << 39 : 0ull) |
-         (B & 0xFFFFFu);
-}
-// The round's run table as the poller publishes it: word 1 + t of every copy
-// line holds slot t (0: the header, tag | kServeRunFlag | R; then two words
-// per run, ldpc_kernels.hpp), each with the host's epoch tag.  A wave reads
-// the table with one instruction (lane t: slot t) and waits out older tags;
-// false if the table never shows this round's tags (the host is gone).
-__device__ __forceinline__ bool read_runs(const uint64_t *line, uint64_t ktag, uint64_t deadline,
-                                          int lane, uint64_t &w) {
-  const uint64_t t0 = ticks();
-  constexpr int kSlots = 1 + 2 * (kServeMaxRuns > 0 ? kServeMaxRuns : 1);
-  w = lane < kSlots ? agent_load(line + 1 + lane) : 0;
-  for (;;) {
-    const uint64_t hdr = lane_bcast(w, 0);
-    const int n = (hdr >> 40) == ktag ? 1 + 2 * (int)(hdr & 0xFFu) : 1;
-    if (__ballot(lane < n && (w >> 40) < ktag) == 0)
-      return __ballot(lane < n && (w >> 40) != ktag) == 0 && (hdr & kServeRunFlag) != 0 &&
-             (int)(hdr & 0xFFu) <= kServeMaxRuns;
-    if (ticks() - t0 > deadline) return false;
-    if (lane < kSlots && (w >> 40) < ktag) w = agent_load(line + 1 + lane);
-  }
-}
-// Window b's key from the run table (wave-uniform; -1 past the runs)
-__device__ __forceinline__ int64_t run_key(uint64_t w, int64_t b) {
-  const int R = (int)(lane_bcast(w, 0) & 0xFFu);
-  int64_t off = 0;
-  for (int r = 0; r < R; ++r) {
-    const uint64_t w0 = lane_bcast(w, 1 + 2 * r), w1 = lane_bcast(w, 2 + 2 * r);
-    const int64_t count = (int64_t)((w1 >> 20) & 0xFFFFFu);
-    if (b < off + count) {
-      const int64_t i = b - off, m = (int64_t)(w1 & 1u) + 1, outer = (int64_t)((w1 >> 1) & 0x7FFFFu);
-      return (int64_t)(w0 & ((1ull << 39) - 1)) + (i / m) * outer + (i % m);
-    }
-    off += count;
-  }
-  return -1;
+__device__ __forceinline__ uint64_t ctl_word(uint32_t ep, uint32_t live, uint32_t B) {
+  return ((uint64_t)ep << 40) | ((uint64_t)(live & 0xFFFFFu) << 20) | (B & 0xFFFFFu);
 }
 __device__ __forceinline__ uint64_t *ctl_copy(uint64_t *ctl, int i) { return ctl + 16 * i; }
 // Where window b's key is published: keys of the first kInlineKeys windows
@@ -156,6 +114,10 @@ __device__ __forceinline__ void dbg_add(uint64_t *p) {
   __hip_atomic_fetch_add((__attribute__((address_space(1))) uint64_t *)p, (uint64_t)1,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
 __device__ __forceinline__ uint64_t wave_uniform(uint64_t v) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
@@ -194,27 +156,15 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
       const uint64_t tag = (uint64_t)(ep & 0xFFFFFFu);
       const uint64_t t_keys = ticks();
       bool lost = false;  // a key slot that never showed this epoch (the host is gone)
-      // key slot 0 says how the round came: a run table (its header, with
-      // kServeRunFlag) or the first window's key
-      uint64_t hdr = lane_bcast(v[0], 1);
-      while (B > 0 && (hdr >> 40) < tag && !lost) {
-        hdr = sys_load((const uint64_t *)s.keys);
-        if (ticks() - t_keys > s.deadline) lost = true;
-      }
-      if (lane == 1) v[0] = hdr;
-      const bool runs = B > 0 && (hdr >> 40) == tag && (hdr & kServeRunFlag) != 0 &&
-                        (int)(hdr & 0xFFu) <= kServeMaxRuns;
-      const int64_t nslots = runs ? 1 + 2 * (int64_t)(hdr & 0xFFu) : B;
-      uint64_t runw = 0;  // runs: lane 1 + t holds slot t
       // key slot c + 64 j + lane; kKeyLoads loads in flight per lane (the
       // first group, c = -1, is the poll's own read)
-      for (int64_t c = -1; c < nslots && !lost; c += 64 * kKeyLoads) {
+      for (int64_t c = -1; c < B && !lost; c += 64 * kKeyLoads) {
         uint64_t k[kKeyLoads];
         bool in[kKeyLoads];
 #pragma unroll
         for (int j = 0; j < kKeyLoads; ++j) {
           const int64_t b = c + 64 * j + lane;
-          in[j] = b >= 0 && b < nslots;
+          in[j] = b >= 0 && b < B;
           k[j] = c < 0 ? v[j] : (in[j] ? sys_load((const uint64_t *)s.keys + b) : 0);
         }
 #pragma unroll
@@ -226,20 +176,9 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
             if (in[j] && (k[j] >> 40) < tag) k[j] = sys_load((const uint64_t *)s.keys + b);
             if (ticks() - t_keys > s.deadline) lost = true;
           }
-          if (runs) {
-            if (c < 0 && j == 0) runw = k[0];
-          } else if (in[j]) {
-            agent_store(key_slot(s, b), k[j]);
-          }
+          if (in[j]) agent_store(key_slot(s, b), k[j]);
         }
       }
-      // runs: the table into words 1.. of every copy line, so each decoder's
-      // poll line holds it
-      if (runs && !lost)
-        for (int t = 0; t < (int)nslots; ++t) {
-          const uint64_t val = lane_bcast(runw, t + 1);
-          if (lane < kServeCopies) agent_store(ctl_copy(s.ctl, lane) + 1 + t, val);
-        }
       if (lost) {
         if (lane < kServeCopies) agent_store(ctl_copy(s.ctl, lane), kQuitRound);
         if (lane == 0) agent_store(diag(s.ctl, kDiagExit), 3);
@@ -260,7 +199,7 @@ __device__ __forceinline__ void poll_rounds(const ServeArgs &s, int lane) {
         }
         live = (uint32_t)__builtin_amdgcn_readfirstlane((int)live);
       }
-      const uint64_t w = quit ? kQuitRound : ctl_word(ep, live, (uint32_t)B, runs);
+      const uint64_t w = quit ? kQuitRound : ctl_word(ep, live, (uint32_t)B);
       if (lane < kServeCopies) agent_store(ctl_copy(s.ctl, lane), w);
       if (s.debug && lane == 0) {
         agent_store(diag(s.ctl, kDiagSeen), t_seen);
@@ -362,9 +301,7 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
       // A slot that still holds an older tag is read again; one that never
       // shows this round's tag within the deadline, or already shows a later
       // round's, yields no key (-1: a kServeLostKey granule, no gather).
-      // (A round of runs: wave 0 derives the key below.)
-      if (r != kQuitRound && !(r & kServeRunFlag) && g < (int64_t)(r & 0xFFFFFu) &&
-          (int64_t)(r & 0xFFFFFu) <= (int64_t)((r >> 20) & 0x7FFFFu)) {
+      if (r != kQuitRound && g < (int64_t)(r & 0xFFFFFu) && (int64_t)(r & 0xFFFFFu) <= (int64_t)((r >> 20) & 0xFFFFFu)) {
         const uint64_t ktag = (r >> 40) & 0xFFFFFFu;
         const uint64_t t_k = ticks();
         while ((k >> 40) < ktag && ticks() - t_k <= s.deadline) k = agent_load(my_key);
@@ -376,17 +313,7 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
     const uint64_t r = (uint64_t)sslot[0];
     if (r == kQuitRound) return;  // every thread of the workgroup
     const uint32_t ep = (uint32_t)(r >> 40), B = (uint32_t)r & 0xFFFFFu;
-    const int64_t G = (int64_t)((r >> 20) & 0x7FFFFu);
-    const bool runs = (r & kServeRunFlag) != 0;
-    if (runs && (int64_t)B <= G) {  // workgroup form: wave 0 derives this decoder's key
-      if (wave == 0 && g < (int64_t)B) {
-        uint64_t rw;
-        const bool ok = read_runs(poll, (uint64_t)(ep & 0xFFFFFFu), s.deadline, lane, rw);
-        const int64_t key = ok ? run_key(rw, g) : -1;
-        if (lane == 0) sslot[1] = key;
-      }
-      __syncthreads();
-    }
+    const int64_t G = (int64_t)((r >> 20) & 0xFFFFFu);
     const uint64_t tag = (uint64_t)((ep & 0x7FFFFFu) << 9) << 32;
     if (s.debug && tid == 0 && (g & 63) == 0) {  // diagnostics: rounds seen (sampled decoders)
       dbg_add(diag(s.ctl, kDiagStarts));
@@ -435,26 +362,17 @@ __global__ void __launch_bounds__(64 * S, kServeWavesPerSimd) serve_kernel(CodeV
     } else {
       // one window per wave
       const int64_t W = G * S;
-      uint64_t rw = 0;
-      bool rok = false;
-      if (runs && g < G && g * S + wave < (int64_t)B)
-        rok = read_runs(poll, (uint64_t)(ep & 0xFFFFFFu), s.deadline, lane, rw);
       for (int64_t b = g * S + wave; b < (int64_t)B && g < G; b += W) {
         // the key, once it carries this round's tag: an older tag is read
         // again (bounded); a key that never shows this round's tag is not
         // decoded (a kServeLostKey granule), nor is one outside the span
         // (kServeBadKey) -- no gather ever uses a key the checks did not pass
         const uint64_t ktag = ep & 0xFFFFFFu;
-        int64_t key = -1;
-        if (runs) {
-          key = rok ? run_key(rw, b) : -1;
-        } else {
-          uint64_t kk = wave_uniform(agent_load(key_slot(s, b)));
-          const uint64_t t_k = ticks();
-          while ((kk >> 40) < ktag && ticks() - t_k <= s.deadline)
-            kk = wave_uniform(agent_load(key_slot(s, b)));
-          key = (kk >> 40) == ktag ? (int64_t)(kk & ((1ull << 40) - 1)) : -1;
-        }
+        uint64_t kk = wave_uniform(agent_load(key_slot(s, b)));
+        const uint64_t t_k = ticks();
+        while ((kk >> 40) < ktag && ticks() - t_k <= s.deadline)
+          kk = wave_uniform(agent_load(key_slot(s, b)));
+        const int64_t key = (kk >> 40) == ktag ? (int64_t)(kk & ((1ull << 40) - 1)) : -1;
         const uint32_t why = key_fault(key, code.N, s.span);
         if (why) {
           if (lane == 0) sys_store(s.res + b, tag | ((uint64_t)why << 32));

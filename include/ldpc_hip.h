@@ -265,9 +265,7 @@ int ldpc_stage_span(ldpc_ctx *ctx, const float *in, int64_t n_in_floats, int ele
  * and sum-product on small codes with KB <= 4 (the reference's codes); other
  * codes and methods return LDPC_EUNSUPPORTED and the caller keeps
  * ldpc_decode_windows.  ldpc_serve_windows decodes one round: windows and
- * outputs as for ldpc_decode_windows (et_period 1; window keys < 2^39; a round
- * of at most 7 runs of equally spaced windows or position pairs is handed to
- * the device as those runs), synchronous -- it returns
+ * outputs as for ldpc_decode_windows (et_period 1), synchronous -- it returns
  * when every result is in (LDPC_ETIMEOUT after 10 s).  ldpc_serve_end lets
  * the launch finish without waiting for it.  Any other call on the context
  * that uses its stream ends a running server first.

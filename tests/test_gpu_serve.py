@@ -177,43 +177,3 @@ def test_serve_epoch_limit_restarts_the_session():
     dec.serve_end()
     dec.close()
     assert max(seen) < SERVE_EPOCH_LIMIT and min(seen) < 16  # it restarted
-
-
-def _run_rounds(rng, span_len, N):
-    """Rounds shaped like the block's: a sample-by-sample search at both
-    polarities, grid frames at both polarities or one, and mixes of them with
-    scattered windows (more than 7 runs: posted key by key)."""
-    def pairs(p0, n, step):
-        return [((p0 + step * i) << 1) | b for i in range(n) for b in (0, 1)]
-    hi = span_len - N - 64 * 70
-    out = []
-    for _ in range(3):
-        p0 = int(rng.integers(0, hi))
-        out.append(pairs(p0, int(rng.integers(1, 130)), 1))                   # search
-        out.append(pairs(p0, int(rng.integers(1, 60)), 64))                   # grid, both
-        out.append([(p0 + 64 * i) << 1 for i in range(int(rng.integers(2, 60)))])  # grid, one
-        mix = pairs(p0, 40, 1) + pairs(p0 + 3000, 20, 64) + [((p0 + 77) << 1) | 1]
-        out.append(mix)
-        out.append(mix + [int(x) for x in _windows(rng, 12, span_len, N)])  # > 7 runs
-        out.append([int(x) for x in _windows(rng, 1, span_len, N)])
-    return [np.array(w, np.int64) for w in out]
-
-
-@pytest.mark.parametrize("method,iters", [(1, 5), (0, 50)])
-def test_serve_run_rounds_equal_oracle(method, iters):
-    """Rounds of runs (posted as run tables, ldpc_kernels.hpp kServeRunFlag)
-    and rounds that need more than 7 runs (key by key), alternating on one
-    server: every window equals the oracle and ldpc_decode_windows."""
-    dec = L.Decoder()
-    Hr = dec.H
-    s = _span(Hr, 5000, 51 + method)
-    rng = np.random.default_rng(12)
-    dec.stage_span(s, max_windows=8192)
-    dec.serve_begin(method=method, max_iters=iters, max_windows=8192)
-    rounds = _run_rounds(rng, s.size, dec.N)
-    got = [dec.serve_windows(w) for w in rounds]
-    dec.serve_end()
-    for w, g in zip(rounds, got):
-        ref = _oracle(method, Hr, s, w, iters)
-        assert (g["packed"] == ref["packed"]).all() and (g["synd"] == ref["synd"]).all()
-    dec.close()

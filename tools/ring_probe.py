@@ -18,10 +18,13 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import ldpc_ece535a as L  # noqa: E402
 
+ITERS = int(os.environ.get("ITERS", "50"))  # iteration cap of every session
+EBN0 = float(os.environ.get("EBN0", "2.0"))
+
 
 def session_n(dec, ins, pool, sp, st, n):
     """An untimed ring session of n batches (the pool is reused)."""
-    dec.ring_begin(method=1, max_iters=50, stream=sp)
+    dec.ring_begin(method=1, max_iters=ITERS, stream=sp)
     for k in range(n):
         pk, it, sy = pool[k % len(pool)]
         dec.ring_post(ins[k % 4].data_ptr(), pk.shape[0], pk.data_ptr(), it.data_ptr(), sy.data_ptr())
@@ -33,7 +36,7 @@ def main():
     dev = torch.device("cuda", 0)
     dec = L.Decoder()
     B = 4096
-    ins = [bench.synth_device(L, torch, dec, B, 2.0, 2024 + 104729 * j, dev)[0] for j in range(4)]
+    ins = [bench.synth_device(L, torch, dec, B, EBN0, 2024 + 104729 * j, dev)[0] for j in range(4)]
     st = torch.cuda.Stream(dev)
     sp = ctypes.c_void_p(st.cuda_stream)
     K = int(os.environ.get("K", "20"))
@@ -49,7 +52,7 @@ def main():
         if pre_sleep:
             with torch.cuda.stream(st):
                 torch.cuda._sleep(int(pre_sleep))
-        dec.ring_begin(method=1, max_iters=50, stream=sp)
+        dec.ring_begin(method=1, max_iters=ITERS, stream=sp)
         tp = []
         for k in range(K):
             a = time.perf_counter()
