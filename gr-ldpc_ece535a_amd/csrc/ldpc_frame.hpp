@@ -39,9 +39,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 //   [0] wave-iterations  [1] some T = +-1 / NaN  [2] every real T in {+-1, NaN, 0}
 //   [3] some nonzero |m| outside [2^-54, 13.5) or NaN  [4] every |m| >= 38.2 or NaN
 //   [7] some |m| >= 13.5 (expm1's k >= 20 formula)
+//   [8] sum of near-1 log operands per wave-iteration  [9] wave-iterations with > 64 of them
+//   [10] sum of those with q == 1 exactly  [11] wave-iterations with > 64 without those
 //   [5] every check message equal (bitwise) to the previous iteration's
 //   [6] [5] and every bit message too (an exact fixed point)
-__device__ unsigned long long g_path_stats[8];
+__device__ unsigned long long g_path_stats[12];
 #endif
 
 #ifndef LDPC_TANH_SPLIT
@@ -329,7 +331,19 @@ __device__ __forceinline__ FrameResult decode_frame(const CodeView &code, const 
           }
           const bool s1 = __ballot(some) != 0, a1 = __ballot(!all) == 0, e1 = __ballot(!same) == 0;
           st_same = e1;
+          int nbase = 0, nunit = 0;
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            const double T = (double)Ts[s], q = (1.0 + T) / (1.0 - T);
+            const bool near = ex::log_is_near1(q);
+            nbase += __popcll(__ballot(near));
+            nunit += __popcll(__ballot(near && q == 1.0));
+          }
           if (lane == 0) {
+            atomicAdd(&g_path_stats[8], (unsigned long long)nbase);
+            if (nbase > 64) atomicAdd(&g_path_stats[9], 1ull);
+            atomicAdd(&g_path_stats[10], (unsigned long long)nunit);
+            if (nbase - nunit > 64) atomicAdd(&g_path_stats[11], 1ull);
             atomicAdd(&g_path_stats[0], 1ull);
             if (s1) atomicAdd(&g_path_stats[1], 1ull);
             if (a1) atomicAdd(&g_path_stats[2], 1ull);

@@ -428,11 +428,11 @@ int launch_ring(const CodeView &code, const RingArgs &r, int method, int prec, i
 
 #ifdef LDPC_PATH_STATS
 extern "C" int ldpc_debug_path_stats(unsigned long long *host, int reset) {
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ldpc::g_path_stats), 8 * sizeof(unsigned long long)) !=
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ldpc::g_path_stats), 12 * sizeof(unsigned long long)) !=
       hipSuccess)
     return -1;
   if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(ldpc::g_path_stats), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;

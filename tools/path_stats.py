@@ -25,7 +25,9 @@ import ldpc_ece535a as L  # noqa: E402
 NAMES = ["wave-iterations", "some T = +-1 / NaN", "every real T in {+-1, NaN, 0}",
          "some nonzero |m| outside [2^-54, 13.5)", "every |m| >= 38.2 or NaN",
          "check messages repeat", "check and bit messages repeat (fixed point)",
-         "some |m| >= 13.5 (expm1 k >= 20)"]
+         "some |m| >= 13.5 (expm1 k >= 20)", "near-1 log operands (sum)",
+         "wave-iterations with > 64 near-1 operands", "near-1 operands with q == 1 (sum)",
+         "wave-iterations with > 64 near-1 operands other than q == 1"]
 
 
 def main():
@@ -43,7 +45,7 @@ def main():
                  torch.empty(B, dtype=torch.int32, device=dev),
                  torch.empty(B, dtype=torch.int32, device=dev)) for _ in range(K)]
         st = torch.cuda.Stream(dev)
-        buf = np.zeros(8, np.uint64)
+        buf = np.zeros(12, np.uint64)
         torch.cuda.synchronize()
         lib.ldpc_debug_path_stats(buf.ctypes.data, 1)
         dec.ring_begin(method=1, max_iters=50, stream=ctypes.c_void_p(st.cuda_stream))
@@ -58,7 +60,7 @@ def main():
         print("Eb/N0 %g dB: %d frames, mean iterations %.2f, %.1f%% at the cap" %
               (db, iters.size, iters.mean(), 100.0 * (iters >= 50).mean()))
         print("  %-46s %12d" % (NAMES[0], int(buf[0])))
-        for i in range(1, 8):
+        for i in range(1, 12):
             print("  %-46s %12d  %6.2f%%" % (NAMES[i], int(buf[i]), 100.0 * buf[i] / max(n, 1)))
 
 
