@@ -158,33 +158,46 @@ __device__ __forceinline__ void log_ratio_n_packed(const double (&T)[n],
   // wave-uniform at once (a per-lane flag held across the loop below costs a
   // VGPR and two conversions per call)
   const bool any_special = ex::ratio_n<n>(T, q);  // wave-uniform
+  // q = 1 exactly (T = +-0: every padding cell, the rows with a degree-1
+  // column; or a tiny |T|) is glibc's log(1) = +0 without evaluating it: those
+  // lanes read the +0 in the last scratch slot instead of a packed result.
+  // They are half the near-1 operands of the headline workload, and without
+  // them 9 % rather than 60 % of wave-iterations need a second packed pass
+  // (tools/path_stats.py).  The packed ones fill [0, base), base <= 64 n - 1
+  // whenever a lane is unit, so the slot survives.
+  constexpr uint32_t kUnitSlot = 64 * n - 1;
+  if (lane == 0) scratch[kUnitSlot] = 0.0;
   uint32_t pos[n];
-  bool near[n];
+  bool near[n], packed[n];
   uint32_t base = 0;  // wave-uniform
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     E[i] = ex::log_main(q[i], tab->log);
     near[i] = ex::log_is_near1(q[i]);
-    const uint64_t m = __builtin_amdgcn_ballot_w64(near[i]);
-    pos[i] = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const bool unit = q[i] == 1.0;
+    packed[i] = near[i] && !unit;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(packed[i]);
+    pos[i] = unit ? kUnitSlot
+                  : base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     base += (uint32_t)__builtin_popcountll(m);
   }
+  asm volatile("" ::: "memory");
   if (base != 0) {
 #pragma unroll
     for (int i = 0; i < n; ++i)
-      if (near[i]) scratch[pos[i]] = q[i];
+      if (packed[i]) scratch[pos[i]] = q[i];
     asm volatile("" ::: "memory");
     for (uint32_t p = 0; p < base; p += 64) {
       const uint32_t idx = p + (uint32_t)lane;
       if (idx < base) scratch[idx] = ex::log_near1(scratch[idx]);
     }
     asm volatile("" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < n; ++i)
-      if (near[i]) E[i] = scratch[pos[i]];
-    asm volatile("" ::: "memory");
   }
+#pragma unroll
+  for (int i = 0; i < n; ++i)
+    if (near[i]) E[i] = scratch[pos[i]];
+  asm volatile("" ::: "memory");
   if (any_special) {
     LDPC_EX_COLD();
     ex::ratio_fix_n<n>(T, E);
