@@ -209,3 +209,36 @@ def test_ring_sessions_back_to_back():
             assert (ok[0].cpu().numpy() == ref["packed"]).all(), s
             assert (ok[1].cpu().numpy() == ref["iters"]).all(), s
     dec.close()
+
+
+@pytest.mark.parametrize("k", [2, 3, 5])
+@pytest.mark.parametrize("method", [0, 1])
+def test_ring_other_codes_vs_oracle(k, method):
+    """The reference's other H matrices (tests/golden/hData{2,3,5}.alist:
+    100 x 50, 16 x 8, 48 x 24): more than one column word (N = 100), and
+    packed outputs of 7 / 1 / 3 bytes, which the ring stores byte by byte
+    (the default H's 4 go as one 32-bit word)."""
+    from ldpc_ece535a import codes
+    from oracle import oracle as orc
+    M, N, rp, ci = codes.read_alist(os.path.join(os.path.dirname(__file__), "golden",
+                                                 "hData%d.alist" % k))
+    H = np.zeros((M, N), np.uint8)
+    for j in range(M):
+        H[j, ci[rp[j]:rp[j + 1]]] = 1
+    dec = L.Decoder(H)
+    Hr = orc.reorder_h(H)[0]
+    assert (dec.H == Hr).all()
+    y = frames(Hr, 3000, 2.0, 60 + k)
+    d_y = torch.from_numpy(y).cuda()
+    o = outs(dec, y.shape[0])
+    torch.cuda.synchronize()
+    dec.ring_begin(method=method, max_iters=50)
+    ids = [post(dec, d_y, o, lo, min(3000, lo + 1100)) for lo in range(0, 3000, 1100)]
+    dec.ring_wait(ids[-1])
+    dec.ring_end()
+    torch.cuda.synchronize()
+    ref = oracle(method, Hr, y)
+    assert (o[0].cpu().numpy() == ref["packed"]).all()
+    assert (o[1].cpu().numpy() == ref["iters"]).all()
+    assert (o[2].cpu().numpy() == ref["synd"]).all()
+    dec.close()
