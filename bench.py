@@ -960,7 +960,10 @@ def main():
             "workload": workload,
             "global_batch": args.batch * (1 if args.strong else world),
             "frames_per_gpu": B,
-            "batches_in_flight": D,
+            "distinct_input_batches": D,
+            "decoder": ("one launch per batch" if dvb else
+                        "frame ring (ldpc_ring_*): one persistent launch per timed region, "
+                        "frames of all posted batches from one queue"),
             "parallelism": "dp%d (independent frames)" % world,
             "mean_iters": round(mean_it, 3),
             "syndrome_fail_frac": round(totals[3] / max(1.0, frames_all), 4),
