@@ -153,20 +153,19 @@ struct Math<1> {
 template <int n>
 __device__ __forceinline__ void log_ratio_n_packed(const double (&T)[n],
                                                    const ex::ExTab *tab, double (&E)[n],
-                                                   double *scratch, int lane) {
+                                                   double *scratch, int lane, uint32_t zero_at) {
   double q[n];
   // wave-uniform at once (a per-lane flag held across the loop below costs a
   // VGPR and two conversions per call)
   const bool any_special = ex::ratio_n<n>(T, q);  // wave-uniform
   // q = 1 exactly (T = +-0: every padding cell, the rows with a degree-1
   // column; or a tiny |T|) is glibc's log(1) = +0 without evaluating it: those
-  // lanes read the +0 in the last scratch slot instead of a packed result.
-  // They are half the near-1 operands of the headline workload, and without
-  // them 9 % rather than 60 % of wave-iterations need a second packed pass
-  // (tools/path_stats.py).  The packed ones fill [0, base), base <= 64 n - 1
-  // whenever a lane is unit, so the slot survives.
-  constexpr uint32_t kUnitSlot = 64 * n - 1;
-  if (lane == 0) scratch[kUnitSlot] = 0.0;
+  // lanes read a +0.0 the caller keeps at scratch[zero_at] (a zero cell,
+  // never written during a frame: one address, an LDS broadcast) instead of
+  // a packed result.  They are
+  // half the near-1 operands of the headline workload, and without them 9 %
+  // rather than 60 % of wave-iterations need a second packed pass
+  // (tools/path_stats.py).
   uint32_t pos[n];
   bool near[n], packed[n];
   uint32_t base = 0;  // wave-uniform
@@ -177,7 +176,7 @@ __device__ __forceinline__ void log_ratio_n_packed(const double (&T)[n],
     const bool unit = q[i] == 1.0;
     packed[i] = near[i] && !unit;
     const uint64_t m = __builtin_amdgcn_ballot_w64(packed[i]);
-    pos[i] = unit ? kUnitSlot
+    pos[i] = unit ? zero_at
                   : base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     base += (uint32_t)__builtin_popcountll(m);

@@ -314,7 +314,7 @@ __device__ __forceinline__ FrameResult decode_frame(const CodeView &code, const 
         // the products below consume them -- until the variable pass)
         Real Es[S];
         if constexpr (PREC == 0)
-          log_ratio_n_packed<S>(Ts, logtab, Es, tb, lane);
+          log_ratio_n_packed<S>(Ts, logtab, Es, tb, lane, (uint32_t)(L.ebd - L.tb));
         else
           Math<PREC>::template check_msg_n<S>(Ts, logtab, Es);
 #ifdef LDPC_PATH_STATS
@@ -618,7 +618,7 @@ __device__ __forceinline__ FrameResult decode_frame(const CodeView &code, const 
         }
         // tb is free from here to the next iteration's tanh stores
         if constexpr (PREC == 0)
-          log_ratio_n_packed<S>(Ts, logtab, Es, tb, lane);
+          log_ratio_n_packed<S>(Ts, logtab, Es, tb, lane, (uint32_t)(L.ebd - L.tb));
         else
           Math<PREC>::template check_msg_n<S>(Ts, logtab, Es);
 #pragma unroll
