@@ -184,6 +184,17 @@ struct RingArgs {
   uint64_t deadline;     // 100 MHz ticks without a posted batch before a wave leaves
   int max_iters, et_period;
 };
+// One returning atomic word serves ~88 claims per us (MI355X_MICROARCH.md,
+// dequeue): frames shorter than ~12 ns of the chip's time per frame (min-sum,
+// f32, the compact mode: ~48 us per 4 096-frame batch whatever the iteration
+// cap, tools/ring_probe.py ITERS=1..5) wait on the queue head and on their
+// batch's done counter, so those modes claim several frames at a time and
+// count them done together.  The exact sum-product (~43 frames per us) claims
+// one: a wave holding unstarted frames lengthens the session's tail.
+constexpr int kRingMaxClaim = 4;
+constexpr int ring_claim(int method, int prec) {
+  return method == 1 && (prec == 0 || prec == 2) ? 1 : kRingMaxClaim;
+}
 constexpr int kRingDoneStride = 64;  // u32 words between two slots' done counters
 constexpr int kRingXcds = 8;         // mirror / lock copies: one per XCD (its own L2)
 int launch_ring(const CodeView &code, const RingArgs &r, int method, int prec, int slots, int nw,

@@ -235,11 +235,34 @@ __global__ void __launch_bounds__(kThreads, MINB) ring_kernel(CodeView code, Rin
   Batch bt{};
   bt.q = r.cursor0;
   bt.start = bt.end = -1;
-  // wave w's first ticket is w; the queue hands out the ones after all the
-  // launch's waves (4 096 first claims on one counter at once took ~46 us:
-  // ~88 per us, MI355X_MICROARCH.md "dequeue")
+  // wave w's first claim is tickets [w c, w c + c) (c = ring_claim); the queue
+  // hands out the claims after all the launch's waves' (4 096 first claims
+  // on one counter at once took ~46 us: ~88 per us, MI355X_MICROARCH.md
+  // "dequeue")
+  constexpr int64_t c = ring_claim(METHOD, PREC);
   const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
-  int64_t t = r.ticket0 + (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  int64_t t = r.ticket0 + ((int64_t)blockIdx.x * kWavesPerBlock + wave) * c;
+  int64_t tend = t + c;  // end of the current claim
+  // frames decoded but not yet counted done: batch pend_q (B = pend_B), count
+  uint64_t pend_q = 0;
+  int pend_B = 0;
+  uint32_t pend_n = 0;
+  // counts the pending frames done (their stores drained first); the add that
+  // completes a batch resets its counter and signals the host
+  auto flush = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are out
+    if (lane == 0) {
+      uint32_t *dn = r.done + (pend_q % kRingSlots) * kRingDoneStride;
+      const uint32_t old = __hip_atomic_fetch_add((gu32 *)dn, pend_n, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      if (old + pend_n == (uint32_t)pend_B) {  // the batch's last frames: reset the slot, then signal
+        __hip_atomic_store((gu32 *)dn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sys_store(r.comp + (pend_q % kRingSlots), pend_q + 1);
+      }
+    }
+    pend_n = 0;
+  };
 #ifdef LDPC_TIMELINE
   const uint64_t t_wave0 = ticks();
 #endif
@@ -275,14 +298,16 @@ __global__ void __launch_bounds__(kThreads, MINB) ring_kernel(CodeView code, Rin
       fr = decode_frame<PREC, METHOD, S, NW, DCN, DVN, false, Real, false, false>(
           code, a, f, wt, tb, eb, rb, sb, lane, logtab, xin, colq, ppos);
     }
-    // the next ticket, claimed when this frame is done: a ticket claimed at
-    // the frame's start waited for the frame (up to 50 iterations), and at
-    // a session's end the last tickets sat with waves busy on long frames
-    // while the others had run out of work (tools/ring_timeline.py: the last
-    // frame started 90 us before the end, the queue emptied ~250 us before).
-    // The claim's round trip overlaps the output stores' drain below.
+    // the next claim, taken when the current one's last frame is done: a
+    // claim taken at a frame's start waited for the frame (up to 50
+    // iterations), and at a session's end the last tickets sat with waves
+    // busy on long frames while the others had run out of work
+    // (tools/ring_timeline.py: the last frame started 90 us before the end,
+    // the queue emptied ~250 us before).  The claim's round trip overlaps the
+    // output stores' drain below.
+    const bool last = c == 1 || t + 1 == tend;
     uint32_t nt = 0;
-    if (lane == 0) nt = atomicAdd(r.ticket, 1u);
+    if (last && lane == 0) nt = atomicAdd(r.ticket, (uint32_t)c);
     // outputs, write-through: packed bytes M.. (:207-219) as 32-bit words
     // where the layout allows, iterations, syndrome weight
     uint8_t *pk = bt.packed + f * KB;
@@ -299,16 +324,17 @@ __global__ void __launch_bounds__(kThreads, MINB) ring_kernel(CodeView code, Rin
       if (bt.iters) wt_store(bt.iters + f, (int32_t)fr.used);
       if (bt.synd) wt_store(bt.synd + f, (int32_t)fr.weight);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are out
-    if (lane == 0) {
-      uint32_t *dn = r.done + (bt.q % kRingSlots) * kRingDoneStride;
-      const uint32_t old = __hip_atomic_fetch_add((gu32 *)dn, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-      if (old + 1 == (uint32_t)bt.B) {  // the batch's last frame: reset the slot, then signal
-        __hip_atomic_store((gu32 *)dn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        sys_store(r.comp + (bt.q % kRingSlots), bt.q + 1);
-      }
+    // done counts: one add per claim and batch
+    if constexpr (c == 1) {
+      pend_q = bt.q;
+      pend_B = bt.B;
+      pend_n = 1;
+      flush();
+    } else {
+      if (pend_n && pend_q != bt.q) flush();
+      pend_q = bt.q;
+      pend_B = bt.B;
+      pend_n += 1;
     }
 #ifdef LDPC_TIMELINE
     {  // per ticket: wave start, frame start, decode start, frame end, wave id |
@@ -325,8 +351,22 @@ __global__ void __launch_bounds__(kThreads, MINB) ring_kernel(CodeView code, Rin
       }
     }
 #endif
-    t = r.ticket0 + nwaves + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)nt);
+    if (last) {
+      t = r.ticket0 + nwaves * c + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)nt);
+      tend = t + c;
+    } else {
+      t += 1;
+    }
+    // counted at the claim's end, or before the next ticket leaves the batch
+    // (locate may wait there for a batch not posted yet, and the host may be
+    // waiting for this one)
+    if constexpr (c > 1)
+      if (last || t >= bt.end) flush();
   }
+  // a claim cut short by the quit descriptor or the deadline: its decoded
+  // frames still count
+  if constexpr (c > 1)
+    if (pend_n) flush();
 }
 
 int cus_of(int dev) {
