@@ -1335,11 +1335,12 @@ int decode_device_impl(ldpc_ctx *ctx, int method, int max_iters, int et_period, 
   // (ldpc_kernels.hpp DecodeArgs::static_stride)
   a.static_stride = max_iters <= 10 ? 1 : 0;
   a.fair_cycles = ctx->fair_cycles;
+  uint32_t advance = 0;
   rc = ldpc::launch_decode(code_view(ctx), a, method, precision, ctx->slots, ctx->nw,
-                           ctx->waves_per_cu, ctx->schedule, st);
+                           ctx->waves_per_cu, ctx->schedule, st, &advance);
   if (rc == -2) return set_err(ctx, LDPC_EUNSUPPORTED, "no kernel for this code shape");
   if (rc != 0) return hip_err(ctx, hipGetLastError(), "kernel launch");
-  if (!a.static_stride) ctx->queues[q].base += (uint32_t)B;  // the launch adds exactly B to its counter
+  ctx->queues[q].base += advance;  // what the launch adds to its counter (B with one frame per claim)
   return LDPC_OK;
 }
 

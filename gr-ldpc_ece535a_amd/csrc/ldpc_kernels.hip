@@ -65,8 +65,11 @@ __global__ void __launch_bounds__(kThreads, MINB)
   __shared__ typename Math<PREC>::Tab logtab[TabLds<PREC>::kN];
   if constexpr (METHOD == 1) stage_tab<PREC>(logtab);
 
-  int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-  if (b >= a.waves || b >= a.B) return;
+  const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const int64_t c = a.claim;  // frames per claim (1 with static_stride)
+  int64_t b = w * c;
+  if (w >= a.waves || b >= a.B) return;
+  int64_t bend = b + c;  // end of the wave's current claim
 
   // the wave's view of the code, in registers
   WaveTables<S, NW> wt;
@@ -142,7 +145,7 @@ __global__ void __launch_bounds__(kThreads, MINB)
   // after the first frame, when the loads have long completed
   float pf[NW];
   {
-    int64_t pb = (int64_t)a.waves + b;
+    int64_t pb = (int64_t)a.waves * c + b;
     pb = pb < a.B ? pb : b;
     float ppol;
     const float *ps = frame_src(a, pb, ppol);
@@ -199,10 +202,12 @@ __global__ void __launch_bounds__(kThreads, MINB)
 #endif
     if (a.static_stride) {
       b += a.waves;
-    } else {
+    } else if (++b == bend || b >= a.B) {
+      // the claim is used up (or cut by the batch's end): the next one
       uint32_t t = 0;
-      if (lane == 0) t = atomicAdd(a.ticket, 1u) - a.ticket_base;
-      b = (int64_t)a.waves + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
+      if (lane == 0) t = atomicAdd(a.ticket, (uint32_t)c) - a.ticket_base;
+      b = (int64_t)a.waves * c + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
+      bend = b + c;
     }
   }
 }
@@ -392,8 +397,9 @@ static int launch_nw(const CodeView &code, const DecodeArgs &a, int method, int 
 }
 
 int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int prec, int slots,
-                  int nw, int waves_per_cu, int schedule, void *stream) {
+                  int nw, int waves_per_cu, int schedule, void *stream, uint32_t *advance_out) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  *advance_out = 0;
   if (args.B <= 0) return 0;
   DecodeArgs a = args;
   // CUs of the current device, looked up once per device
@@ -431,9 +437,19 @@ int launch_decode(const CodeView &code, const DecodeArgs &args, int method, int 
     const int64_t w = std::min<int64_t>((int64_t)a.B, (int64_t)waves_per_cu * cus);
     a.waves = (int)((w + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock);
   }
-  if (nw == 1) return launch_nw<1>(code, a, method, prec, slots, mw, st);
-  if (nw == 4) return launch_nw<4>(code, a, method, prec, slots, mw, st);
-  return -2;
+  // the one-wave kernel's fast modes claim several frames per queue add when
+  // the batch is several times the resident waves (one counter word serves
+  // ~88 adds per us: ring_claim, ldpc_kernels.hpp); smaller batches, the
+  // workgroup form and fixed strides take one (every wave's first claim
+  // starts at once: claims of several frames would serialise a small batch)
+  const int64_t waves_max = (int64_t)waves_per_cu * cus;
+  a.claim = mw || a.static_stride || a.B < 4 * waves_max ? 1 : ring_claim(method, prec);
+  if (nw != 1 && nw != 4) return -2;
+  const int rc = nw == 1 ? launch_nw<1>(code, a, method, prec, slots, mw, st)
+                         : launch_nw<4>(code, a, method, prec, slots, mw, st);
+  if (rc == 0 && !a.static_stride)
+    *advance_out = (uint32_t)(a.claim * ((a.B + a.claim - 1) / a.claim));
+  return rc;
 }
 
 }  // namespace ldpc

@@ -107,6 +107,11 @@ struct DecodeArgs {
   // issue-priority threshold in core clocks for waves whose last iteration
   // was slow (0: off); see decode_frame
   uint32_t fair_cycles;
+  // frames per queue claim of the one-wave kernel (set by launch_decode,
+  // ring_claim): wave w takes frames [w claim, (w + 1) claim), then claims
+  // `claim` frames at a time from waves * claim on; a launch then adds
+  // claim * ceil(B / claim) to its counter
+  int claim;
 };
 
 // ---------------------------------------------------------------------------
@@ -205,7 +210,9 @@ int launch_ring(const CodeView &code, const RingArgs &r, int method, int prec, i
 // slots = ceil(E/64); nw = 1 or 4 (hard-decision words).
 // waves_per_cu (0 = default) sets the number of persistent waves;
 // schedule: 0 auto, 1 one wave per frame, 2 one multi-wave workgroup per frame.
+// *advance_out: what the launch adds to its queue counter (0 with static_stride).
 int launch_decode(const CodeView &code, const DecodeArgs &args, int method,
-                  int prec, int slots, int nw, int waves_per_cu, int schedule, void *stream);
+                  int prec, int slots, int nw, int waves_per_cu, int schedule, void *stream,
+                  uint32_t *advance_out);
 
 }  // namespace ldpc
