@@ -110,6 +110,71 @@ static void keyreads(const char *where, const uint64_t *p, uint64_t *out) {
   }
 }
 
+// The window server's poll: lane 0 reads the round word, lanes 1..63 key
+// slots 0..62, one load each; on a new round, stale slots (tag < round) are
+// read again until fresh.  hist[r]: rounds that needed r re-reads (r <= 3:
+// 3 or more).  The host writes the 63 keys, then the round word; the round
+// word sits 256 bytes before the keys (the server's layout) or in the word
+// right before them (the same 64-byte line as keys 0..6).
+__global__ void pollkeys(const uint64_t *round, const uint64_t *keys, uint64_t *reply, int n,
+                         uint64_t deadline) {
+  const int lane = threadIdx.x;
+  const uint64_t t0 = ticks();
+  uint64_t hist[4] = {0, 0, 0, 0}, tre = 0;
+  for (int i = 1; i <= n; ++i) {
+    uint64_t v;
+    for (;;) {
+      v = __hip_atomic_load(lane == 0 ? round : keys + lane - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (__builtin_amdgcn_readfirstlane((int)v) == i) break;
+      if (ticks() - t0 > deadline) {
+        if (lane == 0) __hip_atomic_store(reply, ~0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+    }
+    const uint64_t ts = ticks();
+    int r = 0;
+    while (__ballot(lane > 0 && v < (uint64_t)i)) {
+      if (lane > 0 && v < (uint64_t)i)
+        v = __hip_atomic_load(keys + lane - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ++r;
+    }
+    tre += ticks() - ts;
+    hist[r < 3 ? r : 3] += 1;
+    if (lane == 0) __hip_atomic_store(reply, (uint64_t)i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (lane == 0) {
+    for (int j = 0; j < 4; ++j) reply[4 + j] = hist[j];
+    reply[8] = tre;
+  }
+}
+
+static void pollkeys_run(const char *name, uint64_t *h_round, uint64_t *h_keys, const uint64_t *d_round,
+                         const uint64_t *d_keys, uint64_t *reply, int n) {
+  *(volatile uint64_t *)h_round = 0;
+  for (int j = 0; j < 63; ++j) h_keys[j] = 0;
+  reply[0] = 0;
+  hipLaunchKernelGGL(pollkeys, dim3(1), dim3(64), 0, 0, d_round, d_keys, reply, n, (uint64_t)100000000);
+  CHECK(hipGetLastError());
+  usleep(20000);
+  const auto t0 = std::chrono::steady_clock::now();
+  bool ok = true;
+  for (int i = 1; i <= n && ok; ++i) {
+    for (int j = 0; j < 63; ++j) __atomic_store_n(h_keys + j, (uint64_t)i, __ATOMIC_RELAXED);
+    __atomic_store_n(h_round, (uint64_t)i, __ATOMIC_RELEASE);
+    for (;;) {
+      const uint64_t v = __atomic_load_n(reply, __ATOMIC_ACQUIRE);
+      if (v == (uint64_t)i) break;
+      if (v == ~0ull) { ok = false; break; }
+    }
+  }
+  const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  CHECK(hipDeviceSynchronize());
+  if (!ok) { std::printf("%s: the kernel never saw a round\n", name); return; }
+  std::printf("%-40s %6.3f us per round; re-reads 0/1/2/3+: %llu %llu %llu %llu; %.2f us re-reading per round\n",
+              name, us / n, (unsigned long long)reply[4], (unsigned long long)reply[5],
+              (unsigned long long)reply[6], (unsigned long long)reply[7], reply[8] / 100.0 / n);
+}
+
 static void on_segv(int) {
   const char m[] = "CPU access to device memory faulted (no large BAR mapping)\n";
   ssize_t r = write(1, m, sizeof m - 1);
@@ -163,6 +228,8 @@ int main(int argc, char **argv) {
   CHECK(hipHostGetDevicePointer((void **)&hkeys_dev, hkeys, 0));
   for (int i = 0; i < 8192; ++i) hkeys[i] = i;
   keyreads("host memory  ", hkeys_dev, reply + 4);
+  pollkeys_run("poll: round word 256 B before the keys", hkeys, hkeys + 32, hkeys_dev, hkeys_dev + 32, reply, n);
+  pollkeys_run("poll: round word in the keys' line", hkeys + 64, hkeys + 65, hkeys_dev + 64, hkeys_dev + 65, reply, n);
 
   uint64_t *dflag = nullptr;
   CHECK(hipExtMallocWithFlags((void **)&dflag, 4096, hipDeviceMallocFinegrained));
