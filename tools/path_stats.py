@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """How often the exact arithmetic's rare paths run in the headline workload
-(diagnostic).  Needs a library built with -DLDPC_PATH_STATS (ab/mkv.sh PS
+(diagnostic).  Needs a library built with -DLDPC_PATH_STATS (tools/mkv.sh PS
 -DLDPC_PATH_STATS; LDPC_PKG_DIR points at it).  Decodes K config-2 batches
 through one ring session and prints, per wave-iteration of the column-centric
 sum-product loop (csrc/ldpc_frame.hpp g_path_stats): the share where some
