@@ -12,6 +12,8 @@ Checked here, each through the C ABI (ldpc_ece535a.Decoder.ring_*):
     oldest batch), and batches of one frame;
   * an input buffer rewritten between two batches of one launch is read
     afresh;
+  * signed-zero, +-inf / NaN and extreme finite samples equal the oracle;
+  * the reference's other H matrices equal the oracle;
   * the errors of the API."""
 import os
 import time
@@ -241,4 +243,48 @@ def test_ring_other_codes_vs_oracle(k, method):
     assert (o[0].cpu().numpy() == ref["packed"]).all()
     assert (o[1].cpu().numpy() == ref["iters"]).all()
     assert (o[2].cpu().numpy() == ref["synd"]).all()
+    dec.close()
+
+
+@pytest.mark.parametrize("method", [0, 1])
+def test_ring_special_samples_vs_oracle(golden, method):
+    """The headline path on the samples the batch kernels' special-value tests
+    use: exact +0.0 / -0.0 samples (every kind of frame the signed-zero test
+    builds), +-inf / NaN samples (the select-based sum-product loop), and
+    finite amplitudes from 1e-40 to 1e30 (tanh saturating to +-1 inside
+    all-finite frames), posted as three batches of one session: bytes,
+    iterations and syndrome weights equal the oracle's."""
+    from oracle import oracle as orc
+    fd = golden("frames_default.npz")
+    rng = np.random.default_rng(2606)
+    base = np.concatenate([fd["db%d_llr" % db] for db in (0, 2, 4)]).astype(np.float32)
+    z = base.copy()
+    hit = rng.random(z.shape) < 0.25
+    sign = rng.random(z.shape) < 0.5
+    z[hit & sign] = 0.0
+    z[hit & ~sign] = -0.0
+    z[0] = 0.0
+    z[1] = -0.0
+    nf = fd["db2_llr"].astype(np.float32).copy()
+    for b in range(0, nf.shape[0], 3):
+        for _ in range(1 + b % 3):
+            nf[b, rng.integers(0, 64)] = rng.choice([np.inf, -np.inf, np.nan])
+    big = fd["db2_llr"].astype(np.float64)
+    ex = np.concatenate([big[:48] * a for a in (8.0, 1e3, 1e30, 1e-30, 1e-40)]).astype(np.float32)
+    y = np.ascontiguousarray(np.concatenate([z, nf, ex]))
+    dec = L.Decoder()
+    d_y = torch.from_numpy(y).cuda()
+    o = outs(dec, y.shape[0])
+    torch.cuda.synchronize()
+    dec.ring_begin(method=method, max_iters=30)
+    cuts = [0, z.shape[0], z.shape[0] + nf.shape[0], y.shape[0]]
+    ids = [post(dec, d_y, o, cuts[k], cuts[k + 1]) for k in range(3)]
+    dec.ring_wait(ids[-1])
+    dec.ring_end()
+    torch.cuda.synchronize()
+    ref = orc.decode_batch(method, dec.H, y, 30)
+    pk, it, sy = (t.cpu().numpy() for t in o)
+    assert (pk == ref["packed"]).all(axis=1).all(), np.flatnonzero((pk != ref["packed"]).any(axis=1))[:8]
+    np.testing.assert_array_equal(it, ref["iters"])
+    np.testing.assert_array_equal(sy, ref["synd"])
     dec.close()
