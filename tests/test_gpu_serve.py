@@ -177,3 +177,38 @@ def test_serve_epoch_limit_restarts_the_session():
     dec.serve_end()
     dec.close()
     assert max(seen) < SERVE_EPOCH_LIMIT and min(seen) < 16  # it restarted
+
+
+@pytest.mark.parametrize("method", [0, 1])
+def test_serve_special_samples_vs_oracle(method):
+    """Windows over a span holding exact +0.0 / -0.0 samples, +-inf / NaN
+    samples and amplitudes from 1e-38 to 1e30, both polarities, in rounds
+    of both decode forms (one window per workgroup, one per wave): packed
+    bytes and syndrome weights equal the oracle's decodes of the same
+    samples."""
+    dec = L.Decoder()
+    Hr = dec.H
+    s = _span(Hr, 400, 515 + method).astype(np.float64)
+    rng = np.random.default_rng(808)
+    n = s.size
+    z = rng.random(n) < 0.08
+    s[z & (rng.random(n) < 0.5)] = 0.0
+    s[z & (s != 0.0)] = -0.0
+    bad = rng.choice(n, size=40, replace=False)
+    s[bad] = rng.choice([np.inf, -np.inf, np.nan], size=bad.size)
+    seg = n // 8
+    s[seg:2 * seg] *= 1e30
+    s[2 * seg:3 * seg] *= 1e-38
+    s[3 * seg:4 * seg] *= 1e3
+    s = s.astype(np.float32)
+    dec.stage_span(s, max_windows=4096)
+    dec.serve_begin(method=method, max_iters=30, max_windows=4096)
+    rounds = [_windows(rng, m, s.size, dec.N) for m in (1, 200, 3000)]
+    got = [dec.serve_windows(w) for w in rounds]
+    dec.serve_end()
+    for w, g in zip(rounds, got):
+        ref = _oracle(method, Hr, s, w, 30)
+        bad_rows = np.flatnonzero((g["packed"] != ref["packed"]).any(axis=1))
+        assert bad_rows.size == 0, (w[bad_rows[:4]], bad_rows[:8])
+        assert (g["synd"] == ref["synd"]).all()
+    dec.close()
